@@ -1,0 +1,148 @@
+/* mazerl.h — C ABI of libmazerl.so, the MI355X-native batched maze environment.
+ *
+ * The reference (Fabri000/Maze-Solving-Agent-Gymnasium) has no FFI: its boundary is the Python
+ * gym.Env class API. This header is the drop-in boundary underneath that API:
+ * the Python classes in maze-solving-agent-gymnasium_amd/mazerl/ bind these entry points with
+ * ctypes (INTEGRATION.md shows the binding). Each entry point names the reference interface it
+ * replaces (file:line in the reference).
+ *
+ * Conventions
+ *   - Every call returns an int status: MZ_OK (0) or a negative MZ_E* code; mz_last_error()
+ *     returns the thread-local message of the last failure.
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream). Calls are async on it
+ *     unless documented as synchronous.
+ *   - Pointers named *_dev are device (HBM) pointers owned by the caller (e.g. torch tensors);
+ *     pointers named *_host are host pointers. The handle owns all per-instance env state.
+ *   - One handle per stream/thread; handles are not internally locked. Instances (envs) of a
+ *     handle are fully independent (no global mutable state, per-instance algorithm id).
+ *   - Grids are uint8, row-major, 0 = wall, 1 = floor, 2 = goal (lib/maze_generation.py:16).
+ *     Shapes must be square and odd (the reference raises IndexError for even N),
+ *     5 <= N <= MZ_MAX_DIM. Window (enrich) mode needs N >= 15 for euclidean mazes (Q7).
+ */
+#ifndef MAZERL_H
+#define MAZERL_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MZ_OK 0
+#define MZ_EINVAL (-1)       /* bad argument */
+#define MZ_EINVAL_SHAPE (-2) /* grid shape the reference cannot represent (even N, N<15 window) */
+#define MZ_EHIP (-3)         /* HIP runtime error */
+#define MZ_ENOMEM (-4)
+#define MZ_EALIGN (-5)       /* output pointer misaligned (window f32 needs 16 B) */
+
+#define MZ_MAX_DIM 127
+#define MZ_WINDOW 15
+#define MZ_WINDOW_BITS 675   /* 3 x 15 x 15 */
+#define MZ_WINDOW_WORDS 22   /* uint32 words per instance in window_bits (bits 675..703 zero) */
+
+/* algorithm ids (BaseMazeEnv.ALGORITHM strings, base_maze_env.py:17; maze_generation.py:24-30) */
+#define MZ_ALGO_RPRIM 0
+#define MZ_ALGO_DFS 1
+#define MZ_ALGO_PRIMKILL 2
+
+typedef struct mz_handle mz_handle;
+
+typedef struct {
+  int32_t num_envs;  /* B: independent env instances on this GPU */
+  int32_t max_dim;   /* storage pitch: every instance's N <= max_dim */
+  int32_t toroidal;  /* 0 euclidean (SimpleMazeEnv family), 1 toroidal (ToroidalMazeEnv family) */
+  int32_t enrich;    /* 1 = *Enrich* observation (3x15x15 window), 0 = plain obs */
+  int32_t device;    /* HIP device ordinal */
+  int32_t reserved[7];
+} mz_config;
+
+/* Per-step outputs; every pointer is a caller-owned device buffer and may be NULL (= not
+ * written). Reward dtype note: the reference returns Python floats/ints; reward64 carries the
+ * exact value, reward is its float32 rounding (what torch.tensor(batch.reward) holds). */
+typedef struct {
+  float* reward;          /* [B] */
+  double* reward64;       /* [B] */
+  uint8_t* terminated;    /* [B] */
+  uint8_t* truncated;     /* [B] */
+  int32_t* pos;           /* [B][2] agent (row, col)           obs["agent"] (plain) */
+  int32_t* best_dir;      /* [B][2] agent - best_next_cell     obs["best dir"] */
+  float* obs6;            /* [B][6] learner state vector concat(agent, target, best dir) as f32,
+                             enrich: agent/maze_shape, target/maze_shape (off_policy_trainer.py:156) */
+  uint32_t* window_bits;  /* [B][22] 675-bit 3x15x15 window, channel-major, LSB-first */
+  float* window;          /* [B][3][15][15] f32 obs["window"] (get_mask_tensor), 16 B aligned */
+  int32_t* done_idx;      /* [B] indices of instances whose step ended terminated|truncated */
+  int32_t* done_count;    /* [1] number of valid done_idx entries (caller zeroes it first) */
+} mz_step_out;
+
+typedef struct { /* host-side snapshot of one instance (mz_query) */
+  int32_t n, start_r, start_c, goal_r, goal_c, max_steps;
+  int32_t r, c, steps, invalid_streak, nmoves, last_action, done;
+} mz_env_info;
+
+const char* mz_last_error(void);
+int mz_device_count(int* n);
+
+/* Create / destroy a batch of B env instances on one GPU. */
+int mz_create(const mz_config* cfg, mz_handle** out);
+int mz_destroy(mz_handle* h);
+
+/* Import mazes bit-exactly (e.g. reference-generated fixtures) into instances env_ids_host[i]
+ * (NULL = 0..n-1). grids_host is [n][dim][dim]; start_goal_host is [n][4] (sr, sc, gr, gc).
+ * Builds the per-maze distance field / move tables, max_steps, and resets the instances.
+ * Replaces: env construction with a given maze (SimpleMazeEnv.__init__, simple_maze_env.py:19-36)
+ * and set_max_steps (:52-58). Synchronous. */
+int mz_load_mazes(mz_handle* h, const uint8_t* grids_host, int32_t dim,
+                  const int32_t* start_goal_host, const int32_t* env_ids_host, int32_t n,
+                  void* stream);
+
+/* Generate new mazes on the GPU for the listed instances (env_ids_dev NULL = all B) with the
+ * per-instance algorithm ids (algo_dev [n] or NULL = algo_all) and Philox seeds
+ * seed + env_id; then builds tables and resets them. Replaces gen_maze / gen_maze_no_border
+ * (maze_generation.py:6-56) + update_new_maze (simple_maze_env.py:118-127) with candidates=1
+ * (best-of-6 difficulty selection, base_maze_env.py:78-97, is not applied — documented). */
+int mz_generate(mz_handle* h, const int32_t* env_ids_dev, int32_t n, const uint8_t* algo_dev,
+                int32_t algo_all, int32_t dim, uint64_t seed, void* stream);
+
+/* Reset every instance / a device list of instances (e.g. step's done_idx/done_count) and
+ * write their reset observations into `out`. Replaces BaseMazeEnv.reset (base_maze_env.py:136-161).
+ * With regen_won != 0, listed instances whose last step terminated get a freshly generated maze
+ * first (the trainer's win -> update_maze protocol, off_policy_trainer.py:190-202), using their
+ * stored algorithm id and seed + env_id + (epoch << 32). */
+int mz_reset_all(mz_handle* h, const mz_step_out* out, void* stream);
+int mz_reset_list(mz_handle* h, const int32_t* idx_dev, const int32_t* count_dev,
+                  int32_t max_count, int32_t regen_won, uint64_t seed, uint32_t epoch,
+                  const mz_step_out* out, void* stream);
+
+/* One env step for all B instances. actions_dev: [B] int32 in 0..3 (BaseMazeEnv.ACTIONS);
+ * a negative action means "observe only": no transition, outputs = observation of the current
+ * state with reward 0 and terminated = truncated = 0 (used to step a subset of instances).
+ * Replaces BaseMazeEnv.step (base_maze_env.py:163-210) with the move rule of
+ * maze_view.move_agent (maze_view.py:167-197) and _get_obs/_find_best_next_cell (:116-122,
+ * :224-262) / the Enrich window (maze_handler.py:4-99). */
+int mz_step(mz_handle* h, const int32_t* actions_dev, const mz_step_out* out, void* stream);
+
+/* get_mask_direction(probs) for all instances: out4_dev [B][4] f32
+ * (simple_maze_env.py:41-50, toroidal_maze_env.py:57-69). */
+int mz_direction_mask(mz_handle* h, int32_t probs, float* out4_dev, void* stream);
+
+/* Fused epsilon-greedy act (dqn_agent.py:104-116): for instance i, with u ~ U[0,1)
+ * (Philox(seed, i, counter)), if u < eps[i] (eps_dev NULL = eps_all) sample from the
+ * normalised get_mask_direction(probs=True) distribution, else take greedy_dev[i]
+ * (NULL = always explore). Writes actions_dev [B] int32. */
+int mz_act(mz_handle* h, const float* eps_dev, float eps_all, const int64_t* greedy_dev,
+           uint64_t seed, uint64_t counter, int32_t* actions_dev, void* stream);
+
+/* Expand n packed windows (window_bits layout) to f32 [n][3][15][15]. */
+int mz_expand_window(const uint32_t* bits_dev, float* out_dev, int32_t n, void* stream);
+
+/* Set the per-instance algorithm ids used by regeneration (BaseMazeEnv.ALGORITHM is global in
+ * the reference, base_maze_env.py:17,60-64; here it is per instance). algo_dev [B] or NULL. */
+int mz_set_algorithm(mz_handle* h, const uint8_t* algo_dev, int32_t algo_all, void* stream);
+
+/* Synchronous host snapshots for the single-env drop-in classes. */
+int mz_query(mz_handle* h, int32_t env, mz_env_info* info_host);
+int mz_get_grid(mz_handle* h, int32_t env, uint8_t* grid_host /* [n][n] */);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,326 @@
+// mz_api.hip — host side of the C ABI declared in include/mazerl.h.
+//
+// Owns the per-handle HBM state (layout: mz_common.h), validates arguments the way the
+// reference fails (even N -> IndexError, window with N < 15 -> crash: reported as
+// MZ_EINVAL_SHAPE), builds the exact penalty tables once (glibc exp, like CPython's math.exp),
+// and launches the kernels of mz_env.hip. No compute path runs on the host: every env quantity is
+// produced by a gfx950 kernel.
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mazerl.h"
+#include "mz_common.h"
+#include "mz_kernels.h"
+
+struct mz_handle {
+  mz_config cfg;
+  MzDev d;
+  std::vector<void*> allocs;
+  uint8_t* staging = nullptr;
+  size_t staging_bytes = 0;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define MZ_HIP(x)                                                                      \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess) return fail(MZ_EHIP, "%s: %s", #x, hipGetErrorString(e_));   \
+  } while (0)
+
+struct DeviceGuard {  // run a call on the handle's device, restore the caller's afterwards
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+MzOut to_dev(const mz_step_out* o) {
+  MzOut m;
+  std::memset(&m, 0, sizeof m);
+  if (!o) return m;
+  m.reward = o->reward; m.reward64 = o->reward64; m.terminated = o->terminated;
+  m.truncated = o->truncated; m.pos = o->pos; m.best_dir = o->best_dir; m.obs6 = o->obs6;
+  m.window_bits = o->window_bits; m.window = o->window; m.done_idx = o->done_idx;
+  m.done_count = o->done_count;
+  return m;
+}
+
+int check_out(const mz_step_out* o) {
+  if (o && o->window && (reinterpret_cast<uintptr_t>(o->window) & 15u))
+    return fail(MZ_EALIGN, "window output must be 16-byte aligned");
+  if (o && o->done_idx && !o->done_count) return fail(MZ_EINVAL, "done_idx needs done_count");
+  return MZ_OK;
+}
+
+int check_dim(const mz_handle* h, int dim) {
+  if (dim < 5 || dim > h->cfg.max_dim)
+    return fail(MZ_EINVAL_SHAPE, "maze dim %d outside [5, max_dim=%d]", dim, h->cfg.max_dim);
+  if ((dim & 1) == 0)
+    return fail(MZ_EINVAL_SHAPE, "even maze dim %d (reference gen_maze raises IndexError, "
+                "lib/maze_generation.py:197-203)", dim);
+  if (h->cfg.enrich && !h->cfg.toroidal && dim < 15)
+    return fail(MZ_EINVAL_SHAPE, "euclidean window needs dim >= 15 (extract_submaze, "
+                "lib/maze_handler.py:18-45)");
+  return MZ_OK;
+}
+
+template <typename T>
+int alloc(mz_handle* h, T** p, size_t count) {
+  void* q = nullptr;
+  hipError_t e = hipMalloc(&q, count * sizeof(T) + 64);
+  if (e != hipSuccess) return fail(MZ_ENOMEM, "hipMalloc(%zu): %s", count * sizeof(T), hipGetErrorString(e));
+  h->allocs.push_back(q);
+  MZ_HIP(hipMemset(q, 0, count * sizeof(T) + 64));
+  *p = static_cast<T*>(q);
+  return MZ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* mz_last_error(void) { return g_err.c_str(); }
+
+int mz_device_count(int* n) {
+  if (!n) return fail(MZ_EINVAL, "null");
+  MZ_HIP(hipGetDeviceCount(n));
+  return MZ_OK;
+}
+
+int mz_create(const mz_config* cfg, mz_handle** out) {
+  if (!cfg || !out) return fail(MZ_EINVAL, "null argument");
+  if (cfg->num_envs < 1) return fail(MZ_EINVAL, "num_envs must be >= 1");
+  if (cfg->max_dim < 5 || cfg->max_dim > MZ_MAX_DIM)
+    return fail(MZ_EINVAL_SHAPE, "max_dim %d outside [5, %d]", cfg->max_dim, MZ_MAX_DIM);
+  int ndev = 0;
+  MZ_HIP(hipGetDeviceCount(&ndev));
+  if (cfg->device < 0 || cfg->device >= ndev)
+    return fail(MZ_EINVAL, "device %d not present (%d HIP devices)", cfg->device, ndev);
+  DeviceGuard g(cfg->device);
+  mz_handle* h = new mz_handle();
+  h->cfg = *cfg;
+  MzDev& d = h->d;
+  d.B = cfg->num_envs;
+  d.P = cfg->max_dim;
+  d.VP = (d.P * d.P + 15) & ~15;
+  d.toroidal = cfg->toroidal != 0;
+  d.enrich = cfg->enrich != 0;
+  const size_t B = (size_t)d.B, P = (size_t)d.P;
+  int rc;
+  if ((rc = alloc(h, &d.cells, B * P * P)) || (rc = alloc(h, &d.planes, B * P * MZ_PLANE_WORDS + 16)) ||
+      (rc = alloc(h, &d.visits, B * (size_t)d.VP)) || (rc = alloc(h, &d.meta0, B)) ||
+      (rc = alloc(h, &d.meta1, B)) || (rc = alloc(h, &d.posw, B)) || (rc = alloc(h, &d.stw, B)) ||
+      (rc = alloc(h, &d.curw, B)) || (rc = alloc(h, &d.algo, B)) || (rc = alloc(h, &d.last_term, B))) {
+    mz_destroy(h);
+    return rc;
+  }
+  // exact penalty tables, built with the same libm exp as CPython's math.exp
+  double pen[512];
+  for (int k = 0; k < 256; ++k) {
+    volatile double ev = std::exp(-0.2 * (double)k);
+    volatile double ei = std::exp(-0.15 * (double)k);
+    pen[k] = 0.0 - (1.0 - ev);
+    pen[256 + k] = 0.0 - (1.0 - ei);
+  }
+  double* dpen = nullptr;
+  if ((rc = alloc(h, &dpen, 512))) { mz_destroy(h); return rc; }
+  hipError_t e = hipMemcpy(dpen, pen, sizeof pen, hipMemcpyHostToDevice);
+  if (e != hipSuccess) { mz_destroy(h); return fail(MZ_EHIP, "%s", hipGetErrorString(e)); }
+  d.pen_visit = dpen;
+  d.pen_inv = dpen + 256;
+  *out = h;
+  return MZ_OK;
+}
+
+int mz_destroy(mz_handle* h) {
+  if (!h) return MZ_OK;
+  DeviceGuard g(h->cfg.device);
+  (void)hipDeviceSynchronize();
+  for (void* p : h->allocs) (void)hipFree(p);
+  if (h->staging) (void)hipFree(h->staging);
+  delete h;
+  return MZ_OK;
+}
+
+int mz_load_mazes(mz_handle* h, const uint8_t* grids_host, int32_t dim,
+                  const int32_t* sg_host, const int32_t* env_ids_host, int32_t n, void* stream) {
+  if (!h || !grids_host || !sg_host || n < 1) return fail(MZ_EINVAL, "bad arguments");
+  int rc = check_dim(h, dim);
+  if (rc) return rc;
+  const size_t cells = (size_t)dim * dim;
+  for (int i = 0; i < n; ++i) {
+    const int32_t* s = sg_host + 4 * i;
+    for (int k = 0; k < 4; ++k)
+      if (s[k] < 0 || s[k] >= dim) return fail(MZ_EINVAL, "maze %d: start/goal out of range", i);
+    const uint8_t* g = grids_host + i * cells;
+    for (size_t c = 0; c < cells; ++c)
+      if (g[c] > 2) return fail(MZ_EINVAL, "maze %d: grid value %d not in {0,1,2}", i, g[c]);
+    if (g[s[0] * dim + s[1]] == 0 || g[s[2] * dim + s[3]] != 2)
+      return fail(MZ_EINVAL, "maze %d: start must be open and goal must hold 2", i);
+    if (env_ids_host && (env_ids_host[i] < 0 || env_ids_host[i] >= h->d.B))
+      return fail(MZ_EINVAL, "env id %d out of range", env_ids_host[i]);
+  }
+  if (!env_ids_host && n > h->d.B) return fail(MZ_EINVAL, "n > num_envs");
+  DeviceGuard g(h->cfg.device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const size_t need = n * cells + 16 * (size_t)n + 4 * (size_t)n + 256;
+  if (need > h->staging_bytes) {
+    if (h->staging) MZ_HIP(hipFree(h->staging));
+    h->staging = nullptr;
+    MZ_HIP(hipMalloc(&h->staging, need));
+    h->staging_bytes = need;
+  }
+  uint8_t* dg = h->staging;
+  int32_t* dsg = reinterpret_cast<int32_t*>(h->staging + ((n * cells + 15) & ~(size_t)15));
+  int32_t* dids = dsg + 4 * n;
+  MZ_HIP(hipMemcpyAsync(dg, grids_host, n * cells, hipMemcpyHostToDevice, s));
+  MZ_HIP(hipMemcpyAsync(dsg, sg_host, 16 * (size_t)n, hipMemcpyHostToDevice, s));
+  if (env_ids_host) MZ_HIP(hipMemcpyAsync(dids, env_ids_host, 4 * (size_t)n, hipMemcpyHostToDevice, s));
+  MZ_HIP(mz_launch_build(h->d, env_ids_host ? dids : nullptr, n, false, nullptr, 0, dim, 0, dg, dsg, s));
+  MZ_HIP(hipStreamSynchronize(s));
+  return MZ_OK;
+}
+
+int mz_generate(mz_handle* h, const int32_t* env_ids_dev, int32_t n, const uint8_t* algo_dev,
+                int32_t algo_all, int32_t dim, uint64_t seed, void* stream) {
+  if (!h) return fail(MZ_EINVAL, "null handle");
+  if (!env_ids_dev) n = h->d.B;
+  if (n < 0 || n > h->d.B) return fail(MZ_EINVAL, "n out of range");
+  if (!algo_dev && (algo_all < 0 || algo_all > 2)) return fail(MZ_EINVAL, "algorithm id %d", algo_all);
+  int rc = check_dim(h, dim);
+  if (rc) return rc;
+  if (h->d.toroidal && dim + 2 > MZ_MAX_DIM + 2) return fail(MZ_EINVAL_SHAPE, "dim too large");
+  DeviceGuard g(h->cfg.device);
+  MZ_HIP(mz_launch_build(h->d, env_ids_dev, n, true, algo_dev, algo_all, dim, seed, nullptr,
+                         nullptr, static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
+int mz_reset_all(mz_handle* h, const mz_step_out* out, void* stream) {
+  if (!h) return fail(MZ_EINVAL, "null handle");
+  int rc = check_out(out);
+  if (rc) return rc;
+  DeviceGuard g(h->cfg.device);
+  MZ_HIP(mz_launch_reset_list(h->d, nullptr, nullptr, h->d.B, to_dev(out),
+                              static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
+int mz_reset_list(mz_handle* h, const int32_t* idx_dev, const int32_t* count_dev,
+                  int32_t max_count, int32_t regen_won, uint64_t seed, uint32_t epoch,
+                  const mz_step_out* out, void* stream) {
+  if (!h || !idx_dev) return fail(MZ_EINVAL, "bad arguments");
+  if (max_count < 0 || max_count > h->d.B) max_count = h->d.B;
+  int rc = check_out(out);
+  if (rc) return rc;
+  DeviceGuard g(h->cfg.device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (regen_won) MZ_HIP(mz_launch_regen(h->d, idx_dev, count_dev, max_count, seed, epoch, s));
+  MZ_HIP(mz_launch_reset_list(h->d, idx_dev, count_dev, max_count, to_dev(out), s));
+  return MZ_OK;
+}
+
+int mz_step(mz_handle* h, const int32_t* actions_dev, const mz_step_out* out, void* stream) {
+  if (!h || !actions_dev) return fail(MZ_EINVAL, "bad arguments");
+  int rc = check_out(out);
+  if (rc) return rc;
+  DeviceGuard g(h->cfg.device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (out && out->done_count) MZ_HIP(hipMemsetAsync(out->done_count, 0, sizeof(int32_t), s));
+  MZ_HIP(mz_launch_step(h->d, actions_dev, to_dev(out), s));
+  return MZ_OK;
+}
+
+int mz_direction_mask(mz_handle* h, int32_t probs, float* out4_dev, void* stream) {
+  if (!h || !out4_dev) return fail(MZ_EINVAL, "bad arguments");
+  if (reinterpret_cast<uintptr_t>(out4_dev) & 15u) return fail(MZ_EALIGN, "out4 must be 16-B aligned");
+  DeviceGuard g(h->cfg.device);
+  MZ_HIP(mz_launch_mask(h->d, probs, out4_dev, static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
+int mz_act(mz_handle* h, const float* eps_dev, float eps_all, const int64_t* greedy_dev,
+           uint64_t seed, uint64_t counter, int32_t* actions_dev, void* stream) {
+  if (!h || !actions_dev) return fail(MZ_EINVAL, "bad arguments");
+  DeviceGuard g(h->cfg.device);
+  MZ_HIP(mz_launch_act(h->d, eps_dev, eps_all, greedy_dev, seed, counter, actions_dev,
+                       static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
+int mz_expand_window(const uint32_t* bits_dev, float* out_dev, int32_t n, void* stream) {
+  if (!bits_dev || !out_dev || n < 0) return fail(MZ_EINVAL, "bad arguments");
+  MZ_HIP(mz_launch_expand(bits_dev, out_dev, n, static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
+int mz_set_algorithm(mz_handle* h, const uint8_t* algo_dev, int32_t algo_all, void* stream) {
+  if (!h) return fail(MZ_EINVAL, "null handle");
+  DeviceGuard g(h->cfg.device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (algo_dev) MZ_HIP(hipMemcpyAsync(h->d.algo, algo_dev, h->d.B, hipMemcpyDeviceToDevice, s));
+  else {
+    if (algo_all < 0 || algo_all > 2) return fail(MZ_EINVAL, "algorithm id %d", algo_all);
+    MZ_HIP(hipMemsetAsync(h->d.algo, algo_all, h->d.B, s));
+  }
+  return MZ_OK;
+}
+
+int mz_query(mz_handle* h, int32_t env, mz_env_info* info) {
+  if (!h || !info || env < 0 || env >= h->d.B) return fail(MZ_EINVAL, "bad arguments");
+  DeviceGuard g(h->cfg.device);
+  MZ_HIP(hipDeviceSynchronize());
+  uint32_t m0, m1, pw, sw;
+  MZ_HIP(hipMemcpy(&m0, h->d.meta0 + env, 4, hipMemcpyDeviceToHost));
+  MZ_HIP(hipMemcpy(&m1, h->d.meta1 + env, 4, hipMemcpyDeviceToHost));
+  MZ_HIP(hipMemcpy(&pw, h->d.posw + env, 4, hipMemcpyDeviceToHost));
+  MZ_HIP(hipMemcpy(&sw, h->d.stw + env, 4, hipMemcpyDeviceToHost));
+  info->n = m0 & 0xFF;
+  info->start_r = (m0 >> 16) & 0xFF; info->start_c = m0 >> 24;
+  info->goal_r = m1 & 0xFF; info->goal_c = (m1 >> 8) & 0xFF; info->max_steps = m1 >> 16;
+  info->r = pw & 0xFF; info->c = (pw >> 8) & 0xFF; info->nmoves = (pw >> 16) & 3;
+  info->last_action = (pw >> 18) & 3; info->done = (pw >> 20) & 1;
+  info->steps = sw & 0xFFFF; info->invalid_streak = (sw >> 16) & 0xFF;
+  return MZ_OK;
+}
+
+int mz_get_grid(mz_handle* h, int32_t env, uint8_t* grid_host) {
+  if (!h || !grid_host || env < 0 || env >= h->d.B) return fail(MZ_EINVAL, "bad arguments");
+  mz_env_info info;
+  int rc = mz_query(h, env, &info);
+  if (rc) return rc;
+  const int P = h->d.P, N = info.n;
+  std::vector<uint32_t> cw((size_t)P * P);
+  DeviceGuard g(h->cfg.device);
+  MZ_HIP(hipMemcpy(cw.data(), h->d.cells + (size_t)env * P * P, 4 * cw.size(), hipMemcpyDeviceToHost));
+  for (int r = 0; r < N; ++r)
+    for (int c = 0; c < N; ++c) {
+      const bool open = (cw[(size_t)r * P + c] & MZ_CELL_OPEN) != 0;
+      grid_host[r * N + c] = !open ? 0 : ((r == info.goal_r && c == info.goal_c) ? 2 : 1);
+    }
+  return MZ_OK;
+}
+
+}  // extern "C"

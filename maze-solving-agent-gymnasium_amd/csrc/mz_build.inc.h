@@ -1,0 +1,366 @@
+// mz_build.inc.h — per-maze build on gfx950 (one 64-lane wave per maze, state in LDS).
+// Included by mz_env.hip (one translation unit: the reset kernel regenerates mazes in place).
+//
+//   generation  random_prim_visit / deept_first_visit / prim_and_kill_visit
+//               (maze_generation.py:59-185) over a Philox stream; lane 0 runs the sequential
+//               carve loop, the prim&kill restart scan (:151) is wave-parallel.
+//   goal        find_random_position (:187-218): wave BFS from start + wave max-reduce
+//   toroidal    gen_maze_no_border (:37-56): generate (N+2)^2, pick goal, crop the border
+//   tables      BFS distance-to-goal field (replaces per-step A*, a_star.py:9-82), best-next
+//               code per cell (_find_best_next_cell base_maze_env.py:224-262), open-neighbour
+//               mask (get_direction_mask maze_handler.py:122-162), open bit-plane rows,
+//               max_steps (set_max_steps simple_maze_env.py:52-58), reset state.
+#pragma once
+#include "mz_common.h"
+
+struct MzBuildLds {
+  uint8_t* g;        // [G*G] grid
+  uint16_t* dist;    // [G*G]
+  uint16_t* queue;   // [G*G]
+  uint32_t* vis;     // [(G*G+31)/32]
+  int* sh;           // scalars
+};
+
+__host__ __device__ inline size_t mz_align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+__host__ __device__ inline size_t mz_build_lds_bytes(int P) {
+  const size_t G = (size_t)P + 2, C = G * G;
+  return 64 + mz_align16(C) + 2 * mz_align16(2 * C) + mz_align16(4 * ((C + 31) / 32));
+}
+
+__device__ inline MzBuildLds mz_build_lds(uint8_t* base, int P) {
+  const size_t G = (size_t)P + 2, C = G * G;
+  MzBuildLds L;
+  L.sh = reinterpret_cast<int*>(base);
+  size_t off = 64;
+  L.g = base + off; off += mz_align16(C);
+  L.dist = reinterpret_cast<uint16_t*>(base + off); off += mz_align16(2 * C);
+  L.queue = reinterpret_cast<uint16_t*>(base + off); off += mz_align16(2 * C);
+  L.vis = reinterpret_cast<uint32_t*>(base + off);
+  return L;
+}
+
+// Level-synchronous wave BFS over open cells of the G x G grid from src (wrap if tor).
+__device__ void mz_wave_bfs(const MzBuildLds& L, int G, bool tor, int src) {
+  const int lane = threadIdx.x, C = G * G;
+  for (int i = lane; i < C; i += 64) L.dist[i] = 0xFFFF;
+  for (int i = lane; i < (C + 31) / 32; i += 64) L.vis[i] = 0u;
+  __syncthreads();
+  if (lane == 0) {
+    L.dist[src] = 0;
+    L.queue[0] = (uint16_t)src;
+    L.vis[src >> 5] |= 1u << (src & 31);
+    L.sh[0] = 1;
+  }
+  __syncthreads();
+  int head = 0, tail = 1;
+  while (head < tail) {
+    for (int base = head; base < tail; base += 64) {
+      const int i = base + lane;
+      if (i < tail) {
+        const int v = L.queue[i], dv = L.dist[v], r = v / G, c = v - r * G;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          int nr = r + mz_dr(k), nc = c + mz_dc(k);
+          if (tor) { nr = mz_wrap(nr, G); nc = mz_wrap(nc, G); }
+          else if (nr < 0 || nr >= G || nc < 0 || nc >= G) continue;
+          const int n = nr * G + nc;
+          if (L.g[n] == 0) continue;
+          const uint32_t bit = 1u << (n & 31);
+          if (atomicOr(&L.vis[n >> 5], bit) & bit) continue;
+          L.dist[n] = (uint16_t)(dv + 1);
+          L.queue[atomicAdd(&L.sh[0], 1)] = (uint16_t)n;
+        }
+      }
+    }
+    __syncthreads();
+    head = tail;
+    tail = L.sh[0];
+    __syncthreads();
+  }
+}
+
+// --- generators (lane 0 unless noted); G = generation grid size (odd) ------------------------
+// neighbour order of get_neighbors / random_walk: (-2,0),(2,0),(0,-2),(0,2) (maze_generation.py:72)
+__device__ inline int mz_g2r(int k) { return k == 0 ? -2 : (k == 1 ? 2 : 0); }
+__device__ inline int mz_g2c(int k) { return k == 2 ? -2 : (k == 3 ? 2 : 0); }
+// direction order of deept_first_visit: (0,-1),(0,1),(-1,0),(1,0) (maze_generation.py:114)
+__device__ inline int mz_fr(int k) { return k == 2 ? -1 : (k == 3 ? 1 : 0); }
+__device__ inline int mz_fc(int k) { return k == 0 ? -1 : (k == 1 ? 1 : 0); }
+
+__device__ void mz_gen_rprim(const MzBuildLds& L, int G, int s, MzRng& rng) {
+  uint8_t* m = L.g;
+  uint16_t* fr = L.queue;
+  uint32_t* inF = L.vis;
+  for (int i = 0; i < (G * G + 31) / 32; ++i) inF[i] = 0u;
+  int nf = 0;
+  const int sr = s / G, sc = s - sr * G;
+  m[s] = 1;
+  for (int k = 0; k < 4; ++k) {
+    int r = sr + mz_g2r(k), c = sc + mz_g2c(k);
+    if (r < 0 || r >= G || c < 0 || c >= G) continue;
+    int j = r * G + c;
+    fr[nf++] = (uint16_t)j; inF[j >> 5] |= 1u << (j & 31);
+  }
+  while (nf > 0) {
+    const int i = (int)rng.below((uint32_t)nf);
+    const int f = fr[i];
+    fr[i] = fr[--nf];
+    const int fx = f / G, fy = f - fx * G;
+    int nb[4], cnt = 0;
+    for (int k = 0; k < 4; ++k) {
+      int r = fx + mz_g2r(k), c = fy + mz_g2c(k);
+      if (r < 0 || r >= G || c < 0 || c >= G) continue;
+      if (m[r * G + c] == 1) nb[cnt++] = r * G + c;
+    }
+    if (cnt) {
+      const int nn = nb[rng.below((uint32_t)cnt)];
+      const int nx = nn / G, ny = nn - nx * G;
+      m[f] = 1;
+      m[((fx + nx) / 2) * G + (fy + ny) / 2] = 1;
+      for (int k = 0; k < 4; ++k) {
+        int r = fx + mz_g2r(k), c = fy + mz_g2c(k);
+        if (r < 0 || r >= G || c < 0 || c >= G) continue;
+        int j = r * G + c;
+        if (m[j] == 0 && !((inF[j >> 5] >> (j & 31)) & 1u)) {
+          fr[nf++] = (uint16_t)j; inF[j >> 5] |= 1u << (j & 31);
+        }
+      }
+    }
+  }
+}
+
+__device__ void mz_gen_dfs(const MzBuildLds& L, int G, int s, MzRng& rng) {
+  uint8_t* m = L.g;
+  uint16_t* st = L.queue;
+  int sp = 0;
+  st[sp++] = (uint16_t)s;
+  while (sp > 0) {
+    const int top = st[sp - 1], x = top / G, y = top - x * G;
+    int cand[4], cnt = 0;
+    for (int k = 0; k < 4; ++k) {
+      int nx = x + 2 * mz_fr(k), ny = y + 2 * mz_fc(k);
+      if (nx >= 0 && nx < G && ny >= 0 && ny < G && m[nx * G + ny] == 0) cand[cnt++] = k;
+    }
+    if (!cnt) { --sp; continue; }
+    const int k = cand[rng.below((uint32_t)cnt)];
+    m[(x + mz_fr(k)) * G + (y + mz_fc(k))] = 1;
+    const int nx = x + 2 * mz_fr(k), ny = y + 2 * mz_fc(k);
+    m[nx * G + ny] = 1;
+    st[sp++] = (uint16_t)(nx * G + ny);
+  }
+}
+
+// prim&kill marks kept in L.dist: 0 = not a cell, 1 = unmarked, 2 = marked
+__device__ inline int mz_pk_nbrs(const uint16_t* mk, int G, int p, int* out) {
+  const int x = p / G, y = p - x * G;
+  int cnt = 0;
+  for (int k = 0; k < 4; ++k) {
+    int r = x + mz_g2r(k), c = y + mz_g2c(k);
+    if (r < 0 || r >= G || c < 0 || c >= G) continue;
+    if (mk[r * G + c] == 1) out[cnt++] = r * G + c;
+  }
+  return cnt;
+}
+
+__device__ void mz_pk_walk(const MzBuildLds& L, int G, int cur, MzRng& rng) {
+  int nb[4], cnt;
+  while ((cnt = mz_pk_nbrs(L.dist, G, cur, nb)) != 0) {
+    const int nx = nb[rng.below((uint32_t)cnt)];
+    const int cx = cur / G, cy = cur - cx * G, x = nx / G, y = nx - x * G;
+    L.g[(cx + (x - cx) / 2) * G + (cy + (y - cy) / 2)] = 1;
+    cur = nx;
+    L.dist[cur] = 2;
+    L.sh[1] -= 1;
+  }
+}
+
+// wave-cooperative; rng lives in lane 0
+__device__ void mz_gen_primkill(const MzBuildLds& L, int G, int s, MzRng& rng) {
+  const int lane = threadIdx.x, C = G * G;
+  for (int p = lane; p < C; p += 64) {
+    const int r = p / G, c = p - r * G;
+    const bool cell = (r & 1) && (c & 1) && r < G && c < G;
+    L.dist[p] = cell ? 1 : 0;
+    if (cell) L.g[p] = 1;
+  }
+  __syncthreads();
+  if (lane == 0) {
+    int cells = ((G - 1) / 2) * ((G - 1) / 2);
+    L.dist[s] = 2;
+    L.sh[1] = cells - 1;  // unmarked count
+    mz_pk_walk(L, G, s, rng);
+  }
+  __syncthreads();
+  while (L.sh[1] > 0) {
+    // marked cells with >= 1 unmarked neighbour, row-major (maze_generation.py:151)
+    int total = 0;
+    for (int b = 0; b < C; b += 64) {
+      const int p = b + lane;
+      int tmp[4];
+      const bool cand = p < C && L.dist[p] == 2 && mz_pk_nbrs(L.dist, G, p, tmp) > 0;
+      total += __popcll(__ballot(cand));
+    }
+    int k = 0;
+    if (lane == 0) k = (int)rng.below((uint32_t)total);
+    k = __shfl(k, 0);
+    int chosen = -1;
+    for (int b = 0; b < C && chosen < 0; b += 64) {
+      const int p = b + lane;
+      int tmp[4];
+      const bool cand = p < C && L.dist[p] == 2 && mz_pk_nbrs(L.dist, G, p, tmp) > 0;
+      unsigned long long bal = __ballot(cand);
+      const int pc = __popcll(bal);
+      if (k < pc) {
+        for (int t = 0; t < k; ++t) bal &= bal - 1;  // drop the k lowest set bits
+        chosen = b + __ffsll((long long)bal) - 1;
+      } else {
+        k -= pc;
+      }
+    }
+    __syncthreads();
+    if (chosen < 0) break;  // unreachable for a connected cell grid; never walk from -1
+    if (lane == 0) mz_pk_walk(L, G, chosen, rng);
+    __syncthreads();
+  }
+}
+
+// find_random_position (maze_generation.py:187-218) on the euclidean G x G grid
+__device__ int mz_goal_select(const MzBuildLds& L, int G, int s) {
+  mz_wave_bfs(L, G, false, s);
+  const int lane = threadIdx.x, C = G * G;
+  uint32_t best = 0;  // (dist << 16) | (0xFFFF - idx); 0 = none
+  for (int p = lane; p < C; p += 64) {
+    const int r = p / G, c = p - r * G;
+    if (!(r & 1) || !(c & 1) || L.g[p] != 1 || p == s || r + 1 >= G || c + 1 >= G) continue;
+    const int nb = (L.g[p - G] != 0) + (L.g[p + G] != 0) + (L.g[p - 1] != 0) + (L.g[p + 1] != 0);
+    if (nb != 1) continue;
+    const uint32_t key = ((uint32_t)(L.dist[p] + 1) << 16) | (uint32_t)(0xFFFF - p);
+    best = key > best ? key : best;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t x = __shfl_xor(best, o);
+    best = x > best ? x : best;
+  }
+  return best ? (int)(0xFFFF - (best & 0xFFFF)) : -1;
+}
+
+// Cell word of open cell (r,c) of the final N x N maze in L.g with distance field L.dist.
+__device__ inline uint32_t mz_cell_word(const MzBuildLds& L, int N, bool tor, int r, int c,
+                                        int gr, int gc) {
+  const int M = 2 * N;  // best-dir A* depth 2*min(H,W) (base_maze_env.py:244)
+  const uint32_t D = L.dist[r * N + c];
+  uint32_t nbm = 0u;
+  int code = 4;
+  double best = __longlong_as_double(0x7FF0000000000000ll);  // +inf
+  for (int k = 0; k < 4; ++k) {
+    // get_direction_mask / get_toroidal_direction_mask (maze_handler.py:122-162)
+    const int mr = mz_wrap(r + mz_dr(k), N), mc = mz_wrap(c + mz_dc(k), N);
+    if (L.g[mr * N + mc] != 0) nbm |= 1u << k;
+  }
+  for (int k = 0; k < 4; ++k) {  // _find_best_next_cell (base_maze_env.py:237-260)
+    int nr = r + mz_dr(k), nc = c + mz_dc(k);
+    bool valid;
+    if (tor) { nr = mz_wrap(nr, N); nc = mz_wrap(nc, N); valid = L.g[nr * N + nc] != 0; }
+    else valid = 0 < nr && nr < N && 0 < nc && nc < N && L.g[nr * N + nc] != 0;
+    if (!valid) continue;
+    const int dn = L.dist[nr * N + nc];
+    const int len = (dn < M ? dn : M) + 1;
+    const int manh = abs(nr - gr) + abs(nc - gc);
+    const double score = __dadd_rn((double)len, __dmul_rn(0.15, (double)manh));
+    if (score < best) { best = score; code = k; }
+    if (nr == gr && nc == gc) { code = k; break; }
+  }
+  return D | ((uint32_t)code << MZ_CELL_CODE_SHIFT) | MZ_CELL_OPEN | (nbm << MZ_CELL_NB_SHIFT);
+}
+
+// Builds maze + tables of instance e and resets it. generate: Philox generation with algo/seed;
+// else import grid_src [N][N] with (sr,sc,gr,gc). Returns via d.meta*: all lanes must call.
+__device__ void mz_build_one(const MzDev& d, int e, bool tor, bool generate, int algo,
+                             uint64_t seed, int N, const uint8_t* grid_src, int isr, int isc,
+                             int igr, int igc, uint8_t* lds) {
+  const int lane = threadIdx.x;
+  const MzBuildLds L = mz_build_lds(lds, d.P);
+  int sr, sc, gr, gc;
+  if (generate) {
+    const int G = tor ? N + 2 : N;
+    for (int i = lane; i < G * G; i += 64) L.g[i] = 0;
+    __syncthreads();
+    MzRng rng{seed, 0ull, {0u, 0u, 0u, 0u}};
+    int s = 0;
+    if (lane == 0) {
+      // start = (randrange(1, G-1, 2), randrange(1, G-1, 2)) (maze_generation.py:21)
+      const int a = 1 + 2 * (int)rng.below((uint32_t)((G - 1) / 2));
+      const int b = 1 + 2 * (int)rng.below((uint32_t)((G - 1) / 2));
+      s = a * G + b;
+      L.g[s] = 1;
+      L.sh[2] = s;
+      if (algo == MZ_ALGO_RPRIM_DEV) mz_gen_rprim(L, G, s, rng);
+      else if (algo == MZ_ALGO_DFS_DEV) mz_gen_dfs(L, G, s, rng);
+    }
+    __syncthreads();
+    s = L.sh[2];
+    if (algo != MZ_ALGO_RPRIM_DEV && algo != MZ_ALGO_DFS_DEV) mz_gen_primkill(L, G, s, rng);
+    __syncthreads();
+    int goal = mz_goal_select(L, G, s);
+    if (goal < 0) goal = s;  // unreachable for G >= 5 (a spanning tree has >= 2 leaves)
+    __syncthreads();
+    if (lane == 0) L.g[goal] = 2;
+    __syncthreads();
+    sr = s / G; sc = s - sr * G; gr = goal / G; gc = goal - gr * G;
+    if (tor) {  // crop the border (maze_generation.py:53-55)
+      for (int i = lane; i < N * N; i += 64) {
+        const int r = i / N, c = i - r * N;
+        L.dist[i] = L.g[(r + 1) * G + (c + 1)];
+      }
+      __syncthreads();
+      for (int i = lane; i < N * N; i += 64) L.g[i] = (uint8_t)L.dist[i];
+      __syncthreads();
+      sr -= 1; sc -= 1; gr -= 1; gc -= 1;
+    }
+  } else {
+    for (int i = lane; i < N * N; i += 64) L.g[i] = grid_src[i];
+    sr = isr; sc = isc; gr = igr; gc = igc;
+    __syncthreads();
+  }
+  // distance-to-goal field (len(find_path(p)) = D[p] + 1)
+  mz_wave_bfs(L, N, tor, gr * N + gc);
+  const size_t es = (size_t)e;
+  const int P = d.P;
+  for (int p = lane; p < P * P; p += 64) {
+    const int r = p / P, c = p - r * P;
+    const bool open = r < N && c < N && L.g[r * N + c] != 0;
+    d.cells[es * P * P + p] = open ? mz_cell_word(L, N, tor, r, c, gr, gc) : 0u;
+  }
+  // open / visited bit-plane rows; visited = {start} (reset)
+  for (int R = lane; R < P; R += 64) {
+    uint32_t w[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    if (R < N)
+      for (int c = 0; c < N; ++c)
+        if (L.g[R * N + c] != 0) w[c >> 5] |= 1u << (c & 31);
+    if (R == sr) w[4 + (sc >> 5)] |= 1u << (sc & 31);
+    uint4* row = reinterpret_cast<uint4*>(d.planes + (es * P + R) * MZ_PLANE_WORDS);
+    row[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    row[1] = make_uint4(w[4], w[5], w[6], w[7]);
+  }
+  uint4* v4 = reinterpret_cast<uint4*>(d.visits + es * d.VP);
+  for (int i = lane; i < d.VP / 16; i += 64) v4[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (lane == 0) {
+    // set_max_steps: ceil((((H-1)*(W-1)) - 1) * (len / CE)), CE = (H-1)*((W-1)//2) - 1
+    const int len = (int)L.dist[sr * N + sc] + 1;
+    const int ce = (N - 1) * ((N - 1) / 2) - 1;
+    const double Lf = __ddiv_rn((double)len, (double)ce);
+    const double prod = __dmul_rn((double)((N - 1) * (N - 1) - 1), Lf);
+    int maxs = (int)ceil(prod);
+    if (maxs > 65535) maxs = 65535;
+    d.meta0[e] = (uint32_t)N | ((uint32_t)N << 8) | ((uint32_t)sr << 16) | ((uint32_t)sc << 24);
+    d.meta1[e] = (uint32_t)gr | ((uint32_t)gc << 8) | ((uint32_t)maxs << 16);
+    d.posw[e] = (uint32_t)sr | ((uint32_t)sc << 8);
+    d.stw[e] = 0u;
+    d.last_term[e] = 0;
+  }
+  __syncthreads();
+  // curw = cells word at start, from LDS (no read-back of global stores inside the launch)
+  if (lane == 0) d.curw[e] = mz_cell_word(L, N, tor, sr, sc, gr, gc);
+  __syncthreads();
+}

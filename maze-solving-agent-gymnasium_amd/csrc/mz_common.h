@@ -1,0 +1,107 @@
+// mz_common.h — shared layout + device helpers for the MI355X maze env (libmazerl.so).
+//
+// HBM layout (one handle = B env instances, pitch P = max_dim, planes padded to 128 bits/row):
+//   cells  u32 [B][P*P]  per-cell word:  D (bits 0-15, BFS distance to goal)
+//                                         | best-next code (16-18: action 0-3, 4 = stay)
+//                                         | open (19) | open-neighbour mask (20-23, per action)
+//                        Everything the reference recomputes with A* every step
+//                        (_find_best_next_cell base_maze_env.py:224-262, find_path
+//                        simple_maze_env.py:70-79) is a function of the cell: computed once per
+//                        maze, gathered once per step.
+//   planes u32 [B][P][8] words 0-3 = open bits of the row, words 4-7 = visited bits (the
+//                        reference's non_visited plane inverted, base_maze_env.py:40-41,184)
+//   visits u8  [B][VP]   entries into each cell since reset (visited_cell.count, :194),
+//                        saturating at 255 (exact: penalties are -1.0 for k >= 188)
+//   SoA per instance (coalesced u32 each):
+//     meta0 = N | N<<8 (H,W) | sr<<16 | sc<<24     meta1 = gr | gc<<8 | max_steps<<16
+//     posw  = r | c<<8 | nm<<16 (min(len(visited_cell),2)) | last_action<<18 | done<<20
+//     stw   = steps (0-15) | invalid streak (16-23, saturating)
+//     curw  = cells word at the current position
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MZ_PLANE_WORDS 8
+#define MZ_CELL_D_MASK 0xFFFFu
+#define MZ_CELL_CODE_SHIFT 16
+#define MZ_CELL_OPEN (1u << 19)
+#define MZ_CELL_NB_SHIFT 20
+
+struct MzDev {
+  int B, P, VP, toroidal, enrich;
+  uint32_t* cells;
+  uint32_t* planes;
+  uint8_t* visits;
+  uint32_t* meta0;
+  uint32_t* meta1;
+  uint32_t* posw;
+  uint32_t* stw;
+  uint32_t* curw;
+  uint8_t* algo;            // per-instance algorithm id for regeneration
+  uint8_t* last_term;       // per-instance: last step terminated (for regen_won)
+  const double* pen_visit;  // [256] 0.0 - (1 - exp(-0.2 k))   (base_maze_env.py:194)
+  const double* pen_inv;    // [256] 0.0 - (1 - exp(-0.15 k))  (base_maze_env.py:200)
+};
+
+struct MzOut {
+  float* reward;
+  double* reward64;
+  uint8_t* terminated;
+  uint8_t* truncated;
+  int32_t* pos;
+  int32_t* best_dir;
+  float* obs6;
+  uint32_t* window_bits;
+  float* window;
+  int32_t* done_idx;
+  int32_t* done_count;
+};
+
+// BaseMazeEnv.ACTIONS (base_maze_env.py:19-24): 0 down, 1 up, 2 right, 3 left
+__host__ __device__ inline int mz_dr(int a) { return a == 0 ? 1 : (a == 1 ? -1 : 0); }
+__host__ __device__ inline int mz_dc(int a) { return a == 2 ? 1 : (a == 3 ? -1 : 0); }
+__host__ __device__ inline int mz_wrap(int v, int n) { v %= n; return v < 0 ? v + n : v; }
+
+// ------------------------------------------------------------------------------------------
+// Philox4x32-10 — identical definition in oracle/mzoracle.c (mzo_philox).
+__host__ __device__ inline void mz_philox(uint64_t key, uint64_t ctr_hi, uint64_t ctr_lo,
+                                          uint32_t out[4]) {
+  uint32_t c0 = (uint32_t)ctr_lo, c1 = (uint32_t)(ctr_lo >> 32), c2 = (uint32_t)ctr_hi,
+           c3 = (uint32_t)(ctr_hi >> 32);
+  uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    if (i) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+    uint32_t lo0 = 0xD2511F53u * c0, hi0 = (uint32_t)(((uint64_t)0xD2511F53u * c0) >> 32);
+    uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = (uint32_t)(((uint64_t)0xCD9E8D57u * c2) >> 32);
+    uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+#define MZ_GEN_STREAM 0x6D617A65ull  // 'maze': generation draws
+#define MZ_ACT_STREAM 0x61637421ull  // 'act!': exploration draws
+
+// Sequential draw stream (one per maze): draw k = word (k & 3) of philox(key, {GEN, k >> 2}).
+struct MzRng {
+  uint64_t key, n;
+  uint32_t buf[4];
+  __device__ inline uint32_t u32() {
+    if ((n & 3) == 0) mz_philox(key, MZ_GEN_STREAM, n >> 2, buf);
+    return buf[(n++) & 3];
+  }
+  __device__ inline uint32_t below(uint32_t m) { return (uint32_t)(((uint64_t)u32() * m) >> 32); }
+};
+
+// extract_submaze axis start (maze_handler.py:18-45), N >= 15 (Q7 excluded at load time)
+__device__ inline int mz_win_start(int p, int N) {
+  if (N == 15) return 0;
+  if (p - 7 >= 0 && p + 7 < N) return p - 7;
+  if (p - 7 < 0) return 0;
+  return N - 15;
+}
+
+#define MZ_ALGO_RPRIM_DEV 0
+#define MZ_ALGO_DFS_DEV 1
+#define MZ_ALGO_PRIMKILL_DEV 2

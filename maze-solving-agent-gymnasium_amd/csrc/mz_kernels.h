@@ -1,0 +1,17 @@
+// mz_kernels.h — launchers of the device kernels (mz_env.hip), used by the C ABI (mz_api.hip).
+#pragma once
+#include "mz_common.h"
+
+size_t mz_build_lds_size(int P);
+hipError_t mz_launch_build(const MzDev& d, const int32_t* env_ids, int32_t n, bool generate,
+                           const uint8_t* algo_list, int32_t algo_all, int32_t dim, uint64_t seed,
+                           const uint8_t* grids, const int32_t* start_goal, hipStream_t s);
+hipError_t mz_launch_regen(const MzDev& d, const int32_t* idx, const int32_t* count,
+                           int32_t n_static, uint64_t seed, uint32_t epoch, hipStream_t s);
+hipError_t mz_launch_step(const MzDev& d, const int32_t* act, const MzOut& o, hipStream_t s);
+hipError_t mz_launch_reset_list(const MzDev& d, const int32_t* idx, const int32_t* count,
+                                int32_t n_static, const MzOut& o, hipStream_t s);
+hipError_t mz_launch_mask(const MzDev& d, int probs, float* out4, hipStream_t s);
+hipError_t mz_launch_act(const MzDev& d, const float* eps, float eps_all, const int64_t* greedy,
+                         uint64_t seed, uint64_t counter, int32_t* actions, hipStream_t s);
+hipError_t mz_launch_expand(const uint32_t* bits, float* out, int n, hipStream_t s);

@@ -1,0 +1,47 @@
+"""Build libmazerl.so (HIP, gfx950) in-tree: mazerl/_lib/libmazerl.so.
+
+hipcc cross-compiles for gfx950 without a GPU. -ffp-contract=off keeps every double reward /
+score / max_steps expression rounded like CPython (the kernels also use explicit __d*_rn ops).
+"""
+import os
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(ROOT, "csrc")
+LIBDIR = os.path.join(PKG, "_lib")
+LIB = os.path.join(LIBDIR, "libmazerl.so")
+SOURCES = ["mz_env.hip", "mz_api.hip"]
+DEPS = SOURCES + ["mz_common.h", "mz_kernels.h", "mz_build.inc.h"]
+HEADER = os.path.join(os.path.dirname(ROOT), "include", "mazerl.h")
+
+
+def hipcc():
+    for c in ("/opt/rocm/bin/hipcc", "hipcc"):
+        if os.path.exists(c) or c == "hipcc":
+            return c
+
+
+def stale():
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    return any(os.path.getmtime(os.path.join(CSRC, f)) > t for f in DEPS) or os.path.getmtime(HEADER) > t
+
+
+def build(force=False, verbose=False):
+    if not force and not stale():
+        return LIB
+    os.makedirs(LIBDIR, exist_ok=True)
+    tmp = LIB + ".tmp"
+    cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-ffp-contract=off", "-Wall", "-o", tmp] + [os.path.join(CSRC, f) for f in SOURCES]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force=True, verbose=True))

@@ -1,0 +1,84 @@
+"""ctypes binding of libmazerl.so (include/mazerl.h). This is the product's only compute path.
+
+If the library is missing or fails to load, every env constructor raises immediately — there is
+no CPU fallback.
+"""
+import ctypes as C
+import os
+
+from . import _build
+
+c_i32p = C.POINTER(C.c_int32)
+
+
+class Config(C.Structure):
+    _fields_ = [("num_envs", C.c_int32), ("max_dim", C.c_int32), ("toroidal", C.c_int32),
+                ("enrich", C.c_int32), ("device", C.c_int32), ("reserved", C.c_int32 * 7)]
+
+
+class StepOut(C.Structure):
+    _fields_ = [("reward", C.c_void_p), ("reward64", C.c_void_p), ("terminated", C.c_void_p),
+                ("truncated", C.c_void_p), ("pos", C.c_void_p), ("best_dir", C.c_void_p),
+                ("obs6", C.c_void_p), ("window_bits", C.c_void_p), ("window", C.c_void_p),
+                ("done_idx", C.c_void_p), ("done_count", C.c_void_p)]
+
+
+class EnvInfo(C.Structure):
+    _fields_ = [(k, C.c_int32) for k in ("n", "start_r", "start_c", "goal_r", "goal_c",
+                                         "max_steps", "r", "c", "steps", "invalid_streak",
+                                         "nmoves", "last_action", "done")]
+
+
+MZ_ERRORS = {-1: ValueError, -2: ValueError, -3: RuntimeError, -4: MemoryError, -5: ValueError}
+
+EXPORTS = ["mz_last_error", "mz_device_count", "mz_create", "mz_destroy", "mz_load_mazes",
+           "mz_generate", "mz_reset_all", "mz_reset_list", "mz_step", "mz_direction_mask",
+           "mz_act", "mz_expand_window", "mz_set_algorithm", "mz_query", "mz_get_grid"]
+
+_lib = None
+
+
+def lib_path():
+    return _build.LIB
+
+
+def load(build_if_missing=True):
+    """Load libmazerl.so (building it with hipcc if absent and allowed)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = _build.LIB
+    if not os.path.exists(path):
+        if not build_if_missing:
+            raise RuntimeError(f"libmazerl.so not built ({path}); run mazerl._build.build()")
+        _build.build()
+    L = C.CDLL(path)
+    vp = C.c_void_p
+    L.mz_last_error.restype = C.c_char_p
+    L.mz_device_count.argtypes = [c_i32p]
+    L.mz_create.argtypes = [C.POINTER(Config), C.POINTER(vp)]
+    L.mz_destroy.argtypes = [vp]
+    L.mz_load_mazes.argtypes = [vp, vp, C.c_int32, vp, vp, C.c_int32, vp]
+    L.mz_generate.argtypes = [vp, vp, C.c_int32, vp, C.c_int32, C.c_int32, C.c_uint64, vp]
+    L.mz_reset_all.argtypes = [vp, C.POINTER(StepOut), vp]
+    L.mz_reset_list.argtypes = [vp, vp, vp, C.c_int32, C.c_int32, C.c_uint64, C.c_uint32,
+                                C.POINTER(StepOut), vp]
+    L.mz_step.argtypes = [vp, vp, C.POINTER(StepOut), vp]
+    L.mz_direction_mask.argtypes = [vp, C.c_int32, vp, vp]
+    L.mz_act.argtypes = [vp, vp, C.c_float, vp, C.c_uint64, C.c_uint64, vp, vp]
+    L.mz_expand_window.argtypes = [vp, vp, C.c_int32, vp]
+    L.mz_set_algorithm.argtypes = [vp, vp, C.c_int32, vp]
+    L.mz_query.argtypes = [vp, C.c_int32, C.POINTER(EnvInfo)]
+    L.mz_get_grid.argtypes = [vp, C.c_int32, vp]
+    for f in EXPORTS:
+        if f != "mz_last_error":
+            getattr(L, f).restype = C.c_int
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != 0:
+        msg = load().mz_last_error().decode(errors="replace")
+        raise MZ_ERRORS.get(rc, RuntimeError)(f"libmazerl error {rc}: {msg}")
+    return rc

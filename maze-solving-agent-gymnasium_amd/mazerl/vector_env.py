@@ -1,0 +1,192 @@
+"""VectorMazeEnv — B independent maze env instances on one GPU, stepped by one HIP launch.
+
+Wraps one libmazerl handle. All outputs live in persistent device tensors that every step /
+reset overwrites in place (zero-copy for the learner); clone what you need to keep.
+
+Observation parity with the reference (per instance):
+  obs6[i]   = float32(concat(obs["agent"], obs["target"], obs["best dir"]))  as built by
+              NeuralOffPolicyTrainer (lib/trainers/off_policy_trainer.py:156,169)
+  window[i] = obs["window"] (3x15x15 f32, Enrich envs, lib/maze_handler.py:82-99)
+  pos[i], best_dir[i] = obs["agent"], obs["best dir"] (plain envs)
+  reward64[i] = the exact Python float the reference returns; reward[i] its float32 rounding.
+The step tuple keeps the reference's order (obs, reward, truncated, terminated, info)
+(gymnasium_env/envs/base_maze_env.py:210).
+"""
+import torch
+
+from . import _native as N
+
+ALGOS = {"r-prim": 0, "dfs": 1, "prim&kill": 2}
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+class VectorMazeEnv:
+    def __init__(self, num_envs, maze_dim, toroidal=False, enrich=True, device=None,
+                 max_dim=None, algorithm="r-prim", seed=0x5EED0000, generate=True,
+                 window=True, window_bits=True, reward64=False, pos=True):
+        if not torch.cuda.is_available():
+            raise RuntimeError("VectorMazeEnv needs a HIP GPU (libmazerl.so has no CPU path)")
+        self.lib = N.load()
+        self.device = torch.device(device if device is not None else f"cuda:{torch.cuda.current_device()}")
+        self.num_envs = int(num_envs)
+        self.maze_dim = int(maze_dim)
+        self.max_dim = int(max_dim or maze_dim)
+        self.toroidal, self.enrich = bool(toroidal), bool(enrich)
+        cfg = N.Config(num_envs=self.num_envs, max_dim=self.max_dim, toroidal=int(toroidal),
+                       enrich=int(enrich), device=self.device.index or 0)
+        h = N.C.c_void_p()
+        N.check(self.lib.mz_create(N.C.byref(cfg), N.C.byref(h)))
+        self._h = h
+        B, dev = self.num_envs, self.device
+        kw = dict(device=dev)
+        self.reward = torch.zeros(B, dtype=torch.float32, **kw)
+        self.reward64 = torch.zeros(B, dtype=torch.float64, **kw) if reward64 else None
+        self.terminated = torch.zeros(B, dtype=torch.uint8, **kw)
+        self.truncated = torch.zeros(B, dtype=torch.uint8, **kw)
+        self.pos = torch.zeros(B, 2, dtype=torch.int32, **kw) if pos else None
+        self.best_dir = torch.zeros(B, 2, dtype=torch.int32, **kw) if pos else None
+        self.obs6 = torch.zeros(B, 6, dtype=torch.float32, **kw)
+        self.window = torch.zeros(B, 3, 15, 15, dtype=torch.float32, **kw) if (enrich and window) else None
+        self.window_bits = torch.zeros(B, 22, dtype=torch.int32, **kw) if (enrich and window_bits) else None
+        self.done_idx = torch.zeros(B, dtype=torch.int32, **kw)
+        self.done_count = torch.zeros(1, dtype=torch.int32, **kw)
+        self.actions = torch.zeros(B, dtype=torch.int32, **kw)
+        self._out = N.StepOut(
+            reward=_ptr(self.reward), reward64=_ptr(self.reward64), terminated=_ptr(self.terminated),
+            truncated=_ptr(self.truncated), pos=_ptr(self.pos), best_dir=_ptr(self.best_dir),
+            obs6=_ptr(self.obs6), window_bits=_ptr(self.window_bits), window=_ptr(self.window),
+            done_idx=_ptr(self.done_idx), done_count=_ptr(self.done_count))
+        self.seed = int(seed)
+        self.epoch = 0
+        if generate:
+            self.generate(algorithm=algorithm)
+            self.reset()
+
+    # ---------------------------------------------------------------------------------------
+    def _stream(self):
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.mz_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------------------------------------
+    def generate(self, env_ids=None, algorithm="r-prim", dim=None, seed=None):
+        """New mazes for env_ids (None = all): gen_maze(shape, algorithm) per instance."""
+        dim = int(dim or self.maze_dim)
+        seed = self.seed if seed is None else int(seed)
+        ids = None if env_ids is None else torch.as_tensor(env_ids, dtype=torch.int32, device=self.device)
+        n = self.num_envs if ids is None else int(ids.numel())
+        algo_t, algo_all = None, 0
+        if isinstance(algorithm, str):
+            algo_all = ALGOS[algorithm]
+        elif isinstance(algorithm, int):
+            algo_all = int(algorithm)
+        else:
+            algo_t = torch.as_tensor(algorithm, dtype=torch.uint8, device=self.device)
+            if algo_t.numel() != n:
+                raise ValueError("per-instance algorithm ids must match the env list")
+        N.check(self.lib.mz_generate(self._h, _ptr(ids), n, _ptr(algo_t), algo_all, dim,
+                                     seed & 0xFFFFFFFFFFFFFFFF, self._stream()))
+        return self
+
+    def load_mazes(self, grids, start_goal, env_ids=None):
+        """Import mazes bit-exactly (uint8 [n, dim, dim], int [n, 4] = sr, sc, gr, gc)."""
+        import numpy as np
+        g = np.ascontiguousarray(grids, dtype=np.uint8)
+        sg = np.ascontiguousarray(start_goal, dtype=np.int32)
+        ids = None if env_ids is None else np.ascontiguousarray(env_ids, dtype=np.int32)
+        n, dim = g.shape[0], g.shape[1]
+        N.check(self.lib.mz_load_mazes(self._h, g.ctypes.data, dim, sg.ctypes.data,
+                                       None if ids is None else ids.ctypes.data, n,
+                                       self._stream()))
+        return self
+
+    def set_algorithm(self, algorithm):
+        if isinstance(algorithm, str):
+            N.check(self.lib.mz_set_algorithm(self._h, None, ALGOS[algorithm], self._stream()))
+        else:
+            t = torch.as_tensor(algorithm, dtype=torch.uint8, device=self.device)
+            N.check(self.lib.mz_set_algorithm(self._h, _ptr(t), 0, self._stream()))
+
+    # ---------------------------------------------------------------------------------------
+    def reset(self):
+        N.check(self.lib.mz_reset_all(self._h, N.C.byref(self._out), self._stream()))
+        return self.obs(), {}
+
+    def reset_list(self, idx, count=None, regen_won=False, seed=None):
+        """Reset listed instances (device int32 list + optional device count)."""
+        idx = torch.as_tensor(idx, dtype=torch.int32, device=self.device)
+        if regen_won:
+            self.epoch += 1
+        N.check(self.lib.mz_reset_list(self._h, _ptr(idx), _ptr(count), int(idx.numel()),
+                                       int(bool(regen_won)),
+                                       (self.seed if seed is None else int(seed)) & 0xFFFFFFFFFFFFFFFF,
+                                       self.epoch & 0xFFFFFFFF, N.C.byref(self._out),
+                                       self._stream()))
+
+    def reset_done(self, regen_won=False, seed=None):
+        """Auto-reset: reset every instance of the last step's done list (device-side list)."""
+        self.reset_list(self.done_idx, self.done_count, regen_won=regen_won, seed=seed)
+
+    def step(self, actions):
+        """actions: int tensor [B] on the device (negative = observe only)."""
+        a = actions if (actions.dtype == torch.int32 and actions.device == self.device) else \
+            actions.to(device=self.device, dtype=torch.int32)
+        a = a.contiguous()
+        N.check(self.lib.mz_step(self._h, a.data_ptr(), N.C.byref(self._out), self._stream()))
+        return self.obs(), self.reward, self.truncated, self.terminated, {}
+
+    def obs(self):
+        o = {"obs6": self.obs6}
+        if self.pos is not None:
+            o["agent"], o["best dir"] = self.pos, self.best_dir
+        if self.window is not None:
+            o["window"] = self.window
+        if self.window_bits is not None:
+            o["window_bits"] = self.window_bits
+        return o
+
+    def direction_mask(self, probs=False, out=None):
+        out = out if out is not None else torch.empty(self.num_envs, 4, dtype=torch.float32, device=self.device)
+        N.check(self.lib.mz_direction_mask(self._h, int(bool(probs)), out.data_ptr(), self._stream()))
+        return out
+
+    def act(self, eps=1.0, greedy=None, seed=0, counter=0, out=None):
+        """epsilon-greedy with the reference's masked exploration distribution."""
+        out = out if out is not None else self.actions
+        eps_t = eps if torch.is_tensor(eps) else None
+        g = None if greedy is None else greedy.to(dtype=torch.int64).contiguous()
+        N.check(self.lib.mz_act(self._h, _ptr(eps_t), float(eps) if eps_t is None else 0.0,
+                                _ptr(g), seed & 0xFFFFFFFFFFFFFFFF, counter & 0xFFFFFFFFFFFFFFFF,
+                                out.data_ptr(), self._stream()))
+        return out
+
+    def expand_window(self, bits, out=None):
+        n = bits.shape[0]
+        out = out if out is not None else torch.empty(n, 3, 15, 15, dtype=torch.float32, device=bits.device)
+        N.check(self.lib.mz_expand_window(bits.data_ptr(), out.data_ptr(), n, self._stream()))
+        return out
+
+    # ---------------------------------------------------------------------------------------
+    def query(self, i):
+        info = N.EnvInfo()
+        N.check(self.lib.mz_query(self._h, int(i), N.C.byref(info)))
+        return {k: getattr(info, k) for k, _ in N.EnvInfo._fields_}
+
+    def grid(self, i):
+        import numpy as np
+        n = self.query(i)["n"]
+        g = np.zeros((n, n), np.uint8)
+        N.check(self.lib.mz_get_grid(self._h, int(i), g.ctypes.data))
+        return g
