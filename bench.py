@@ -1,0 +1,165 @@
+#!/usr/bin/env python3
+"""Headline benchmark: env steps/sec on 40x40-cell (81x81 grid) r-prim mazes (BASELINE.json).
+
+One "step" = one vector step of the hot path over every instance on the GPU:
+  k_act (reference masked-exploration action, dqn_agent.py:110-112)
+  -> k_step (BaseMazeEnv.step + Enrich obs: reward, terminated/truncated, obs6, f32 3x15x15 window)
+  -> k_reset_list (auto-reset of the instances that just finished, base_maze_env.py:136-161)
+Workload: configs[2] of BASELINE.json — 65,536 instances of 81x81-grid r-prim mazes per GPU,
+generated on the GPU before the timed region (generation is reported separately).
+Multi-GPU: one process per GPU (torchrun), independent env shards (no data-path collective),
+weak scaling; value = all ranks' env steps / max-over-ranks wall time.
+
+Extra JSON fields: roofline of k_step (HIP events on the launch stream), cpu_baseline (the CPU
+oracle in reference-cost mode, A* per find_path, timed on host cores — rank 0, N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "maze-solving-agent-gymnasium_amd"))
+
+# Algorithmic bytes per instance-step of k_step: 66 B compact state/outputs
+# + 2,955 B for the Enrich window (2,700 B f32 window write + 225 B visit plane + 30 B wall rows)
+ALG_BYTES_PER_STEP = 3021
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--envs", type=int, default=65536, help="instances per GPU")
+    ap.add_argument("--dim", type=int, default=81)
+    ap.add_argument("--algo", default="r-prim")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="cpu_baseline sample budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(env, seconds):
+    """Oracle (oracle/mzoracle.c, 'port' of the reference algorithm at its cost model: heap A*
+    for every find_path) timed on this host's cores on one of the benchmark's own mazes."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as O
+    q = env.query(0)
+    grid = env.grid(0)
+    start, goal = (q["start_r"], q["start_c"]), (q["goal_r"], q["goal_c"])
+    threads = max(1, min(16, os.cpu_count() or 1))
+    # calibrate on a short run, then size the sample to ~`seconds`
+    t, n = O.bench(grid, start, goal, False, True, True, threads, 20, threads)
+    rate = n / max(t, 1e-9)
+    per_env = max(20, int(rate * seconds / threads))
+    t, n = O.bench(grid, start, goal, False, True, True, threads, per_env, threads, seed=2)
+    tf, nf = O.bench(grid, start, goal, False, True, False, threads, per_env * 20, threads, seed=3)
+    return {"value": n / t, "unit": "env steps/s", "cores": threads, "kind": "port",
+            "sample": f"{threads} envs x {per_env} steps (81x81 r-prim Enrich, masked-exploration "
+                      f"actions, auto-reset), oracle in reference-cost mode (heap A* per find_path); "
+                      f"{t:.1f} s",
+            "bfs_field_mode": {"value": nf / tf, "steps": nf, "seconds": round(tf, 2)}}
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    import mazerl
+    B = a.envs
+    # global instance ids rank*B .. : Philox seed 0x5EED0000 + global id
+    t0 = time.perf_counter()
+    env = mazerl.VectorMazeEnv(B, a.dim, enrich=True, device=dev, algorithm=a.algo,
+                               seed=0x5EED0000 + rank * B, window=True, window_bits=False,
+                               pos=False)
+    torch.cuda.synchronize()
+    gen_s = time.perf_counter() - t0
+    stream = torch.cuda.current_stream(dev)
+
+    def vstep(k, ev=None):
+        acts = env.act(eps=1.0, seed=0xBE7C4 + rank, counter=k)
+        if ev is not None:
+            ev[0].record(stream)
+        env.step(acts)
+        if ev is not None:
+            ev[1].record(stream)
+        env.reset_done()
+
+    for k in range(a.warmup):
+        vstep(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(a.steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(a.steps):
+        vstep(a.warmup + k, evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    step_ms = [s.elapsed_time(e) for s, e in evs]
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    total_steps = B * a.steps * world
+    value = total_steps / el
+    avg_kernel_ms = sum(step_ms) / len(step_ms)
+    achieved = ALG_BYTES_PER_STEP * B / (avg_kernel_ms * 1e-3) / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_k_step.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            p = json.load(f)
+        if p.get("envs") == B and p.get("dim") == a.dim:
+            traffic = p.get("hbm_bytes_per_launch")
+
+    if rank == 0:
+        out = {
+            "metric": "env steps/sec (whole node) + DQN win-rate, 40x40 r-prim mazes",
+            "value": value,
+            "unit": "env steps/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": el / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic (GPU-generated r-prim mazes, Philox seeds 0x5EED0000 + instance id)",
+            "config": {"workload": f"{B} x 40x40-cell ({a.dim}x{a.dim} grid) {a.algo} Enrich mazes "
+                                   f"per GPU: act + env step (f32 3x15x15 window) + auto-reset",
+                       "envs_per_gpu": B, "grid": a.dim, "algo": a.algo, "parallelism": f"dp{world} env shards"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_step", "avg_kernel_ms": avg_kernel_ms,
+                         "alg_bytes_per_instance_step": ALG_BYTES_PER_STEP},
+            "generation": {"mazes": B, "seconds": round(gen_s, 3), "mazes_per_s": B / gen_s,
+                           "note": "first build incl. module load; excluded from value"},
+            "win_rate": None,
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(env, a.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

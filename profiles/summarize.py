@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Turn rocprofv3 outputs under gpurun_out/ into the committed summaries under profiles/.
+
+  python profiles/summarize.py <round_tag> <kernel-trace dir> <FETCH_SIZE dir> <WRITE_SIZE dir> \
+      --envs 65536 --dim 81
+
+Writes profiles/<tag>_kernel_stats.csv (copy of rocprofv3 --stats) and profiles/pmc_k_step.json:
+per-launch HBM bytes of k_step = (2 x FETCH_SIZE + WRITE_SIZE) x 1024, the gfx950 correction of
+MI355X_MICROARCH.md §HBM (FETCH_SIZE reads half of the bytes of wide streaming reads; the
+gathers of k_step are uncalibrated, so the doubled figure is an upper bound on its read side).
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import shutil
+import statistics
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def counter(d, name, kernel_sub):
+    f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(f))
+            if r["Counter_Name"] == name and kernel_sub in r["Kernel_Name"]]
+    return statistics.mean(vals), len(vals)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag")
+    ap.add_argument("kt")
+    ap.add_argument("fetch")
+    ap.add_argument("write")
+    ap.add_argument("--envs", type=int, default=65536)
+    ap.add_argument("--dim", type=int, default=81)
+    ap.add_argument("--kernel", default="k_step<false, true>")
+    a = ap.parse_args()
+    stats = glob.glob(os.path.join(a.kt, "**", "*kernel_stats.csv"), recursive=True)[0]
+    shutil.copy(stats, os.path.join(HERE, f"{a.tag}_kernel_stats.csv"))
+    avg_ns = [float(r["AverageNs"]) for r in csv.DictReader(open(stats)) if a.kernel in r["Name"]][0]
+    fetch_kb, nf = counter(a.fetch, "FETCH_SIZE", a.kernel)
+    write_kb, nw = counter(a.write, "WRITE_SIZE", a.kernel)
+    out = {
+        "kernel": a.kernel, "envs": a.envs, "dim": a.dim,
+        "rocprof_avg_ns": avg_ns,
+        "FETCH_SIZE_kb_per_launch": fetch_kb, "WRITE_SIZE_kb_per_launch": write_kb,
+        "launches_sampled": [nf, nw],
+        "hbm_bytes_per_launch": (2 * fetch_kb + write_kb) * 1024,
+        "hbm_bytes_per_launch_uncorrected": (fetch_kb + write_kb) * 1024,
+        "note": "traffic = (2*FETCH_SIZE + WRITE_SIZE)*1024 per MI355X_MICROARCH.md §HBM; "
+                "separate --pmc passes for FETCH_SIZE and WRITE_SIZE",
+    }
+    with open(os.path.join(HERE, "pmc_k_step.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
