@@ -2,8 +2,8 @@
 """Headline benchmark: env steps/sec on 40x40-cell (81x81 grid) r-prim mazes (BASELINE.json).
 
 One "step" = one vector step of the hot path over every instance on the GPU:
-  k_act (reference masked-exploration action, dqn_agent.py:110-112)
-  -> k_step (BaseMazeEnv.step + Enrich obs: reward, terminated/truncated, obs6, f32 3x15x15 window)
+  k_step with the fused reference masked-exploration act (dqn_agent.py:110-112) +
+     BaseMazeEnv.step + Enrich obs (reward, terminated/truncated, obs6, f32 3x15x15 window)
   -> k_reset_list (auto-reset of the instances that just finished, base_maze_env.py:136-161)
 Workload: configs[2] of BASELINE.json — 65,536 instances of 81x81-grid r-prim mazes per GPU,
 generated on the GPU before the timed region (generation is reported separately).
@@ -82,16 +82,16 @@ def main():
     t0 = time.perf_counter()
     env = mazerl.VectorMazeEnv(B, a.dim, enrich=True, device=dev, algorithm=a.algo,
                                seed=0x5EED0000 + rank * B, window=True, window_bits=False,
-                               pos=False)
+                               pos=False, done_list=False)
     torch.cuda.synchronize()
     gen_s = time.perf_counter() - t0
     stream = torch.cuda.current_stream(dev)
 
     def vstep(k, ev=None):
-        acts = env.act(eps=1.0, seed=0xBE7C4 + rank, counter=k)
+        # fused act + step (one launch), then auto-reset of the finished instances
         if ev is not None:
             ev[0].record(stream)
-        env.step(acts)
+        env.step_act(eps=1.0, seed=0xBE7C4 + rank, counter=k)
         if ev is not None:
             ev[1].record(stream)
         env.reset_done()
@@ -143,7 +143,7 @@ def main():
             "dtype": "int32",
             "data": "synthetic (GPU-generated r-prim mazes, Philox seeds 0x5EED0000 + instance id)",
             "config": {"workload": f"{B} x 40x40-cell ({a.dim}x{a.dim} grid) {a.algo} Enrich mazes "
-                                   f"per GPU: act + env step (f32 3x15x15 window) + auto-reset",
+                                   f"per GPU: fused act+env step (f32 3x15x15 window) + auto-reset",
                        "envs_per_gpu": B, "grid": a.dim, "algo": a.algo, "parallelism": f"dp{world} env shards"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -104,12 +104,20 @@ int mz_generate(mz_handle* h, const int32_t* env_ids_dev, int32_t n, const uint8
 
 /* Reset every instance / a device list of instances (e.g. step's done_idx/done_count) and
  * write their reset observations into `out`. Replaces BaseMazeEnv.reset (base_maze_env.py:136-161).
+ * A non-NULL count_dev is consumed: the kernel sets it to 0 once every workgroup has read it,
+ * so the next mz_step_act may pass MZ_STEP_COUNT_ZEROED.
  * With regen_won != 0, listed instances whose last step terminated get a freshly generated maze
  * first (the trainer's win -> update_maze protocol, off_policy_trainer.py:190-202), using their
  * stored algorithm id and seed + env_id + (epoch << 32). */
 int mz_reset_all(mz_handle* h, const mz_step_out* out, void* stream);
 int mz_reset_list(mz_handle* h, const int32_t* idx_dev, const int32_t* count_dev,
                   int32_t max_count, int32_t regen_won, uint64_t seed, uint32_t epoch,
+                  const mz_step_out* out, void* stream);
+
+/* Auto-reset: reset every instance whose last step ended terminated|truncated (a per-instance
+ * flag kept by the step; no device list needed) and write its reset observation into `out`.
+ * With regen_won != 0 the instances that won get a new maze first (as mz_reset_list). */
+int mz_reset_done(mz_handle* h, int32_t regen_won, uint64_t seed, uint32_t epoch,
                   const mz_step_out* out, void* stream);
 
 /* One env step for all B instances. actions_dev: [B] int32 in 0..3 (BaseMazeEnv.ACTIONS);
@@ -119,6 +127,14 @@ int mz_reset_list(mz_handle* h, const int32_t* idx_dev, const int32_t* count_dev
  * maze_view.move_agent (maze_view.py:167-197) and _get_obs/_find_best_next_cell (:116-122,
  * :224-262) / the Enrich window (maze_handler.py:4-99). */
 int mz_step(mz_handle* h, const int32_t* actions_dev, const mz_step_out* out, void* stream);
+
+/* Fused act + step (one launch): each instance takes the epsilon-greedy action of mz_act
+ * (below) and steps; actions_out_dev [B] (nullable) receives the actions taken.
+ * flags: MZ_STEP_COUNT_ZEROED = out->done_count is already 0 (skip the memset). */
+#define MZ_STEP_COUNT_ZEROED 1
+int mz_step_act(mz_handle* h, const float* eps_dev, float eps_all, const int64_t* greedy_dev,
+                uint64_t seed, uint64_t counter, int32_t* actions_out_dev, const mz_step_out* out,
+                int32_t flags, void* stream);
 
 /* get_mask_direction(probs) for all instances: out4_dev [B][4] f32
  * (simple_maze_env.py:41-50, toroidal_maze_env.py:57-69). */

@@ -132,7 +132,8 @@ int mz_create(const mz_config* cfg, mz_handle** out) {
   if ((rc = alloc(h, &d.cells, B * P * P)) || (rc = alloc(h, &d.planes, B * P * MZ_PLANE_WORDS + 16)) ||
       (rc = alloc(h, &d.visits, B * (size_t)d.VP)) || (rc = alloc(h, &d.meta0, B)) ||
       (rc = alloc(h, &d.meta1, B)) || (rc = alloc(h, &d.posw, B)) || (rc = alloc(h, &d.stw, B)) ||
-      (rc = alloc(h, &d.curw, B)) || (rc = alloc(h, &d.algo, B)) || (rc = alloc(h, &d.last_term, B))) {
+      (rc = alloc(h, &d.curw, B)) || (rc = alloc(h, &d.algo, B)) || (rc = alloc(h, &d.last_term, B)) ||
+      (rc = alloc(h, &d.ticket, 16))) {
     mz_destroy(h);
     return rc;
   }
@@ -238,7 +239,18 @@ int mz_reset_list(mz_handle* h, const int32_t* idx_dev, const int32_t* count_dev
   DeviceGuard g(h->cfg.device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (regen_won) MZ_HIP(mz_launch_regen(h->d, idx_dev, count_dev, max_count, seed, epoch, s));
-  MZ_HIP(mz_launch_reset_list(h->d, idx_dev, count_dev, max_count, to_dev(out), s));
+  MZ_HIP(mz_launch_reset_list(h->d, idx_dev, const_cast<int32_t*>(count_dev), max_count, to_dev(out), s));
+  return MZ_OK;
+}
+
+int mz_reset_done(mz_handle* h, int32_t regen_won, uint64_t seed, uint32_t epoch,
+                  const mz_step_out* out, void* stream) {
+  if (!h) return fail(MZ_EINVAL, "null handle");
+  int rc = check_out(out);
+  if (rc) return rc;
+  DeviceGuard g(h->cfg.device);
+  MZ_HIP(mz_launch_reset_done(h->d, regen_won ? 1 : 0, seed, epoch, to_dev(out),
+                              static_cast<hipStream_t>(stream)));
   return MZ_OK;
 }
 
@@ -249,7 +261,22 @@ int mz_step(mz_handle* h, const int32_t* actions_dev, const mz_step_out* out, vo
   DeviceGuard g(h->cfg.device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (out && out->done_count) MZ_HIP(hipMemsetAsync(out->done_count, 0, sizeof(int32_t), s));
-  MZ_HIP(mz_launch_step(h->d, actions_dev, to_dev(out), s));
+  MZ_HIP(mz_launch_step(h->d, actions_dev, nullptr, to_dev(out), s));
+  return MZ_OK;
+}
+
+int mz_step_act(mz_handle* h, const float* eps_dev, float eps_all, const int64_t* greedy_dev,
+                uint64_t seed, uint64_t counter, int32_t* actions_out_dev, const mz_step_out* out,
+                int32_t flags, void* stream) {
+  if (!h) return fail(MZ_EINVAL, "null handle");
+  int rc = check_out(out);
+  if (rc) return rc;
+  DeviceGuard g(h->cfg.device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (out && out->done_count && !(flags & MZ_STEP_COUNT_ZEROED))
+    MZ_HIP(hipMemsetAsync(out->done_count, 0, sizeof(int32_t), s));
+  MzAct ap{eps_dev, eps_all, greedy_dev, seed, counter, actions_out_dev};
+  MZ_HIP(mz_launch_step(h->d, nullptr, &ap, to_dev(out), s));
   return MZ_OK;
 }
 
@@ -265,8 +292,8 @@ int mz_act(mz_handle* h, const float* eps_dev, float eps_all, const int64_t* gre
            uint64_t seed, uint64_t counter, int32_t* actions_dev, void* stream) {
   if (!h || !actions_dev) return fail(MZ_EINVAL, "bad arguments");
   DeviceGuard g(h->cfg.device);
-  MZ_HIP(mz_launch_act(h->d, eps_dev, eps_all, greedy_dev, seed, counter, actions_dev,
-                       static_cast<hipStream_t>(stream)));
+  MzAct ap{eps_dev, eps_all, greedy_dev, seed, counter, actions_dev};
+  MZ_HIP(mz_launch_act(h->d, ap, static_cast<hipStream_t>(stream)));
   return MZ_OK;
 }
 

@@ -332,13 +332,13 @@ __device__ void mz_build_one(const MzDev& d, int e, bool tor, bool generate, int
     const bool open = r < N && c < N && L.g[r * N + c] != 0;
     d.cells[es * P * P + p] = open ? mz_cell_word(L, N, tor, r, c, gr, gc) : 0u;
   }
-  // open / visited bit-plane rows; visited = {start} (reset)
+  // open / visited bit-plane rows, interleaved word pairs; visited = {start} (reset)
   for (int R = lane; R < P; R += 64) {
     uint32_t w[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
     if (R < N)
       for (int c = 0; c < N; ++c)
-        if (L.g[R * N + c] != 0) w[c >> 5] |= 1u << (c & 31);
-    if (R == sr) w[4 + (sc >> 5)] |= 1u << (sc & 31);
+        if (L.g[R * N + c] != 0) w[2 * (c >> 5)] |= 1u << (c & 31);
+    if (R == sr) w[2 * (sc >> 5) + 1] |= 1u << (sc & 31);
     uint4* row = reinterpret_cast<uint4*>(d.planes + (es * P + R) * MZ_PLANE_WORDS);
     row[0] = make_uint4(w[0], w[1], w[2], w[3]);
     row[1] = make_uint4(w[4], w[5], w[6], w[7]);

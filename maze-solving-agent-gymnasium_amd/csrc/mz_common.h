@@ -8,8 +8,9 @@
 //                        (_find_best_next_cell base_maze_env.py:224-262, find_path
 //                        simple_maze_env.py:70-79) is a function of the cell: computed once per
 //                        maze, gathered once per step.
-//   planes u32 [B][P][8] words 0-3 = open bits of the row, words 4-7 = visited bits (the
-//                        reference's non_visited plane inverted, base_maze_env.py:40-41,184)
+//   planes u32 [B][P][8] per row, interleaved (open, visited) word pairs for columns 32k..32k+31:
+//                        [o0 v0 o1 v1 o2 v2 o3 v3]; visited = the reference's non_visited plane
+//                        inverted (base_maze_env.py:40-41,184). A window row needs 2 x 8 B loads.
 //   visits u8  [B][VP]   entries into each cell since reset (visited_cell.count, :194),
 //                        saturating at 255 (exact: penalties are -1.0 for k >= 188)
 //   SoA per instance (coalesced u32 each):
@@ -41,6 +42,15 @@ struct MzDev {
   uint8_t* last_term;       // per-instance: last step terminated (for regen_won)
   const double* pen_visit;  // [256] 0.0 - (1 - exp(-0.2 k))   (base_maze_env.py:194)
   const double* pen_inv;    // [256] 0.0 - (1 - exp(-0.15 k))  (base_maze_env.py:200)
+  int* ticket;              // exit ticket of k_reset_list (done-count consumption)
+};
+
+struct MzAct {  // fused epsilon-greedy act (dqn_agent.py:104-116)
+  const float* eps;
+  float eps_all;
+  const int64_t* greedy;
+  uint64_t seed, counter;
+  int32_t* act_out;
 };
 
 struct MzOut {

@@ -1,15 +1,19 @@
-// mz_env.hip — the per-step hot path of the batched maze env on gfx950.
+// mz_env.hip — the per-step hot path of the batched maze env on gfx950 (+ build/reset kernels).
 //
-//   k_step        one lane per instance: BaseMazeEnv.step (base_maze_env.py:163-210) with the
-//                 move rule of maze_view.move_agent (maze_view.py:167-197), the Enrich window
-//                 (maze_handler.py:4-99) and "best dir" from the precomputed cell word.
-//                 Per 64-instance wave the 675-bit windows are assembled in LDS and written out
-//                 with fully coalesced 16-B stores (1 KiB per wave instruction).
-//   k_reset_list  one wave per listed instance: BaseMazeEnv.reset (:136-161), optionally after
-//                 regenerating the maze of instances that just won (off_policy_trainer.py:190-202)
-//   k_act         fused epsilon-greedy / masked exploration (dqn_agent.py:104-116)
-//   k_mask        get_mask_direction (simple_maze_env.py:41-50, toroidal_maze_env.py:57-69)
-//   k_expand      packed window bits -> f32 [3][15][15]
+//   k_step        BaseMazeEnv.step (base_maze_env.py:163-210) for 32 instances per 64-lane wave:
+//                 phase 1, one lane per instance: (optional fused epsilon-greedy act,
+//                   dqn_agent.py:104-116) move rule of maze_view.move_agent (maze_view.py:167-197),
+//                   reward, counters, "best dir" from the precomputed cell word, done-list
+//                   compaction by wave ballot + one atomic per wave;
+//                 phase 2, one lane per (instance, window row): the Enrich window
+//                   (maze_handler.py:4-99) from the open/visited bit planes, 15 consecutive lanes
+//                   reading 15 consecutive 32-B rows of one instance (few cache lines per load);
+//                 phase 3, the wave's 32 windows (21,600 bits back to back in LDS) leave as f32
+//                   with 16-B stores, 1 KiB contiguous per wave instruction.
+//   k_reset_list  one wave per listed instance: BaseMazeEnv.reset (:136-161); consumes the
+//                 device done count it was given (zeroes it when the grid has read it).
+//   k_build / k_regen_list  maze generation + tables (mz_build.inc.h).
+//   k_act / k_mask / k_expand  exploration act, get_mask_direction, bits -> f32.
 //
 // Floating point: every reward / score is formed with explicitly rounded IEEE double ops
 // (__dadd_rn/__dmul_rn/__ddiv_rn) so contraction cannot change a bit vs CPython.
@@ -20,7 +24,8 @@
 #include "../../include/mazerl.h"
 
 #define WAVE 64
-#define CAT_WORDS (WAVE * 675 / 32 + 2)
+#define IPW 32                          // instances per wave in k_step
+#define CAT_WORDS (IPW * 675 / 32 + 2)  // 21,600 window bits + funnel-shift slack
 
 namespace {
 
@@ -53,71 +58,56 @@ __device__ inline uint32_t wrap_colmask(int col, int C0, int N) {
   return m;
 }
 
-template <int OFF>
-__device__ inline void put15(uint32_t (&w)[MZ_WINDOW_WORDS], uint32_t v) {
-  w[OFF >> 5] |= v << (OFF & 31);
-  if ((OFF & 31) > 17) w[(OFF >> 5) + 1] |= v >> (32 - (OFF & 31));
-}
-
-template <int I>
-__device__ inline void put_row(uint32_t (&w)[MZ_WINDOW_WORDS], uint32_t ch0, uint32_t ch1,
-                               uint32_t ch2) {
-  put15<0 * 225 + I * 15>(w, ch0);
-  put15<1 * 225 + I * 15>(w, ch1);
-  put15<2 * 225 + I * 15>(w, ch2);
-}
-
-// Builds the 675-bit window of instance e at (r,c) from the open/visited planes. (vr,vc) is a
-// cell to treat as visited although its plane bit may not be stored yet (the cell just entered,
-// base_maze_env.py:184 happens before _get_obs); vr < 0 = none. visited_start_only: at reset
-// the visited plane is {start} (base_maze_env.py:148-149), used without reading it back.
-template <bool TOR, int I>
-__device__ inline void window_row(const MzDev& d, size_t e, int N, int r, int c, int gr, int gc,
-                                  int vr, int vc, bool visited_start_only, int sr, int sc,
-                                  uint32_t (&w)[MZ_WINDOW_WORDS]) {
+// Window row i (0..14) of instance e at (r,c): the three 15-bit channel rows of get_mask_tensor
+// (maze_handler.py:82-99): [maze==0, maze==1, non_visited]; the goal (2) is 0 in channels 0 and
+// 1; non_visited = open & ~visited. (vr,vc): cell to count as visited although its plane bit may
+// not be stored yet (just entered, base_maze_env.py:184 precedes _get_obs); vr < 0 = none.
+// vso: at reset the visited plane is {start} (:148-149) — used without reading it back.
+__device__ inline void win_row(const MzDev& d, size_t e, bool tor, int N, int r, int c, int gr,
+                               int gc, int vr, int vc, bool vso, int i, uint32_t& ch0,
+                               uint32_t& ch1, uint32_t& ch2) {
   uint32_t open15, vis15, gmask = 0;
-  if (!TOR) {
-    const int r0 = mz_win_start(r, N), c0 = mz_win_start(c, N);
-    const int R = r0 + I;
+  if (!tor) {
+    const int r0 = mz_win_start(r, N), c0 = mz_win_start(c, N);  // len(maze) for both axes
+    const int R = r0 + i;
     const uint32_t* row = d.planes + (e * d.P + R) * MZ_PLANE_WORDS;
     const int w0 = c0 >> 5, sh = c0 & 31;
-    open15 = ext15(row[w0], row[w0 + 1], sh);
-    if (visited_start_only) {
-      vis15 = (R == sr) ? (1u << (sc - c0)) : 0u;  // start always inside its own window
-    } else {
-      vis15 = ext15(row[4 + w0], row[5 + w0], sh);
-    }
-    if (R == vr) vis15 |= 1u << (vc - c0);
+    const uint2 a = *reinterpret_cast<const uint2*>(row + 2 * w0);      // (open, visited) w0
+    const uint2 b = *reinterpret_cast<const uint2*>(row + 2 * w0 + 2);  // (open, visited) w0+1
+    open15 = ext15(a.x, b.x, sh);
+    vis15 = vso ? ((R == vr) ? (1u << (vc - c0)) : 0u) : ext15(a.y, b.y, sh);
+    if (!vso && R == vr) vis15 |= 1u << (vc - c0);
     if (R == gr && gc >= c0 && gc < c0 + 15) gmask = 1u << (gc - c0);
   } else {
-    const int R = mz_wrap(r + I - 7, N), C0 = mz_wrap(c - 7, N);
+    const int R = mz_wrap(r + i - 7, N), C0 = mz_wrap(c - 7, N);
     const uint4* row4 = reinterpret_cast<const uint4*>(d.planes + (e * d.P + R) * MZ_PLANE_WORDS);
-    uint4 o = row4[0];
-    uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+    const uint4 x = row4[0], y = row4[1];
+    const uint32_t ow[4] = {x.x, x.z, y.x, y.z};
     open15 = row15_wrap(ow, C0, N);
-    if (visited_start_only) {
-      vis15 = (R == sr) ? wrap_colmask(sc, C0, N) : 0u;
+    if (vso) {
+      vis15 = (R == vr) ? wrap_colmask(vc, C0, N) : 0u;
     } else {
-      uint4 v = row4[1];
-      uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+      const uint32_t vw[4] = {x.y, x.w, y.y, y.w};
       vis15 = row15_wrap(vw, C0, N);
+      if (R == vr) vis15 |= wrap_colmask(vc, C0, N);
     }
-    if (R == vr) vis15 |= wrap_colmask(vc, C0, N);
     if (R == gr) gmask = wrap_colmask(gc, C0, N);
   }
-  // get_mask_tensor (maze_handler.py:82-99): [maze==0, maze==1, non_visited]; goal (2) is 0 in
-  // channels 0 and 1; non_visited = open & ~visited.
-  put_row<I>(w, ~open15 & 0x7FFFu, open15 & ~gmask, open15 & ~vis15);
+  ch0 = ~open15 & 0x7FFFu;
+  ch1 = open15 & ~gmask;
+  ch2 = open15 & ~vis15;
 }
 
-template <bool TOR, int I = 0>
-__device__ inline void window_rows(const MzDev& d, size_t e, int N, int r, int c, int gr, int gc,
-                                   int vr, int vc, bool vso, int sr, int sc,
-                                   uint32_t (&w)[MZ_WINDOW_WORDS]) {
-  if constexpr (I < 15) {
-    window_row<TOR, I>(d, e, N, r, c, gr, gc, vr, vc, vso, sr, sc, w);
-    window_rows<TOR, I + 1>(d, e, N, r, c, gr, gc, vr, vc, vso, sr, sc, w);
-  }
+__device__ inline void cat_put(uint32_t* cat, int o, uint32_t v) {
+  if (!v) return;
+  atomicOr(&cat[o >> 5], v << (o & 31));
+  if ((o & 31) > 17) atomicOr(&cat[(o >> 5) + 1], v >> (32 - (o & 31)));
+}
+
+// 32 window bits starting at bit o of cat
+__device__ inline uint32_t cat_get32(const uint32_t* cat, int o) {
+  const int w = o >> 5, s = o & 31;
+  return s ? (cat[w] >> s) | (cat[w + 1] << (32 - s)) : cat[w];
 }
 
 // "best dir" = agent - best_next_cell (base_maze_env.py:122) from the cell's best-next code
@@ -146,14 +136,14 @@ __device__ inline void write_obs6(float* o6, int r, int c, int gr, int gc, int b
   o6[5] = (float)bc;
 }
 
-// Write one wave's windows (bits in `cat`, 675 bits per instance back to back) as f32 with
-// 16-B stores: float f of the block <-> bit f of cat, so a float4 never straddles a word.
+// Write nb windows (bits back to back in cat, 675 per instance) as f32 with 16-B stores:
+// float f of the block <-> bit f of cat, so a float4 never straddles a word.
 __device__ inline void store_window_f32(const uint32_t* cat, float* out, int nb, int lane) {
   const int nfl = nb * 675;
   const int nq = nfl >> 2;
   float4* o4 = reinterpret_cast<float4*>(out);
   for (int q = lane; q < nq; q += WAVE) {
-    uint32_t nib = (cat[q >> 3] >> ((q & 7) * 4)) & 0xFu;
+    const uint32_t nib = (cat[q >> 3] >> ((q & 7) * 4)) & 0xFu;
     float4 v;
     v.x = (float)(nib & 1u);
     v.y = (float)((nib >> 1) & 1u);
@@ -164,36 +154,71 @@ __device__ inline void store_window_f32(const uint32_t* cat, float* out, int nb,
   for (int f = (nq << 2) + lane; f < nfl; f += WAVE) out[f] = (float)((cat[f >> 5] >> (f & 31)) & 1u);
 }
 
-__device__ inline void cat_or(uint32_t* cat, int lane, const uint32_t (&w)[MZ_WINDOW_WORDS]) {
-  const int base = lane * 675, w0 = base >> 5, sh = base & 31;
-#pragma unroll
-  for (int k = 0; k < MZ_WINDOW_WORDS; ++k) {
-    if (w[k] == 0u) continue;
-    atomicOr(&cat[w0 + k], w[k] << sh);
-    if (sh) atomicOr(&cat[w0 + k + 1], w[k] >> (32 - sh));
+__device__ inline void store_window_bits(const uint32_t* cat, uint32_t* wb, int nb, int lane) {
+  for (int k = lane; k < nb * MZ_WINDOW_WORDS; k += WAVE) {
+    const int j = k / MZ_WINDOW_WORDS, w = k - j * MZ_WINDOW_WORDS;
+    uint32_t v = cat_get32(cat, j * 675 + 32 * w);
+    if (w == MZ_WINDOW_WORDS - 1) v &= (1u << (675 - 32 * (MZ_WINDOW_WORDS - 1))) - 1u;
+    wb[k] = v;
   }
 }
 
-// ------------------------------------------------------------------------------------------
-template <bool TOR, bool ENRICH>
-__global__ __launch_bounds__(WAVE) void k_step(MzDev d, const int32_t* __restrict__ act, MzOut o) {
-  __shared__ uint32_t cat[CAT_WORDS];
-  __shared__ uint32_t pad[WAVE][MZ_WINDOW_WORDS + 1];
-  const int lane = threadIdx.x;
-  const int e0 = blockIdx.x * WAVE;
-  const int e = e0 + lane;
-  const int nb = min(WAVE, d.B - e0);
-  const bool live = lane < nb;
-  if (ENRICH) {
-    for (int i = lane; i < CAT_WORDS; i += WAVE) cat[i] = 0u;
-    __syncthreads();
+// get_mask_direction(probs): open-neighbour bits from the current cell word; with probs and
+// >= 2 moves since reset the direction of the previous cell gets 0.25 — on the torus the
+// reference looks it up transposed (Q6): previous below -> "right", above -> "left", etc.
+__device__ inline void dir_mask(uint32_t pw, uint32_t cw, bool tor, bool probs, float m[4]) {
+  const uint32_t nb = (cw >> MZ_CELL_NB_SHIFT) & 0xFu;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) m[k] = (float)((nb >> k) & 1u);
+  const int nm = (pw >> 16) & 3, la = (pw >> 18) & 3;
+  if (probs && nm >= 2) {
+    const int back = la ^ 1;  // action that leads to visited_cell[-2]
+    m[tor ? (back ^ 2) : back] = 0.25f;
   }
+}
+
+// epsilon-greedy with the reference exploration distribution (dqn_agent.py:104-116):
+// u < eps -> np.random.choice(4, p = mask / mask.sum()) by inverse CDF, else greedy.
+__device__ inline int act_sample(const MzAct& ap, int e, uint32_t pw, uint32_t cw, bool tor) {
+  uint32_t u[4];
+  mz_philox(ap.seed, MZ_ACT_STREAM ^ ((uint64_t)e << 32), ap.counter, u);
+  const float ue = (float)(u[0] >> 8) * (1.0f / 16777216.0f);
+  const float ep = ap.eps ? ap.eps[e] : ap.eps_all;
+  if (ap.greedy && !(ue < ep)) return (int)ap.greedy[e];
+  float m[4];
+  dir_mask(pw, cw, tor, true, m);
+  const float tot = m[0] + m[1] + m[2] + m[3];
+  float x = (float)(u[1] >> 8) * (1.0f / 16777216.0f) * tot;
+  int a = 0;
+  while (a < 3 && x >= m[a]) { x -= m[a]; ++a; }
+  while (a > 0 && m[a] == 0.f) --a;
+  return a;
+}
+
+// ------------------------------------------------------------------------------------------
+template <bool TOR, bool ENRICH, bool ACT>
+__global__ __launch_bounds__(WAVE) void k_step(MzDev d, const int32_t* __restrict__ act, MzAct ap,
+                                               MzOut o) {
+  __shared__ uint32_t cat[CAT_WORDS];
+  __shared__ int4 prm[IPW];  // per instance: (r | c<<8 | N<<16, gr | gc<<8, vr, vc)
+  const int lane = threadIdx.x;
+  const int e0 = blockIdx.x * IPW;
+  const int nb = min(IPW, d.B - e0);
+  if (ENRICH)
+    for (int i = lane; i < CAT_WORDS; i += WAVE) cat[i] = 0u;
   bool done = false;
-  if (live) {
+  const int e = e0 + lane;
+  if (lane < nb) {
     const size_t es = (size_t)e;
     const uint32_t m0 = d.meta0[e], m1 = d.meta1[e];
     uint32_t pw = d.posw[e], sw = d.stw[e], cw = d.curw[e];
-    const int araw = act[e];
+    int araw;
+    if (ACT) {
+      araw = act_sample(ap, e, pw, cw, TOR);
+      if (ap.act_out) ap.act_out[e] = araw;
+    } else {
+      araw = act[e];
+    }
     const int a = araw & 3;
     const int N = m0 & 0xFF, gr = m1 & 0xFF, gc = (m1 >> 8) & 0xFF, maxs = m1 >> 16;
     int r = pw & 0xFF, c = (pw >> 8) & 0xFF, nm = (pw >> 16) & 3, la = (pw >> 18) & 3;
@@ -206,8 +231,7 @@ __global__ __launch_bounds__(WAVE) void k_step(MzDev d, const int32_t* __restric
       bool inb;
       if (TOR) { nr = mz_wrap(nr, N); nc = mz_wrap(nc, N); inb = true; }
       else inb = 0 < nr && nr < N - 1 && 0 < nc && nc < N - 1;  // maze_view.py:169 (Q3)
-      const size_t ci = es * d.P * d.P + (size_t)nr * d.P + nc;
-      const uint32_t ncw = inb ? d.cells[ci] : 0u;
+      const uint32_t ncw = inb ? d.cells[es * d.P * d.P + (size_t)nr * d.P + nc] : 0u;
       const bool moved = (ncw & MZ_CELL_OPEN) != 0u;
       if (moved) {
         const size_t vi = es * d.VP + (size_t)nr * d.P + nc;
@@ -215,7 +239,7 @@ __global__ __launch_bounds__(WAVE) void k_step(MzDev d, const int32_t* __restric
         if (cnt == 0) {
           // first entry: non_visited[cell] = 0 (base_maze_env.py:184)
           vr = nr; vc = nc;
-          atomicOr(&d.planes[(es * d.P + nr) * MZ_PLANE_WORDS + 4 + (nc >> 5)], 1u << (nc & 31));
+          atomicOr(&d.planes[(es * d.P + nr) * MZ_PLANE_WORDS + 2 * (nc >> 5) + 1], 1u << (nc & 31));
           if (nr == gr && nc == gc) { rew = 1.0; term = true; }  // :185-187
           else {  // (old_dist - new_dist) * 0.5 - 0.05 with len = D + 1 (:189-192)
             const int dold = (int)(cw & MZ_CELL_D_MASK), dnew = (int)(ncw & MZ_CELL_D_MASK);
@@ -243,7 +267,6 @@ __global__ __launch_bounds__(WAVE) void k_step(MzDev d, const int32_t* __restric
       d.curw[e] = cw;
       d.last_term[e] = term;
     }
-
     int br, bc;
     best_dir(r, c, cw, N, TOR, br, bc);
     if (o.reward) o.reward[e] = (float)rew;
@@ -253,15 +276,7 @@ __global__ __launch_bounds__(WAVE) void k_step(MzDev d, const int32_t* __restric
     if (o.pos) { o.pos[2 * es] = r; o.pos[2 * es + 1] = c; }
     if (o.best_dir) { o.best_dir[2 * es] = br; o.best_dir[2 * es + 1] = bc; }
     if (o.obs6) write_obs6<ENRICH>(o.obs6 + 6 * es, r, c, gr, gc, br, bc, N);
-    if (ENRICH) {
-      uint32_t w[MZ_WINDOW_WORDS];
-#pragma unroll
-      for (int k = 0; k < MZ_WINDOW_WORDS; ++k) w[k] = 0u;
-      window_rows<TOR>(d, es, N, r, c, gr, gc, vr, vc, false, 0, 0, w);
-      cat_or(cat, lane, w);
-#pragma unroll
-      for (int k = 0; k < MZ_WINDOW_WORDS; ++k) pad[lane][k] = w[k];
-    }
+    if (ENRICH) prm[lane] = make_int4(r | (c << 8) | (N << 16), gr | (gc << 8), vr, vc);
   }
   // done-list compaction: wave ballot + one atomic per wave
   if (o.done_idx) {
@@ -275,22 +290,25 @@ __global__ __launch_bounds__(WAVE) void k_step(MzDev d, const int32_t* __restric
   }
   if (ENRICH) {
     __syncthreads();
-    if (o.window_bits) {
-      uint32_t* wb = o.window_bits + (size_t)e0 * MZ_WINDOW_WORDS;
-      for (int i = lane; i < nb * MZ_WINDOW_WORDS; i += WAVE)
-        wb[i] = pad[i / MZ_WINDOW_WORDS][i % MZ_WINDOW_WORDS];
+    for (int p = lane; p < nb * 15; p += WAVE) {
+      const int j = p / 15, i = p - 15 * j;
+      const int4 q = prm[j];
+      uint32_t c0, c1, c2;
+      win_row(d, (size_t)(e0 + j), TOR, (q.x >> 16) & 0xFF, q.x & 0xFF, (q.x >> 8) & 0xFF,
+              q.y & 0xFF, (q.y >> 8) & 0xFF, q.z, q.w, false, i, c0, c1, c2);
+      const int base = j * 675 + i * 15;
+      cat_put(cat, base, c0);
+      cat_put(cat, base + 225, c1);
+      cat_put(cat, base + 450, c2);
     }
+    __syncthreads();
+    if (o.window_bits) store_window_bits(cat, o.window_bits + (size_t)e0 * MZ_WINDOW_WORDS, nb, lane);
     if (o.window) store_window_f32(cat, o.window + (size_t)e0 * 675, nb, lane);
   }
 }
 
-}  // namespace
-
 // ------------------------------------------------------------------------------------------
-namespace {
-
-// Wave-cooperative reset of instance e (lane 0 = scalar state; all lanes clear), then its
-// reset observation. Used by k_reset_list (after optional regeneration in mz_build.hip).
+// Wave-cooperative reset of instance e: BaseMazeEnv.reset (base_maze_env.py:136-161).
 template <bool TOR, bool ENRICH>
 __device__ void reset_one(const MzDev& d, int e, const MzOut& o, uint32_t* wsh) {
   const int lane = threadIdx.x;
@@ -301,21 +319,16 @@ __device__ void reset_one(const MzDev& d, int e, const MzOut& o, uint32_t* wsh) 
   // visits[:] = 0 (visited_cell = [], base_maze_env.py:159)
   uint4* v4 = reinterpret_cast<uint4*>(d.visits + es * d.VP);
   for (int i = lane; i < d.VP / 16; i += WAVE) v4[i] = make_uint4(0, 0, 0, 0);
-  // visited plane = {start} (non_visited = open & ~start, :148-149)
-  for (int R = lane; R < d.P; R += WAVE) {
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (R == sr) {
-      uint32_t bit = 1u << (sc & 31);
-      int wi = sc >> 5;
-      v.x = wi == 0 ? bit : 0u; v.y = wi == 1 ? bit : 0u;
-      v.z = wi == 2 ? bit : 0u; v.w = wi == 3 ? bit : 0u;
-    }
-    reinterpret_cast<uint4*>(d.planes + (es * d.P + R) * MZ_PLANE_WORDS)[1] = v;
+  // visited plane = {start} (non_visited = open & ~start, :148-149): odd words of each row
+  for (int k = lane; k < d.P * 4; k += WAVE) {
+    const int R = k >> 2, w = k & 3;
+    const uint32_t v = (R == sr && w == (sc >> 5)) ? (1u << (sc & 31)) : 0u;
+    d.planes[(es * d.P + R) * MZ_PLANE_WORDS + 2 * w + 1] = v;
   }
   const uint32_t cw = d.cells[es * d.P * d.P + (size_t)sr * d.P + sc];
-  int br, bc;
-  best_dir(sr, sc, cw, N, TOR, br, bc);
   if (lane == 0) {
+    int br, bc;
+    best_dir(sr, sc, cw, N, TOR, br, bc);
     d.posw[e] = (uint32_t)sr | ((uint32_t)sc << 8);
     d.stw[e] = 0u;
     d.curw[e] = cw;
@@ -329,16 +342,17 @@ __device__ void reset_one(const MzDev& d, int e, const MzOut& o, uint32_t* wsh) 
     if (o.obs6) write_obs6<ENRICH>(o.obs6 + 6 * es, sr, sc, gr, gc, br, bc, N);
   }
   if (ENRICH) {
-    if (lane == 0) {
-      uint32_t w[MZ_WINDOW_WORDS];
-#pragma unroll
-      for (int k = 0; k < MZ_WINDOW_WORDS; ++k) w[k] = 0u;
-      window_rows<TOR>(d, es, N, sr, sc, gr, gc, -1, -1, true, sr, sc, w);
-#pragma unroll
-      for (int k = 0; k < MZ_WINDOW_WORDS; ++k) wsh[k] = w[k];
+    if (lane < 24) wsh[lane] = 0u;
+    __syncthreads();
+    if (lane < 15) {  // open words are static; the visited plane is {start} (not read back)
+      uint32_t c0, c1, c2;
+      win_row(d, es, TOR, N, sr, sc, gr, gc, sr, sc, true, lane, c0, c1, c2);
+      cat_put(wsh, lane * 15, c0);
+      cat_put(wsh, 225 + lane * 15, c1);
+      cat_put(wsh, 450 + lane * 15, c2);
     }
     __syncthreads();
-    if (o.window_bits && lane < MZ_WINDOW_WORDS) o.window_bits[es * MZ_WINDOW_WORDS + lane] = wsh[lane];
+    if (o.window_bits) store_window_bits(wsh, o.window_bits + es * MZ_WINDOW_WORDS, 1, lane);
     if (o.window)
       for (int f = lane; f < 675; f += WAVE) o.window[es * 675 + f] = (float)((wsh[f >> 5] >> (f & 31)) & 1u);
     __syncthreads();
@@ -347,13 +361,48 @@ __device__ void reset_one(const MzDev& d, int e, const MzOut& o, uint32_t* wsh) 
 
 template <bool TOR, bool ENRICH>
 __global__ __launch_bounds__(WAVE) void k_reset_list(MzDev d, const int32_t* idx,
-                                                     const int32_t* count, int32_t n_static,
-                                                     MzOut o) {
+                                                     int32_t* count, int32_t n_static, MzOut o) {
   __shared__ __align__(16) uint32_t wsh[32];
   const int n = count ? min(*count, n_static) : n_static;
   for (int j = blockIdx.x; j < n; j += gridDim.x) {
     const int e = idx ? idx[j] : j;
     reset_one<TOR, ENRICH>(d, e, o, wsh);
+    __syncthreads();
+  }
+  if (count && threadIdx.x == 0) {
+    // Consume the count: zero it once every block has read it. Each block's read of *count
+    // has returned before its ticket add issues (the add follows the loop whose bound is that
+    // value), so a relaxed device-scope ticket suffices — no per-block L2 write-back fence.
+    const int t = atomicAdd(d.ticket, 1);
+    if (t == (int)gridDim.x - 1) {
+      __hip_atomic_store(count, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(d.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Auto-reset by flag scan: each wave looks at 64 instances' done flags (one coalesced load),
+// then resets its done instances cooperatively, one after another — waves with nothing to do
+// exit at once, no device list or counter is involved. With regen, instances whose last step
+// terminated first get a new maze (win -> update_maze, off_policy_trainer.py:190-202).
+template <bool TOR, bool ENRICH>
+__global__ __launch_bounds__(WAVE) void k_reset_done(MzDev d, int regen, uint64_t seed,
+                                                     uint32_t epoch, MzOut o) {
+  extern __shared__ __align__(16) uint8_t lds[];
+  __shared__ __align__(16) uint32_t wsh[32];
+  const int e = blockIdx.x * WAVE + threadIdx.x;
+  const bool done = e < d.B && ((d.posw[e] >> 20) & 1u);
+  unsigned long long bal = __ballot(done);
+  while (bal) {
+    const int j = __ffsll((long long)bal) - 1;
+    bal &= bal - 1;
+    const int ej = blockIdx.x * WAVE + j;
+    if (regen && d.last_term[ej]) {
+      mz_build_one(d, ej, TOR, true, d.algo[ej], seed + (uint64_t)ej + ((uint64_t)epoch << 32),
+                   (int)(d.meta0[ej] & 0xFF), nullptr, 0, 0, 0, 0, lds);
+      __syncthreads();  // this workgroup's global stores are visible to it past the barrier
+    }
+    reset_one<TOR, ENRICH>(d, ej, o, wsh);
     __syncthreads();
   }
 }
@@ -394,20 +443,6 @@ __global__ __launch_bounds__(WAVE) void k_regen_list(MzDev d, const int32_t* idx
   }
 }
 
-// get_mask_direction(probs): open-neighbour bits from the current cell word; with probs and
-// >= 2 moves since reset the direction of the previous cell gets 0.25 — on the torus the
-// reference looks it up transposed (Q6): previous below -> "right", above -> "left", etc.
-__device__ inline void dir_mask(uint32_t pw, uint32_t cw, bool tor, bool probs, float m[4]) {
-  const uint32_t nb = (cw >> MZ_CELL_NB_SHIFT) & 0xFu;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) m[k] = (float)((nb >> k) & 1u);
-  const int nm = (pw >> 16) & 3, la = (pw >> 18) & 3;
-  if (probs && nm >= 2) {
-    const int back = la ^ 1;  // action that leads to visited_cell[-2]
-    m[tor ? (back ^ 2) : back] = 0.25f;
-  }
-}
-
 __global__ void k_mask(MzDev d, int probs, float* out4) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= d.B) return;
@@ -416,24 +451,10 @@ __global__ void k_mask(MzDev d, int probs, float* out4) {
   reinterpret_cast<float4*>(out4)[e] = make_float4(m[0], m[1], m[2], m[3]);
 }
 
-__global__ void k_act(MzDev d, const float* eps, float eps_all, const int64_t* greedy,
-                      uint64_t seed, uint64_t counter, int32_t* actions) {
+__global__ void k_act(MzDev d, MzAct ap) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= d.B) return;
-  uint32_t u[4];
-  mz_philox(seed, MZ_ACT_STREAM ^ ((uint64_t)e << 32), counter, u);
-  const float ue = (float)(u[0] >> 8) * (1.0f / 16777216.0f);
-  const float ep = eps ? eps[e] : eps_all;
-  if (greedy && !(ue < ep)) { actions[e] = (int32_t)greedy[e]; return; }
-  float m[4];
-  dir_mask(d.posw[e], d.curw[e], d.toroidal, true, m);
-  // np.random.choice(4, p = mask / mask.sum()) by inverse CDF (dqn_agent.py:110-112)
-  const float tot = m[0] + m[1] + m[2] + m[3];
-  float x = (float)(u[1] >> 8) * (1.0f / 16777216.0f) * tot;
-  int a = 0;
-  while (a < 3 && (x >= m[a] || m[a] == 0.f)) { x -= m[a]; ++a; }
-  while (a > 0 && m[a] == 0.f) --a;
-  actions[e] = a;
+  ap.act_out[e] = act_sample(ap, e, d.posw[e], d.curw[e], d.toroidal);
 }
 
 __global__ void k_expand(const uint32_t* bits, float* out, int n) {
@@ -444,31 +465,19 @@ __global__ void k_expand(const uint32_t* bits, float* out, int n) {
   out[t] = (float)((bits[i * MZ_WINDOW_WORDS + (f >> 5)] >> (f & 31)) & 1u);
 }
 
+// the build kernels may need more than the 64 KiB default dynamic LDS at large max_dim
+hipError_t mz_lds_attr(const void* fn, size_t bytes) {
+  if (bytes <= 65536) return hipSuccess;
+  return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+int mz_grid_for(int n) { return n < 4096 ? n : 4096; }
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
 // launchers (called by mz_api.hip)
-hipError_t mz_launch_step(const MzDev& d, const int32_t* act, const MzOut& o, hipStream_t s) {
-  dim3 grid((d.B + WAVE - 1) / WAVE), block(WAVE);
-  if (d.toroidal) {
-    if (d.enrich) hipLaunchKernelGGL((k_step<true, true>), grid, block, 0, s, d, act, o);
-    else hipLaunchKernelGGL((k_step<true, false>), grid, block, 0, s, d, act, o);
-  } else {
-    if (d.enrich) hipLaunchKernelGGL((k_step<false, true>), grid, block, 0, s, d, act, o);
-    else hipLaunchKernelGGL((k_step<false, false>), grid, block, 0, s, d, act, o);
-  }
-  return hipGetLastError();
-}
-
 size_t mz_build_lds_size(int P) { return mz_build_lds_bytes(P); }
-
-static int mz_grid_for(int n) { return n < 4096 ? n : 4096; }
-
-// the build kernels may need more than the 64 KiB default dynamic LDS at large max_dim
-static hipError_t mz_lds_attr(const void* fn, size_t bytes) {
-  if (bytes <= 65536) return hipSuccess;
-  return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-}
 
 hipError_t mz_launch_build(const MzDev& d, const int32_t* env_ids, int32_t n, bool generate,
                            const uint8_t* algo_list, int32_t algo_all, int32_t dim, uint64_t seed,
@@ -491,10 +500,27 @@ hipError_t mz_launch_regen(const MzDev& d, const int32_t* idx, const int32_t* co
   return hipGetLastError();
 }
 
-hipError_t mz_launch_reset_list(const MzDev& d, const int32_t* idx, const int32_t* count,
+hipError_t mz_launch_step(const MzDev& d, const int32_t* act, const MzAct* ap, const MzOut& o,
+                          hipStream_t s) {
+  dim3 grid((d.B + IPW - 1) / IPW), block(WAVE);
+  MzAct a{};
+  if (ap) a = *ap;
+#define MZ_ST(T, E, A) hipLaunchKernelGGL((k_step<T, E, A>), grid, block, 0, s, d, act, a, o)
+  if (ap) {
+    if (d.toroidal) { if (d.enrich) MZ_ST(true, true, true); else MZ_ST(true, false, true); }
+    else { if (d.enrich) MZ_ST(false, true, true); else MZ_ST(false, false, true); }
+  } else {
+    if (d.toroidal) { if (d.enrich) MZ_ST(true, true, false); else MZ_ST(true, false, false); }
+    else { if (d.enrich) MZ_ST(false, true, false); else MZ_ST(false, false, false); }
+  }
+#undef MZ_ST
+  return hipGetLastError();
+}
+
+hipError_t mz_launch_reset_list(const MzDev& d, const int32_t* idx, int32_t* count,
                                 int32_t n_static, const MzOut& o, hipStream_t s) {
   if (n_static <= 0) return hipSuccess;
-  const int blocks = n_static < 2048 ? n_static : 2048;
+  const int blocks = n_static < 1024 ? n_static : 1024;
 #define MZ_RL(T, E) \
   hipLaunchKernelGGL((k_reset_list<T, E>), dim3(blocks), dim3(WAVE), 0, s, d, idx, count, n_static, o)
   if (d.toroidal) { if (d.enrich) MZ_RL(true, true); else MZ_RL(true, false); }
@@ -503,15 +529,34 @@ hipError_t mz_launch_reset_list(const MzDev& d, const int32_t* idx, const int32_
   return hipGetLastError();
 }
 
+hipError_t mz_launch_reset_done(const MzDev& d, int regen, uint64_t seed, uint32_t epoch,
+                                const MzOut& o, hipStream_t s) {
+  const int blocks = (d.B + WAVE - 1) / WAVE;
+  size_t lds = 0;
+  hipError_t ae = hipSuccess;
+#define MZ_RD(T, E)                                                                           \
+  do {                                                                                        \
+    if (regen) {                                                                              \
+      lds = mz_build_lds_bytes(d.P);                                                          \
+      ae = mz_lds_attr(reinterpret_cast<const void*>(k_reset_done<T, E>), lds);              \
+      if (ae != hipSuccess) return ae;                                                        \
+    }                                                                                         \
+    hipLaunchKernelGGL((k_reset_done<T, E>), dim3(blocks), dim3(WAVE), lds, s, d, regen, seed, \
+                       epoch, o);                                                             \
+  } while (0)
+  if (d.toroidal) { if (d.enrich) MZ_RD(true, true); else MZ_RD(true, false); }
+  else { if (d.enrich) MZ_RD(false, true); else MZ_RD(false, false); }
+#undef MZ_RD
+  return hipGetLastError();
+}
+
 hipError_t mz_launch_mask(const MzDev& d, int probs, float* out4, hipStream_t s) {
   hipLaunchKernelGGL(k_mask, dim3((d.B + 255) / 256), dim3(256), 0, s, d, probs, out4);
   return hipGetLastError();
 }
 
-hipError_t mz_launch_act(const MzDev& d, const float* eps, float eps_all, const int64_t* greedy,
-                         uint64_t seed, uint64_t counter, int32_t* actions, hipStream_t s) {
-  hipLaunchKernelGGL(k_act, dim3((d.B + 255) / 256), dim3(256), 0, s, d, eps, eps_all, greedy,
-                     seed, counter, actions);
+hipError_t mz_launch_act(const MzDev& d, const MzAct& ap, hipStream_t s) {
+  hipLaunchKernelGGL(k_act, dim3((d.B + 255) / 256), dim3(256), 0, s, d, ap);
   return hipGetLastError();
 }
 

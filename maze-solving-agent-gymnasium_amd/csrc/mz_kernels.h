@@ -8,10 +8,12 @@ hipError_t mz_launch_build(const MzDev& d, const int32_t* env_ids, int32_t n, bo
                            const uint8_t* grids, const int32_t* start_goal, hipStream_t s);
 hipError_t mz_launch_regen(const MzDev& d, const int32_t* idx, const int32_t* count,
                            int32_t n_static, uint64_t seed, uint32_t epoch, hipStream_t s);
-hipError_t mz_launch_step(const MzDev& d, const int32_t* act, const MzOut& o, hipStream_t s);
-hipError_t mz_launch_reset_list(const MzDev& d, const int32_t* idx, const int32_t* count,
+hipError_t mz_launch_step(const MzDev& d, const int32_t* act, const MzAct* ap, const MzOut& o,
+                          hipStream_t s);
+hipError_t mz_launch_reset_list(const MzDev& d, const int32_t* idx, int32_t* count,
                                 int32_t n_static, const MzOut& o, hipStream_t s);
+hipError_t mz_launch_reset_done(const MzDev& d, int regen, uint64_t seed, uint32_t epoch,
+                                const MzOut& o, hipStream_t s);
 hipError_t mz_launch_mask(const MzDev& d, int probs, float* out4, hipStream_t s);
-hipError_t mz_launch_act(const MzDev& d, const float* eps, float eps_all, const int64_t* greedy,
-                         uint64_t seed, uint64_t counter, int32_t* actions, hipStream_t s);
+hipError_t mz_launch_act(const MzDev& d, const MzAct& ap, hipStream_t s);
 hipError_t mz_launch_expand(const uint32_t* bits, float* out, int n, hipStream_t s);

@@ -26,7 +26,7 @@ def _ptr(t):
 class VectorMazeEnv:
     def __init__(self, num_envs, maze_dim, toroidal=False, enrich=True, device=None,
                  max_dim=None, algorithm="r-prim", seed=0x5EED0000, generate=True,
-                 window=True, window_bits=True, reward64=False, pos=True):
+                 window=True, window_bits=True, reward64=False, pos=True, done_list=True):
         if not torch.cuda.is_available():
             raise RuntimeError("VectorMazeEnv needs a HIP GPU (libmazerl.so has no CPU path)")
         self.lib = N.load()
@@ -58,9 +58,11 @@ class VectorMazeEnv:
             reward=_ptr(self.reward), reward64=_ptr(self.reward64), terminated=_ptr(self.terminated),
             truncated=_ptr(self.truncated), pos=_ptr(self.pos), best_dir=_ptr(self.best_dir),
             obs6=_ptr(self.obs6), window_bits=_ptr(self.window_bits), window=_ptr(self.window),
-            done_idx=_ptr(self.done_idx), done_count=_ptr(self.done_count))
+            done_idx=_ptr(self.done_idx) if done_list else None,
+            done_count=_ptr(self.done_count) if done_list else None)
         self.seed = int(seed)
         self.epoch = 0
+        self._count_zero = True  # done_count is 0 (fresh, or consumed by reset_done)
         if generate:
             self.generate(algorithm=algorithm)
             self.reset()
@@ -134,9 +136,21 @@ class VectorMazeEnv:
                                        (self.seed if seed is None else int(seed)) & 0xFFFFFFFFFFFFFFFF,
                                        self.epoch & 0xFFFFFFFF, N.C.byref(self._out),
                                        self._stream()))
+        if count is not None and count.data_ptr() == self.done_count.data_ptr():
+            self._count_zero = True  # the reset kernel consumed it
 
     def reset_done(self, regen_won=False, seed=None):
-        """Auto-reset: reset every instance of the last step's done list (device-side list)."""
+        """Auto-reset every instance whose last step ended terminated|truncated (flag scan, no
+        list); with regen_won the winners get a new maze first (win -> update_maze)."""
+        if regen_won:
+            self.epoch += 1
+        N.check(self.lib.mz_reset_done(self._h, int(bool(regen_won)),
+                                       (self.seed if seed is None else int(seed)) & 0xFFFFFFFFFFFFFFFF,
+                                       self.epoch & 0xFFFFFFFF, N.C.byref(self._out),
+                                       self._stream()))
+
+    def reset_done_list(self, regen_won=False, seed=None):
+        """Auto-reset from the step's device done list (consumes done_count)."""
         self.reset_list(self.done_idx, self.done_count, regen_won=regen_won, seed=seed)
 
     def step(self, actions):
@@ -145,6 +159,20 @@ class VectorMazeEnv:
             actions.to(device=self.device, dtype=torch.int32)
         a = a.contiguous()
         N.check(self.lib.mz_step(self._h, a.data_ptr(), N.C.byref(self._out), self._stream()))
+        self._count_zero = False
+        return self.obs(), self.reward, self.truncated, self.terminated, {}
+
+    def step_act(self, eps=1.0, greedy=None, seed=0, counter=0, actions_out=None):
+        """Fused epsilon-greedy act + step in one launch (actions taken -> actions_out)."""
+        out = self.actions if actions_out is None else actions_out
+        eps_t = eps if torch.is_tensor(eps) else None
+        g = None if greedy is None else greedy.to(dtype=torch.int64).contiguous()
+        flags = N.MZ_STEP_COUNT_ZEROED if self._count_zero else 0
+        N.check(self.lib.mz_step_act(self._h, _ptr(eps_t), float(eps) if eps_t is None else 0.0,
+                                     _ptr(g), seed & 0xFFFFFFFFFFFFFFFF,
+                                     counter & 0xFFFFFFFFFFFFFFFF, out.data_ptr(),
+                                     N.C.byref(self._out), flags, self._stream()))
+        self._count_zero = False
         return self.obs(), self.reward, self.truncated, self.terminated, {}
 
     def obs(self):

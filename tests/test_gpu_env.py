@@ -167,3 +167,61 @@ def test_rejects_reference_crash_shapes(mazerl):
         mazerl.VectorMazeEnv(4, 40, enrich=False)  # even N: reference IndexError (Q4)
     with pytest.raises(ValueError):
         mazerl.VectorMazeEnv(4, 9, enrich=True)  # euclidean window with N < 15 (Q7)
+
+
+@pytest.mark.parametrize("tor,dim", [(False, 41), (True, 29)])
+def test_fused_step_act_matches_separate(mazerl, tor, dim):
+    """mz_step_act (one launch) == mz_act + mz_step, including done lists and auto-resets."""
+    B = 3000
+    e1 = mazerl.VectorMazeEnv(B, dim, toroidal=tor, enrich=True, reward64=True, seed=99)
+    e2 = mazerl.VectorMazeEnv(B, dim, toroidal=tor, enrich=True, reward64=True, seed=99)
+    for k in range(120):
+        a = e1.act(eps=1.0, seed=5, counter=k).clone()
+        e1.step(a)
+        e2.step_act(eps=1.0, seed=5, counter=k)
+        assert torch.equal(e2.actions, a)
+        for name in ("reward64", "terminated", "truncated", "pos", "best_dir", "obs6", "window",
+                     "window_bits"):
+            assert torch.equal(getattr(e1, name), getattr(e2, name)), (k, name)
+        c1, c2 = int(e1.done_count.item()), int(e2.done_count.item())
+        assert c1 == c2
+        assert sorted(e1.done_idx[:c1].tolist()) == sorted(e2.done_idx[:c2].tolist())
+        e1.reset_done()        # flag-scan auto-reset
+        e2.reset_done_list()   # device-list auto-reset (consumes the count)
+        assert int(e2.done_count.item()) == 0
+        for name in ("obs6", "window", "window_bits"):
+            assert torch.equal(getattr(e1, name), getattr(e2, name)), (k, name)
+    e1.close(); e2.close()
+
+
+def test_regen_on_win(mazerl):
+    """win -> new maze (regen_won): a won instance gets a different maze of the same size whose
+    tables are consistent (oracle goal/max_steps), others keep theirs."""
+    import pyoracle as O
+    B, dim = 256, 15
+    env = mazerl.VectorMazeEnv(B, dim, enrich=True, seed=1234)
+    grids0 = [env.grid(i) for i in range(B)]
+    won = set()
+    for k in range(400):
+        # follow "best dir" greedily: a = action whose delta == -best_dir
+        bd = env.best_dir.long()
+        dr, dc = -bd[:, 0], -bd[:, 1]
+        greedy = torch.where(dr == 1, 0, torch.where(dr == -1, 1, torch.where(dc == 1, 2, 3)))
+        env.step_act(eps=0.0, greedy=greedy, seed=1, counter=k)
+        won |= set(torch.nonzero(env.terminated).flatten().tolist())
+        env.reset_done(regen_won=True)
+        if len(won) >= 32:
+            break
+    assert len(won) >= 32
+    torch.cuda.synchronize()
+    changed = 0
+    for i in range(B):
+        g = env.grid(i)
+        if i in won:
+            changed += not np.array_equal(g, grids0[i])
+            q = env.query(i)
+            h = g.copy(); h[h == 2] = 1
+            assert O.goal_select(h, (q["start_r"], q["start_c"])) == (q["goal_r"], q["goal_c"])
+            assert q["max_steps"] == O.max_steps(g, (q["start_r"], q["start_c"]), (q["goal_r"], q["goal_c"]))
+    assert changed >= len(won) - 1
+    env.close()
