@@ -1,0 +1,199 @@
+"""DQN / DDQN learners.
+
+q_loss()            the Q-learning loss of DQNAgent.optimize_model (agents/dqn_agent.py:121-157)
+                    and DDQNAgent.optimize_model (agents/ddqn_agent.py:113-152), term for term:
+                    Q(s,a) = source(s).gather(a); target = r + gamma * V(s'), V = max_a' target(s')
+                    (DQN) or target(s')[argmax source(s')] (DDQN); NO terminal masking — the
+                    reference never stores None next states, so terminal transitions bootstrap
+                    (SURVEY Q12); mse_loss(mean). Network calls happen in the reference's order
+                    (source(s), [source(s')], target(s')) so dropout draws line up on CPU.
+learner_update()    backward, grad.clamp_(-1, 1) on every parameter, optimizer.step().
+DQNAgent/DDQNAgent  single-env drop-ins with the reference constructor and methods
+                    (get_action/memorize/optimize_model/scheduler_step/has_to_update/
+                    update_target/update_steps_done/update_hyperparameter/calculate_epsilon).
+VectorDQNLearner    the MI355X learner for VectorMazeEnv: device replay (HBM), batched fused
+                    act, K updates per vector step, optional DDP gradient all-reduce (RCCL) with
+                    the clamp applied after averaging (single-GPU semantics).
+"""
+import math
+import random
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+import torch.optim as optim
+from torch.optim import lr_scheduler
+
+from ..replay import ReplayMemory, Transition
+from .nets import QNet
+
+
+def q_loss(source, target, state, action, reward, next_state, gamma, double):
+    """Loss of optimize_model for a batch: state = (obs6 [B,6], window [B,3,15,15])."""
+    q_sa = source(state).gather(1, action.view(-1, 1))
+    if double:
+        best = source(next_state).max(1)[1].unsqueeze(1)
+        v_next = target(next_state).gather(1, best).squeeze(1).detach()
+    else:
+        v_next = target(next_state).max(1)[0].detach()
+    expected = (v_next * gamma) + reward
+    return F.mse_loss(q_sa, expected.unsqueeze(1))
+
+
+def learner_update(net, optimizer, loss, clamp=1.0, allreduce=None):
+    optimizer.zero_grad()
+    loss.backward()
+    if allreduce is not None:
+        allreduce(net)  # average grads over ranks, then clamp (single-GPU semantics)
+    for p in net.parameters():
+        p.grad.data.clamp_(-clamp, clamp)
+    optimizer.step()
+
+
+class _AgentBase:
+    VARIANT = "dqn"
+    T_MAX = 100
+
+    def __init__(self, env, learning_rate, starting_epsilon, final_epsilon, epsilon_decay,
+                 discount_factor, eta, batch_size, memory_size, target_update_frequency, device,
+                 hidden_dim=1024, h_channels=32):
+        self.env = env
+        self.device = device
+        self.learning_rate = learning_rate
+        self.starting_epsilon = starting_epsilon
+        self.final_epsilon = final_epsilon
+        self.epsilon_decay = epsilon_decay
+        self.discount_factor = discount_factor
+        self.batch_size = batch_size
+        self.target_update_frequency = target_update_frequency
+        self.eta = eta
+        n_actions = env.action_space.n
+        observation, _ = env.reset()
+        n_obs = len(np.concatenate([observation[k] for k in observation if k != "window"]))
+        self.source_net = QNet(3, n_obs, n_actions, h_channels, hidden_dim, self.VARIANT).to(device)
+        self.target_net = QNet(3, n_obs, n_actions, h_channels, hidden_dim, self.VARIANT).to(device)
+        self.memory = ReplayMemory(memory_size)
+        self.optimizer = optim.AdamW(self.source_net.parameters(), learning_rate)
+        self.lr_scheduler = lr_scheduler.CosineAnnealingLR(self.optimizer, T_max=self.T_MAX, eta_min=1e-5)
+        self.steps_done = 0
+
+    def memorize(self, *args):
+        self.memory.push(*args)
+
+    def calculate_epsilon(self):
+        return self.final_epsilon + (self.starting_epsilon - self.final_epsilon) * \
+            math.exp(-1. * self.steps_done / self.epsilon_decay)
+
+    def get_action(self, state):
+        sample = random.random()
+        eps = self.calculate_epsilon()
+        self.steps_done += 1
+        if sample < eps:
+            mask_dir = self.env.env.get_mask_direction(probs=True)
+            ps = mask_dir / mask_dir.sum()
+            return torch.tensor(np.random.choice(len(ps), p=ps), device=self.device, dtype=torch.long)
+        with torch.no_grad():
+            return self.source_net(state).max(1)[1].view(1, 1)
+
+    def optimize_model(self):
+        if len(self.memory) < self.batch_size:
+            return
+        transitions = self.memory.sample(self.batch_size)
+        batch = Transition(*zip(*transitions))
+        next_states = (torch.cat([s[0] for s in batch.next_state]), torch.cat([s[1] for s in batch.next_state]))
+        state_batch = (torch.cat([s[0] for s in batch.state]), torch.cat([s[1] for s in batch.state], dim=0))
+        device = state_batch[0].device
+        action_batch = torch.tensor(batch.action).to(device)
+        reward_batch = torch.tensor(batch.reward).to(device)
+        loss = q_loss(self.source_net, self.target_net, state_batch, action_batch, reward_batch,
+                      next_states, self.discount_factor, self.VARIANT == "ddqn")
+        ret = loss.item()
+        learner_update(self.source_net, self.optimizer, loss)
+        return ret
+
+    def scheduler_step(self):
+        self.lr_scheduler.step()
+
+    def has_to_update(self, episode):
+        return episode % self.target_update_frequency == 0
+
+    def update_target(self):
+        self.target_net.load_state_dict(self.source_net.state_dict())
+
+    def update_steps_done(self):
+        self.steps_done = 0
+
+    def update_hyperparameter(self, is_better):
+        self.discount_factor = self.discount_factor + (self.eta if is_better else -self.eta)
+
+
+class DQNAgent(_AgentBase):
+    VARIANT, T_MAX = "dqn", 100       # dqn_agent.py:98
+
+
+class DDQNAgent(_AgentBase):
+    VARIANT, T_MAX = "ddqn", 150      # ddqn_agent.py:270
+
+
+# ---------------------------------------------------------------------------------------------
+class VectorDQNLearner:
+    """Batched DQN/DDQN learner on one GPU (optionally one DDP rank).
+
+    Defaults follow the reference's DDQN script (training_examples/.../test_ddqn.py:20-35):
+    lr 1e-3, eps 0.95 -> 0.1, decay ((N-1)^2 // 2) * 5, gamma 0.7, batch 128, AdamW, cosine LR.
+    Vectorisation policy (documented deviations): epsilon is per instance
+    (steps_done per instance, reset to 0 on that instance's win, off_policy_trainer.py:192);
+    gamma drift (Q15) is off by default; the cosine schedule and the target sync advance per
+    `updates_per_epoch` updates instead of per episode; K updates per vector step.
+    """
+
+    def __init__(self, num_envs, device, variant="ddqn", lr=1e-3, eps_start=0.95, eps_final=0.1,
+                 eps_decay=8000.0, gamma=0.7, batch_size=128, capacity=1_000_000,
+                 updates_per_step=1, target_every=100, hidden_dim=1024, h_channels=32,
+                 act_bf16=True, t_max=150, updates_per_epoch=100, allreduce=None, seed=0):
+        self.device = torch.device(device)
+        torch.manual_seed(seed)
+        self.variant = variant
+        self.source = QNet(3, 6, 4, h_channels, hidden_dim, variant).to(self.device)
+        self.target = QNet(3, 6, 4, h_channels, hidden_dim, variant).to(self.device)
+        self.target.load_state_dict(self.source.state_dict())
+        self.opt = optim.AdamW(self.source.parameters(), lr)
+        self.sched = lr_scheduler.CosineAnnealingLR(self.opt, T_max=t_max, eta_min=1e-5)
+        from ..replay import DeviceReplay
+        self.replay = DeviceReplay(capacity, self.device)
+        self.gamma, self.batch_size = gamma, batch_size
+        self.eps_start, self.eps_final, self.eps_decay = eps_start, eps_final, eps_decay
+        self.updates_per_step, self.target_every = updates_per_step, target_every
+        self.updates_per_epoch = updates_per_epoch
+        self.act_bf16 = act_bf16
+        self.allreduce = allreduce
+        self.steps_done = torch.zeros(num_envs, dtype=torch.float32, device=self.device)
+        self.n_updates = 0
+        self.last_loss = torch.zeros((), device=self.device)
+
+    def epsilon(self):
+        return self.eps_final + (self.eps_start - self.eps_final) * torch.exp(-self.steps_done / self.eps_decay)
+
+    @torch.no_grad()
+    def greedy(self, obs6, window):
+        if self.act_bf16 and self.device.type == "cuda":
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                q = self.source((obs6, window))
+        else:
+            q = self.source((obs6, window))
+        return q.float().argmax(1)
+
+    def update(self, expand):
+        if len(self.replay) < self.batch_size:
+            return None
+        for _ in range(self.updates_per_step):
+            state, a, r, nxt = self.replay.sample(self.batch_size, expand)
+            loss = q_loss(self.source, self.target, state, a, r, nxt, self.gamma, self.variant == "ddqn")
+            learner_update(self.source, self.opt, loss, allreduce=self.allreduce)
+            self.last_loss = loss.detach()
+            self.n_updates += 1
+            if self.n_updates % self.target_every == 0:
+                self.target.load_state_dict(self.source.state_dict())
+            if self.n_updates % self.updates_per_epoch == 0:
+                self.sched.step()
+        return self.last_loss

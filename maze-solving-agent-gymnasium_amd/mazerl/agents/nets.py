@@ -1,0 +1,62 @@
+"""Q-networks with the reference's exact architecture and parameter layout.
+
+`QNet(variant="dqn")`  == agents/dqn_agent.py:19-57 (DQN): Conv2d(3->h,3x3,p1) -> LeakyReLU ->
+                          MaxPool2d(2) -> flatten || obs -> Linear -> LeakyReLU -> Linear ->
+                          LeakyReLU -> Linear; conv weight Xavier-uniform (:43-45).
+`QNet(variant="ddqn")` == agents/ddqn_agent.py:18-52: adds Dropout(0.2) after the conv
+                          activation and uses ReLU in the second hidden layer; no Xavier init.
+Module names (conv.0, fc.0, fc.2, fc.4) match the reference so state_dicts interchange.
+With window 15x15, h=32: 1568 conv features + 6 obs -> 1574 -> 1024 -> 512 -> 4
+(2,140,548 parameters, 4,665,024 FLOP per sample forward).
+
+On MI355X the three Linear layers are plain GEMMs and go through hipBLASLt (f32 in/out runs on
+the f32 MFMA at the f32 rate, bit-exact f32; `autocast(bf16)` puts them on the bf16 MFMA for
+acting). The conv front-end is MIOpen.
+"""
+import torch
+import torch.nn as nn
+
+WINDOW = (15, 15)
+
+
+class QNet(nn.Module):
+    def __init__(self, in_channels=3, n_observations=6, n_actions=4, h_channels=32,
+                 hidden_dim=1024, variant="dqn"):
+        super().__init__()
+        self.in_channels = in_channels
+        self.variant = variant
+        conv = [nn.Conv2d(in_channels, h_channels, kernel_size=3, stride=1, padding=1), nn.LeakyReLU()]
+        if variant == "ddqn":
+            conv.append(nn.Dropout(p=0.2))
+        conv.append(nn.MaxPool2d(2, 2))
+        self.conv = nn.Sequential(*conv)
+        conv_out = h_channels * (WINDOW[0] // 2) * (WINDOW[1] // 2)
+        act2 = nn.ReLU() if variant == "ddqn" else nn.LeakyReLU()
+        self.fc = nn.Sequential(
+            nn.Linear(conv_out + n_observations, hidden_dim),
+            nn.LeakyReLU(),
+            nn.Linear(hidden_dim, hidden_dim // 2),
+            act2,
+            nn.Linear(hidden_dim // 2, n_actions),
+        )
+        if variant == "dqn":
+            for layer in self.conv:
+                if isinstance(layer, nn.Conv2d):
+                    nn.init.xavier_uniform_(layer.weight)
+
+    def forward(self, x):
+        s, w = x
+        fw = self.conv(w)
+        fw = fw.view(fw.shape[0], -1)
+        return self.fc(torch.cat((fw, s), dim=1))
+
+
+def count_params(net):
+    return sum(p.numel() for p in net.parameters())
+
+
+def forward_flops(h_channels=32, hidden_dim=1024, n_obs=6, n_actions=4, in_channels=3):
+    """FLOP per sample of one forward (multiply-add = 2 FLOP), conv counted at full 15x15."""
+    conv = 2 * in_channels * 9 * h_channels * WINDOW[0] * WINDOW[1]
+    d0 = h_channels * (WINDOW[0] // 2) * (WINDOW[1] // 2) + n_obs
+    return conv + 2 * (d0 * hidden_dim + hidden_dim * (hidden_dim // 2) + (hidden_dim // 2) * n_actions)

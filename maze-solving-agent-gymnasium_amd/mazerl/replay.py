@@ -1,0 +1,92 @@
+"""Replay memories.
+
+ReplayMemory   — the reference's deque + random.sample memory (lib/replay_memory.py:8-24), kept
+                 for the single-env drop-in agents (bit-for-bit the same sampling with the same
+                 global `random` state).
+DeviceReplay   — the vectorised learner's ring buffer, resident in HBM as structure-of-arrays:
+                 obs6 f32[C,6], window bits i32[C,22] (675-bit 3x15x15 window, 88 B instead of
+                 the 2,700 B f32 tensor), action i64[C], reward f32[C], and the next-state pair.
+                 push() takes a whole vector step at once (index_copy into the ring); sample()
+                 draws uniform indices on the device and expands the windows with the HIP
+                 kernel of libmazerl (mz_expand_window). Sampling is with replacement (the
+                 reference's random.sample is without; at C >> batch the difference is a few
+                 duplicate rows per batch — documented deviation).
+"""
+import random
+from collections import deque, namedtuple
+
+import torch
+
+Transition = namedtuple("Transition", ("state", "action", "reward", "next_state"))
+
+
+class ReplayMemory:
+    def __init__(self, capacity):
+        self.memory = deque([], maxlen=capacity)
+
+    def push(self, *args):
+        self.memory.append(Transition(*args))
+
+    def sample(self, batch_size):
+        return random.sample(self.memory, batch_size)
+
+    def clear_memory(self):
+        self.memory.clear()
+
+    def __len__(self):
+        return len(self.memory)
+
+
+class DeviceReplay:
+    def __init__(self, capacity, device, obs_dim=6, window_words=22):
+        self.capacity = int(capacity)
+        self.device = torch.device(device)
+        C, kw = self.capacity, dict(device=self.device)
+        self.s6 = torch.zeros(C, obs_dim, dtype=torch.float32, **kw)
+        self.sw = torch.zeros(C, window_words, dtype=torch.int32, **kw)
+        self.a = torch.zeros(C, dtype=torch.int64, **kw)
+        self.r = torch.zeros(C, dtype=torch.float32, **kw)
+        self.s6n = torch.zeros(C, obs_dim, dtype=torch.float32, **kw)
+        self.swn = torch.zeros(C, window_words, dtype=torch.int32, **kw)
+        self.ptr = 0
+        self.size = 0
+        self._gen = torch.Generator(device=self.device)
+        self._gen.manual_seed(0x5EED)
+
+    def __len__(self):
+        return self.size
+
+    def nbytes(self):
+        return sum(t.numel() * t.element_size() for t in (self.s6, self.sw, self.a, self.r, self.s6n, self.swn))
+
+    def push(self, s6, sw, a, r, s6n, swn, mask=None):
+        """Append n transitions (device tensors with leading dim n); mask selects rows to keep."""
+        if mask is not None:
+            keep = torch.nonzero(mask, as_tuple=False).flatten()
+            s6, sw, a, r, s6n, swn = (t.index_select(0, keep) for t in (s6, sw, a, r, s6n, swn))
+        n = s6.shape[0]
+        if n == 0:
+            return
+        if n > self.capacity:
+            s6, sw, a, r, s6n, swn = (t[-self.capacity:] for t in (s6, sw, a, r, s6n, swn))
+            n = self.capacity
+        idx = (torch.arange(n, device=self.device) + self.ptr) % self.capacity
+        self.s6.index_copy_(0, idx, s6)
+        self.sw.index_copy_(0, idx, sw)
+        self.a.index_copy_(0, idx, a.to(torch.int64))
+        self.r.index_copy_(0, idx, r.to(torch.float32))
+        self.s6n.index_copy_(0, idx, s6n)
+        self.swn.index_copy_(0, idx, swn)
+        self.ptr = (self.ptr + n) % self.capacity
+        self.size = min(self.size + n, self.capacity)
+
+    def sample_indices(self, batch):
+        return torch.randint(0, self.size, (batch,), device=self.device, generator=self._gen)
+
+    def sample(self, batch, expand):
+        """Returns ((s6, window), a, r, (s6', window')) with f32 windows from `expand(bits)`."""
+        i = self.sample_indices(batch)
+        bits = torch.cat((self.sw.index_select(0, i), self.swn.index_select(0, i)), 0)
+        w = expand(bits)
+        return ((self.s6.index_select(0, i), w[:batch]), self.a.index_select(0, i),
+                self.r.index_select(0, i), (self.s6n.index_select(0, i), w[batch:]))
