@@ -38,7 +38,37 @@ def parse():
     ap.add_argument("--algo", default="r-prim")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="cpu_baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--train-steps", type=int, default=600,
+                    help="DDQN vector steps for the win-rate half of the metric (0 = skip)")
+    ap.add_argument("--eval-mazes", type=int, default=1000)
     return ap.parse_args()
+
+
+def win_rate(a, dev):
+    """Second half of the metric: train DDQN (reference DDQN net/loss, vectorised) on the same
+    config, then the win-rate on `eval_mazes` fresh mazes, greedy and with the reference's
+    epsilon (0.1) protocol (off_policy_trainer.py:228-263)."""
+    import torch
+    from mazerl import VectorMazeEnv
+    from mazerl.agents.dqn import VectorDQNLearner
+    from mazerl.trainers.vector_trainer import VectorOffPolicyTrainer, evaluate
+    env = VectorMazeEnv(a.envs, a.dim, enrich=True, device=dev, algorithm=a.algo, seed=0xA11CE,
+                        done_list=False)
+    decay = ((a.dim - 1) * (a.dim - 1) // 2) * 5 / 40.0
+    L = VectorDQNLearner(a.envs, dev, variant="ddqn", lr=1e-3, eps_start=0.95, eps_final=0.1,
+                         eps_decay=decay, gamma=0.7, batch_size=512, capacity=2_000_000,
+                         updates_per_step=4, target_every=50)
+    tr = VectorOffPolicyTrainer(env, L, seed=3)
+    tr.train(20)  # warm-up: MIOpen / hipBLASLt first calls
+    secs = tr.train(a.train_steps)
+    g, _ = evaluate(L, a.eval_mazes, a.dim, a.algo, seed=0x7E570000, eps=0.0, device=dev)
+    e, _ = evaluate(L, a.eval_mazes, a.dim, a.algo, seed=0x7E570000, eps=0.1, device=dev)
+    env.close()
+    return {"greedy": g, "eps_0.1": e, "eval_mazes": a.eval_mazes, "variant": "ddqn",
+            "train_vector_steps": a.train_steps + 20, "train_seconds_steady": round(secs, 3),
+            "train_env_steps_per_s": a.envs * a.train_steps / secs,
+            "updates": L.n_updates, "batch": 512,
+            "note": "fresh GPU-generated mazes never seen in training (test(new=True) protocol)"}
 
 
 def cpu_baseline(env, seconds):
@@ -155,8 +185,11 @@ def main():
         }
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(env, a.cpu_seconds)
-        print(json.dumps(out), flush=True)
     env.close()
+    if rank == 0:
+        if world == 1 and a.train_steps > 0:
+            out["win_rate"] = win_rate(a, dev)
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

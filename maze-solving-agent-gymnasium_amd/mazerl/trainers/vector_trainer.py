@@ -1,0 +1,102 @@
+"""Vectorised off-policy trainer and win-rate evaluation on VectorMazeEnv.
+
+VectorOffPolicyTrainer.train() is NeuralOffPolicyTrainer.train (lib/trainers/off_policy_trainer.py
+:144-225) over B instances at once. Per vector step:
+  greedy  = argmax Q_source(obs)                      (bf16 MFMA GEMMs, dqn_agent.py:113-116)
+  step    = fused epsilon-greedy act + env step       (one k_step launch, per-instance epsilon)
+  replay  <- (s, a, r, s') for every instance, s' = the step's (terminal) observation; terminal
+             transitions bootstrap like the reference's
+  bookkeeping: steps_done += 1, = 0 on a win (off_policy_trainer.py:192); wins/episodes counters
+  auto-reset: winners get a new maze (update_maze, :202), truncated instances restart the same
+             maze (reset, :153) — one flag-scan kernel
+  K learner updates (replay ratio), target sync / cosine step per update count.
+evaluate() is NeuralOffPolicyTrainer.test(new=True)/infer (:228-299): fresh mazes, one episode
+each, win = terminated; greedy (eps = 0) or the reference's epsilon protocol (Q14).
+"""
+import time
+
+import torch
+
+from ..vector_env import ALGOS, VectorMazeEnv
+
+
+class VectorOffPolicyTrainer:
+    def __init__(self, env, learner, seed=0, regen_won=True, curriculum=False, allreduce_stats=None):
+        self.env, self.learner = env, learner
+        self.seed = seed
+        self.regen_won = regen_won
+        self.curriculum = curriculum
+        self.allreduce_stats = allreduce_stats
+        dev = env.device
+        self.wins = torch.zeros((), dtype=torch.int64, device=dev)
+        self.episodes = torch.zeros((), dtype=torch.int64, device=dev)
+        self.inst_wins = torch.zeros(env.num_envs, dtype=torch.int32, device=dev)
+        self.counter = 0
+        self.history = []
+
+    def _expand(self, bits):
+        return self.env.expand_window(bits)
+
+    def vector_step(self):
+        env, L = self.env, self.learner
+        greedy = L.greedy(env.obs6, env.window)
+        s6 = env.obs6.clone()
+        sw = env.window_bits.clone()
+        env.step_act(eps=L.epsilon(), greedy=greedy, seed=self.seed, counter=self.counter)
+        self.counter += 1
+        L.replay.push(s6, sw, env.actions, env.reward, env.obs6, env.window_bits)
+        term = env.terminated.bool()
+        done = term | env.truncated.bool()
+        L.steps_done += 1
+        L.steps_done.masked_fill_(term, 0)
+        self.wins += term.sum()
+        self.episodes += done.sum()
+        if self.curriculum:  # change_algorithm (off_policy_trainer.py:302-310), per instance
+            self.inst_wins += term.to(torch.int32)
+            algo = torch.where(self.inst_wins >= 10, ALGOS["dfs"],
+                               torch.where(self.inst_wins >= 5, ALGOS["prim&kill"], ALGOS["r-prim"]))
+            env.set_algorithm(algo.to(torch.uint8))
+        env.reset_done(regen_won=self.regen_won)
+        return L.update(self._expand)
+
+    def train(self, vector_steps, log_every=0, log=print):
+        t0 = time.perf_counter()
+        for k in range(vector_steps):
+            loss = self.vector_step()
+            if log_every and (k + 1) % log_every == 0:
+                torch.cuda.synchronize()
+                rec = dict(step=k + 1, wins=int(self.wins), episodes=int(self.episodes),
+                           loss=float(loss) if loss is not None else None,
+                           eps_mean=float(self.learner.epsilon().mean()),
+                           seconds=round(time.perf_counter() - t0, 2))
+                self.history.append(rec)
+                if log:
+                    log(rec)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+
+@torch.no_grad()
+def evaluate(learner, num_mazes, dim, algorithm="r-prim", seed=0x7E57, eps=0.0, toroidal=False,
+             device=None, max_vector_steps=None):
+    """Fraction of `num_mazes` fresh mazes solved in one episode (terminated before truncation)."""
+    env = VectorMazeEnv(num_mazes, dim, toroidal=toroidal, enrich=True, device=device,
+                        algorithm=algorithm, seed=seed, done_list=False, pos=False)
+    finished = torch.zeros(num_mazes, dtype=torch.bool, device=env.device)
+    won = torch.zeros(num_mazes, dtype=torch.bool, device=env.device)
+    limit = max_vector_steps or (dim - 1) * (dim - 1) + 2  # > any max_steps
+    k = 0
+    while k < limit:
+        greedy = learner.greedy(env.obs6, env.window)
+        acts = env.act(eps=eps, greedy=greedy, seed=seed, counter=k)
+        acts = torch.where(finished, torch.full_like(acts, -1), acts)
+        env.step(acts)
+        term = env.terminated.bool()
+        won |= term & ~finished
+        finished |= term | env.truncated.bool()
+        k += 1
+        if k % 32 == 0 and bool(finished.all()):
+            break
+    rate = float(won.float().mean())
+    env.close()
+    return rate, k
