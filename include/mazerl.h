@@ -154,6 +154,13 @@ int mz_expand_window(const uint32_t* bits_dev, float* out_dev, int32_t n, void* 
  * the reference, base_maze_env.py:17,60-64; here it is per instance). algo_dev [B] or NULL. */
 int mz_set_algorithm(mz_handle* h, const uint8_t* algo_dev, int32_t algo_all, void* stream);
 
+/* McClendon difficulty of a maze (host computation, synchronous): ComplexityEvaluation(maze,
+ * start, goal).difficulty_of_maze() (maze_complexity_evaluation.py:38-329) for a euclidean grid
+ * (toroidal mazes: pass the bordered (N+2) grid, as gen_maze_no_border does, :37-56).
+ * Used by get_maze_difficulty (base_maze_env.py:99-105) and best-of-6 generation (:78-97). */
+int mz_difficulty(const uint8_t* grid_host, int32_t h, int32_t w, int32_t sr, int32_t sc,
+                  int32_t gr, int32_t gc, double* out_host);
+
 /* Synchronous host snapshots for the single-env drop-in classes. */
 int mz_query(mz_handle* h, int32_t env, mz_env_info* info_host);
 int mz_get_grid(mz_handle* h, int32_t env, uint8_t* grid_host /* [n][n] */);

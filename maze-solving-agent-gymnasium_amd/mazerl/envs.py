@@ -14,8 +14,8 @@ Randomness: like the reference, mazes depend on Python's global `ra
 each new maze's Philox seed is random.getrandbits(64); `random.seed(s)` before construction makes
 an env reproducible. `reset(seed=...)` ignores the seed, as the reference does. The algorithm is
 the class-wide BaseMazeEnv.ALGORITHM (set_algorithm changes it for every env, base_maze_env.py:60).
-Generation uses one candidate (the reference keeps the easiest of 6 by McClendon difficulty,
-base_maze_env.py:78-97; documented deviation until the difficulty port lands).
+New mazes follow the reference's best-of-6 rule (base_maze_env.py:78-97): six GPU-generated
+candidates, the first with the smallest McClendon difficulty (native mz_difficulty) is kept.
 """
 import random
 
@@ -60,6 +60,7 @@ class BaseMazeEnv(_EnvBase):
     ENRICH = False
     VARIABLE = False
     START_SHAPE = None
+    CANDIDATES = 6  # best-of-6 by difficulty, as the reference; set 1 for single-candidate
 
     def __init__(self, maze_shape, render_mode="human", device=None, _maze=None):
         self.render_mode = render_mode
@@ -106,10 +107,27 @@ class BaseMazeEnv(_EnvBase):
         self.maze_map = self._venv.grid(0).astype(int).tolist()
         self.maze_shape = (q["n"], q["n"])
 
+    def _difficulty_of_current(self):
+        from .difficulty import maze_difficulty, toroidal_difficulty
+        fn = toroidal_difficulty if self.TOROIDAL else maze_difficulty
+        return fn(np.array(self.maze_map, np.uint8), self._start_pos,
+                  tuple(int(x) for x in self._target_location))
+
     def _new_maze(self, n):
-        seed = random.getrandbits(64)
-        self._venv.generate(algorithm=ALGOS[BaseMazeEnv.ALGORITHM], dim=n, seed=seed)
-        self._pull()
+        """generate_maze (base_maze_env.py:78-97, toroidal_maze_env.py:40-54): CANDIDATES mazes
+        generated on the GPU, the first with the smallest McClendon difficulty is kept."""
+        best = None
+        for _ in range(max(1, self.CANDIDATES)):
+            seed = random.getrandbits(64)
+            self._venv.generate(algorithm=ALGOS[BaseMazeEnv.ALGORITHM], dim=n, seed=seed)
+            self._pull()
+            if self.CANDIDATES <= 1:
+                return
+            d = self._difficulty_of_current()
+            if best is None or d < best[0]:
+                best = (d, np.array(self.maze_map, np.uint8), self._start_pos,
+                        tuple(int(x) for x in self._target_location))
+        self._load(best[1], best[2], best[3])
 
     def _load(self, grid, start, goal):
         grid = np.asarray(grid, np.uint8)
@@ -188,13 +206,8 @@ class BaseMazeEnv(_EnvBase):
         return getattr(self, "max_shape", self.maze_shape)
 
     def get_maze_difficulty(self):
-        from .difficulty import maze_difficulty
-        grid = np.array(self.maze_map, np.uint8)
-        if self.TOROIDAL:  # evaluated on the bordered maze (off_policy_trainer.py:194-196)
-            grid = np.pad(grid, 1)
-            return maze_difficulty(grid, (self._start_pos[0] + 1, self._start_pos[1] + 1),
-                                   tuple(int(x) + 1 for x in self._target_location))
-        return maze_difficulty(grid, self._start_pos, tuple(int(x) for x in self._target_location))
+        # toroidal mazes are evaluated on the bordered maze (off_policy_trainer.py:194-196)
+        return self._difficulty_of_current()
 
     def set_max_steps(self):
         self.max_steps_taken = self._venv.query(0)["max_steps"]

@@ -1,0 +1,31 @@
+"""Native McClendon difficulty (libmazerl mz_difficulty, host C++) vs the reference's
+ComplexityEvaluation values stored in the golden fixtures (maze_complexity_evaluation.py:319-329).
+CPU-only: mz_difficulty makes no HIP call. Tolerance: 1e-15 relative (the reference sums a
+hallway's 1/(2d) terms in Python-set order inside networkx subgraph views; where that order differs
+from insertion order the last bit can differ); at least 95% of the fixtures must match exactly."""
+import math
+
+import pytest
+
+import golden_io as G
+
+
+@pytest.fixture(scope="module")
+def diff():
+    from mazerl import difficulty
+    from mazerl import _build
+    _build.build()
+    return difficulty
+
+
+def test_difficulty_matches_reference(diff):
+    exact = total = 0
+    for name, fn in (("gen_euclid.npz", diff.maze_difficulty), ("gen_toroid.npz", diff.toroidal_difficulty)):
+        for m in G.mazes(name):
+            if math.isnan(m["difficulty"]):
+                continue
+            d = fn(m["grid"], m["start"], m["goal"])
+            assert d == pytest.approx(m["difficulty"], rel=1e-15, abs=0), (name, m["algo"], m["n"], m["seed"])
+            exact += d == m["difficulty"]
+            total += 1
+    assert total >= 200 and exact >= 0.95 * total

@@ -105,6 +105,30 @@ def test_reference_shaped_training_loop(envs):
     env.close()
 
 
+def test_best_of_6_generation(envs):
+    """generate_maze keeps the first of 6 candidates with the smallest difficulty
+    (base_maze_env.py:78-97); the candidates' seeds come from the global `random` state."""
+    from mazerl import VectorMazeEnv
+    from mazerl.difficulty import maze_difficulty
+    envs.BaseMazeEnv.ALGORITHM = "r-prim"
+    random.seed(77)
+    env = envs.SimpleMazeEnv((21, 21))
+    random.seed(77)
+    seeds = [random.getrandbits(64) for _ in range(6)]
+    v = VectorMazeEnv(1, 21, enrich=False, generate=False)
+    cands = []
+    for s in seeds:
+        v.generate(algorithm="r-prim", dim=21, seed=s)
+        q = v.query(0)
+        g = v.grid(0)
+        cands.append((maze_difficulty(g, (q["start_r"], q["start_c"]), (q["goal_r"], q["goal_c"])), g))
+    best = min(range(6), key=lambda i: (cands[i][0], i))
+    assert np.array_equal(np.array(env.maze_map), cands[best][1])
+    assert env.get_maze_difficulty() == cands[best][0]
+    v.close()
+    env.close()
+
+
 def test_variable_env_growth(envs):
     random.seed(1)
     env = envs.SimpleVariableMazeEnv((23, 23))
