@@ -105,6 +105,32 @@ def test_reference_shaped_training_loop(envs):
     env.close()
 
 
+def test_q_agent_on_dropin_env_matches_reference(envs):
+    """Config 1 plumbing: the tabular QAgent (str(obs) keys) on the GPU drop-in SimpleMazeEnv
+    yields the reference's keys and Q-table for the same op sequence (agents/q_agent.py:56-67)."""
+    from mazerl.agents.q_agent import QAgent
+    fx = G.load("agents.npz")
+    t = [t for t in G.traces() if t["kind"] == G.KIND_SIMPLE][int(fx["q.trace_index"])]
+    env = envs.SimpleMazeEnv.from_maze(t["grid"], t["start"], t["goal"])
+    ag = QAgent(env, learning_rate=0.1, initial_epsilon=0.95, epsilon_decay=40,
+                final_epsilon=0.05, discount_factor=0.7, eta=0.01)
+    obs, _ = env.reset()
+    keys = []
+    for op in t["op"][:600]:
+        if op == 4:
+            obs, _ = env.reset()
+            continue
+        nobs, r, tr, te, _ = env.step(int(op))
+        ag.update(obs, int(op), r, te, nobs)
+        keys.append(str(obs))
+        obs = nobs
+    assert keys == list(fx["q.obs"])
+    assert sorted(ag.q_values) == list(fx["q.keys"])
+    for k, v in zip(fx["q.keys"], fx["q.values"]):
+        np.testing.assert_array_equal(ag.q_values[str(k)], v)
+    env.close()
+
+
 def test_best_of_6_generation(envs):
     """generate_maze keeps the first of 6 candidates with the smallest difficulty
     (base_maze_env.py:78-97); the candidates' seeds come from the global `random` state."""
