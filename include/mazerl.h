@@ -154,6 +154,17 @@ int mz_expand_window(const uint32_t* bits_dev, float* out_dev, int32_t n, void* 
  * the reference, base_maze_env.py:17,60-64; here it is per instance). algo_dev [B] or NULL. */
 int mz_set_algorithm(mz_handle* h, const uint8_t* algo_dev, int32_t algo_all, void* stream);
 
+/* Per-instance maze metadata into meta_dev [B][6] int32: N, start r, start c, goal r, goal c,
+ * max_steps (the attributes maze_shape/_start_pos/_target_location/max_steps_taken). */
+int mz_get_meta(mz_handle* h, int32_t* meta_dev, void* stream);
+
+/* PPO discounted returns (ppo_agent.py:170-179) for n episodes on the device: episode k is row
+ * rows_dev[k] of rew_dev (float64, leading dim ld) with length lens_dev[k]; out_dev[k*ldo + t] =
+ * float32(sum_j gamma^j r[t+j]) accumulated backwards in float64 like the reference's loop. */
+int mz_discounted_returns(const double* rew_dev, int32_t ld, const int32_t* rows_dev,
+                          const int32_t* lens_dev, int32_t n, double gamma, float* out_dev,
+                          int32_t ldo, void* stream);
+
 /* McClendon difficulty of a maze (host computation, synchronous): ComplexityEvaluation(maze,
  * start, goal).difficulty_of_maze() (maze_complexity_evaluation.py:38-329) for a euclidean grid
  * (toroidal mazes: pass the bordered (N+2) grid, as gen_maze_no_border does, :37-56).

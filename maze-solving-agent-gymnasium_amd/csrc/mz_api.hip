@@ -315,6 +315,22 @@ int mz_set_algorithm(mz_handle* h, const uint8_t* algo_dev, int32_t algo_all, vo
   return MZ_OK;
 }
 
+int mz_get_meta(mz_handle* h, int32_t* meta_dev, void* stream) {
+  if (!h || !meta_dev) return fail(MZ_EINVAL, "bad arguments");
+  DeviceGuard g(h->cfg.device);
+  MZ_HIP(mz_launch_meta(h->d, meta_dev, static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
+int mz_discounted_returns(const double* rew_dev, int32_t ld, const int32_t* rows_dev,
+                          const int32_t* lens_dev, int32_t n, double gamma, float* out_dev,
+                          int32_t ldo, void* stream) {
+  if (!rew_dev || !rows_dev || !lens_dev || !out_dev || n < 0) return fail(MZ_EINVAL, "bad arguments");
+  MZ_HIP(mz_launch_returns(rew_dev, ld, rows_dev, lens_dev, n, gamma, out_dev, ldo,
+                           static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
 int mz_query(mz_handle* h, int32_t env, mz_env_info* info) {
   if (!h || !info || env < 0 || env >= h->d.B) return fail(MZ_EINVAL, "bad arguments");
   DeviceGuard g(h->cfg.device);

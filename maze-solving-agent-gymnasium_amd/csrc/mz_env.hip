@@ -465,6 +465,32 @@ __global__ void k_expand(const uint32_t* bits, float* out, int n) {
   out[t] = (float)((bits[i * MZ_WINDOW_WORDS + (f >> 5)] >> (f & 31)) & 1u);
 }
 
+// Per-instance maze metadata as int32 [B][6]: N, start r/c, goal r/c, max_steps.
+__global__ void k_meta(MzDev d, int32_t* out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= d.B) return;
+  const uint32_t m0 = d.meta0[e], m1 = d.meta1[e];
+  int32_t* o = out + 6 * (size_t)e;
+  o[0] = m0 & 0xFF; o[1] = (m0 >> 16) & 0xFF; o[2] = m0 >> 24;
+  o[3] = m1 & 0xFF; o[4] = (m1 >> 8) & 0xFF; o[5] = m1 >> 16;
+}
+
+// PPO returns (ppo_agent.py:170-179): per episode, backwards, acc = r + acc * gamma in float64
+// (the reference's Python floats), stored as float32 (torch.tensor of the list). One lane per
+// episode; episode `k` is row rows[k] of rew (leading dimension ld), length lens[k].
+__global__ void k_returns(const double* rew, int ld, const int32_t* rows, const int32_t* lens,
+                          int n, double gamma, float* out, int ldo) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const double* r = rew + (size_t)rows[k] * ld;
+  float* o = out + (size_t)k * ldo;
+  double acc = 0.0;
+  for (int t = lens[k] - 1; t >= 0; --t) {
+    acc = __dadd_rn(r[t], __dmul_rn(acc, gamma));
+    o[t] = (float)acc;
+  }
+}
+
 // the build kernels may need more than the 64 KiB default dynamic LDS at large max_dim
 hipError_t mz_lds_attr(const void* fn, size_t bytes) {
   if (bytes <= 65536) return hipSuccess;
@@ -547,6 +573,19 @@ hipError_t mz_launch_reset_done(const MzDev& d, int regen, uint64_t seed, uint32
   if (d.toroidal) { if (d.enrich) MZ_RD(true, true); else MZ_RD(true, false); }
   else { if (d.enrich) MZ_RD(false, true); else MZ_RD(false, false); }
 #undef MZ_RD
+  return hipGetLastError();
+}
+
+hipError_t mz_launch_meta(const MzDev& d, int32_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_meta, dim3((d.B + 255) / 256), dim3(256), 0, s, d, out);
+  return hipGetLastError();
+}
+
+hipError_t mz_launch_returns(const double* rew, int ld, const int32_t* rows, const int32_t* lens,
+                             int n, double gamma, float* out, int ldo, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_returns, dim3((n + 63) / 64), dim3(64), 0, s, rew, ld, rows, lens, n, gamma,
+                     out, ldo);
   return hipGetLastError();
 }
 

@@ -12,6 +12,9 @@ hipError_t mz_launch_step(const MzDev& d, const int32_t* act, const MzAct* ap, c
                           hipStream_t s);
 hipError_t mz_launch_reset_list(const MzDev& d, const int32_t* idx, int32_t* count,
                                 int32_t n_static, const MzOut& o, hipStream_t s);
+hipError_t mz_launch_meta(const MzDev& d, int32_t* out, hipStream_t s);
+hipError_t mz_launch_returns(const double* rew, int ld, const int32_t* rows, const int32_t* lens,
+                             int n, double gamma, float* out, int ldo, hipStream_t s);
 hipError_t mz_launch_reset_done(const MzDev& d, int regen, uint64_t seed, uint32_t epoch,
                                 const MzOut& o, hipStream_t s);
 hipError_t mz_launch_mask(const MzDev& d, int probs, float* out4, hipStream_t s);

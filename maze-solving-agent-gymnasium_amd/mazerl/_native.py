@@ -35,7 +35,7 @@ MZ_ERRORS = {-1: ValueError, -2: ValueError, -3: RuntimeError, -4: MemoryError, 
 EXPORTS = ["mz_last_error", "mz_device_count", "mz_create", "mz_destroy", "mz_load_mazes",
            "mz_generate", "mz_reset_all", "mz_reset_list", "mz_reset_done", "mz_step", "mz_direction_mask",
            "mz_act", "mz_step_act", "mz_expand_window", "mz_set_algorithm", "mz_query", "mz_get_grid",
-           "mz_difficulty"]
+           "mz_difficulty", "mz_get_meta", "mz_discounted_returns"]
 
 _lib = None
 
@@ -75,6 +75,9 @@ def load(build_if_missing=True):
     L.mz_set_algorithm.argtypes = [vp, vp, C.c_int32, vp]
     L.mz_query.argtypes = [vp, C.c_int32, C.POINTER(EnvInfo)]
     L.mz_get_grid.argtypes = [vp, C.c_int32, vp]
+    L.mz_get_meta.argtypes = [vp, vp, vp]
+    L.mz_discounted_returns.argtypes = [vp, C.c_int32, vp, vp, C.c_int32, C.c_double, vp,
+                                        C.c_int32, vp]
     L.mz_difficulty.argtypes = [vp] + [C.c_int32] * 6 + [C.POINTER(C.c_double)]
     for f in EXPORTS:
         if f != "mz_last_error":

@@ -76,12 +76,33 @@ class VectorOffPolicyTrainer:
         return time.perf_counter() - t0
 
 
+def make_env(num_envs, dims, toroidal=False, algorithm="r-prim", seed=0x5EED0000, device=None,
+             **kw):
+    """VectorMazeEnv whose instance i gets maze size dims[i % len(dims)] (variable-size configs)."""
+    dims = [dims] if isinstance(dims, int) else list(dims)
+    env = VectorMazeEnv(num_envs, dims[0], toroidal=toroidal, enrich=True, device=device,
+                        max_dim=max(dims), algorithm=algorithm, seed=seed, generate=len(dims) == 1,
+                        **kw)
+    if len(dims) > 1:
+        ids = torch.arange(num_envs, device=env.device)
+        for j, n in enumerate(dims):
+            sel = ids[ids % len(dims) == j]
+            if sel.numel():
+                algo = algorithm if isinstance(algorithm, str) else torch.as_tensor(algorithm)[sel.cpu()]
+                env.generate(env_ids=sel.to(torch.int32), algorithm=algo, dim=n, seed=seed)
+        env.set_algorithm(algorithm if isinstance(algorithm, str) else torch.as_tensor(algorithm).to(torch.uint8))
+        env.reset()
+    return env
+
+
 @torch.no_grad()
 def evaluate(learner, num_mazes, dim, algorithm="r-prim", seed=0x7E57, eps=0.0, toroidal=False,
              device=None, max_vector_steps=None):
-    """Fraction of `num_mazes` fresh mazes solved in one episode (terminated before truncation)."""
-    env = VectorMazeEnv(num_mazes, dim, toroidal=toroidal, enrich=True, device=device,
-                        algorithm=algorithm, seed=seed, done_list=False, pos=False)
+    """Fraction of `num_mazes` fresh mazes solved in one episode (terminated before truncation).
+    `dim` may be a list of sizes (instance i gets dim[i % len])."""
+    env = make_env(num_mazes, dim, toroidal=toroidal, algorithm=algorithm, seed=seed,
+                   device=device, done_list=False, pos=False)
+    dim = max(dim) if not isinstance(dim, int) else dim
     finished = torch.zeros(num_mazes, dtype=torch.bool, device=env.device)
     won = torch.zeros(num_mazes, dtype=torch.bool, device=env.device)
     limit = max_vector_steps or (dim - 1) * (dim - 1) + 2  # > any max_steps

@@ -206,6 +206,12 @@ class VectorMazeEnv:
         N.check(self.lib.mz_expand_window(bits.data_ptr(), out.data_ptr(), n, self._stream()))
         return out
 
+    def meta(self, out=None):
+        """int32 [B, 6]: N, start r, start c, goal r, goal c, max_steps (device tensor)."""
+        out = out if out is not None else torch.empty(self.num_envs, 6, dtype=torch.int32, device=self.device)
+        N.check(self.lib.mz_get_meta(self._h, out.data_ptr(), self._stream()))
+        return out
+
     # ---------------------------------------------------------------------------------------
     def query(self, i):
         info = N.EnvInfo()
