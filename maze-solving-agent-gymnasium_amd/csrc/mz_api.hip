@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -127,9 +128,11 @@ int mz_create(const mz_config* cfg, mz_handle** out) {
   d.VP = (d.P * d.P + 15) & ~15;
   d.toroidal = cfg->toroidal != 0;
   d.enrich = cfg->enrich != 0;
+  d.NW = (d.P + 31) / 32;
+  d.PW = 2 * d.NW;
   const size_t B = (size_t)d.B, P = (size_t)d.P;
   int rc;
-  if ((rc = alloc(h, &d.cells, B * P * P)) || (rc = alloc(h, &d.planes, B * P * MZ_PLANE_WORDS + 16)) ||
+  if ((rc = alloc(h, &d.cells, B * P * P)) || (rc = alloc(h, &d.planes, B * P * (size_t)d.PW + 16)) ||
       (rc = alloc(h, &d.visits, B * (size_t)d.VP)) || (rc = alloc(h, &d.meta0, B)) ||
       (rc = alloc(h, &d.meta1, B)) || (rc = alloc(h, &d.posw, B)) || (rc = alloc(h, &d.stw, B)) ||
       (rc = alloc(h, &d.curw, B)) || (rc = alloc(h, &d.algo, B)) || (rc = alloc(h, &d.last_term, B)) ||

@@ -334,14 +334,15 @@ __device__ void mz_build_one(const MzDev& d, int e, bool tor, bool generate, int
   }
   // open / visited bit-plane rows, interleaved word pairs; visited = {start} (reset)
   for (int R = lane; R < P; R += 64) {
-    uint32_t w[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    if (R < N)
-      for (int c = 0; c < N; ++c)
-        if (L.g[R * N + c] != 0) w[2 * (c >> 5)] |= 1u << (c & 31);
-    if (R == sr) w[2 * (sc >> 5) + 1] |= 1u << (sc & 31);
-    uint4* row = reinterpret_cast<uint4*>(d.planes + (es * P + R) * MZ_PLANE_WORDS);
-    row[0] = make_uint4(w[0], w[1], w[2], w[3]);
-    row[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    uint2* row = reinterpret_cast<uint2*>(d.planes + (es * P + R) * d.PW);
+    for (int k = 0; k < d.NW; ++k) {
+      uint32_t o = 0u, v = 0u;
+      if (R < N)
+        for (int c = 32 * k; c < N && c < 32 * k + 32; ++c)
+          if (L.g[R * N + c] != 0) o |= 1u << (c & 31);
+      if (R == sr && (sc >> 5) == k) v = 1u << (sc & 31);
+      row[k] = make_uint2(o, v);
+    }
   }
   uint4* v4 = reinterpret_cast<uint4*>(d.visits + es * d.VP);
   for (int i = lane; i < d.VP / 16; i += 64) v4[i] = make_uint4(0u, 0u, 0u, 0u);

@@ -8,9 +8,10 @@
 //                        (_find_best_next_cell base_maze_env.py:224-262, find_path
 //                        simple_maze_env.py:70-79) is a function of the cell: computed once per
 //                        maze, gathered once per step.
-//   planes u32 [B][P][8] per row, interleaved (open, visited) word pairs for columns 32k..32k+31:
-//                        [o0 v0 o1 v1 o2 v2 o3 v3]; visited = the reference's non_visited plane
-//                        inverted (base_maze_env.py:40-41,184). A window row needs 2 x 8 B loads.
+//   planes u32 [B][P][PW] per row, interleaved (open, visited) word pairs for columns 32k..32k+31,
+//                        PW = 2 * ceil(P / 32) (24 B rows at P = 81): [o0 v0 o1 v1 o2 v2];
+//                        visited = the reference's non_visited plane inverted
+//                        (base_maze_env.py:40-41,184). A window row needs 2 x 8 B loads.
 //   visits u8  [B][VP]   entries into each cell since reset (visited_cell.count, :194),
 //                        saturating at 255 (exact: penalties are -1.0 for k >= 188)
 //   SoA per instance (coalesced u32 each):
@@ -22,7 +23,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#define MZ_PLANE_WORDS 8
 #define MZ_CELL_D_MASK 0xFFFFu
 #define MZ_CELL_CODE_SHIFT 16
 #define MZ_CELL_OPEN (1u << 19)
@@ -30,6 +30,7 @@
 
 struct MzDev {
   int B, P, VP, toroidal, enrich;
+  int NW, PW;               // plane words per row per plane (ceil(P/32)) and row pitch (2*NW)
   uint32_t* cells;
   uint32_t* planes;
   uint8_t* visits;
