@@ -53,7 +53,7 @@ def win_rate(a, dev):
     from mazerl.agents.dqn import VectorDQNLearner
     from mazerl.trainers.vector_trainer import VectorOffPolicyTrainer, evaluate
     env = VectorMazeEnv(a.envs, a.dim, enrich=True, device=dev, algorithm=a.algo, seed=0xA11CE,
-                        done_list=False)
+                        done_list=False, window=False, window_bits=True)  # acting reads the bits
     decay = ((a.dim - 1) * (a.dim - 1) // 2) * 5 / 40.0
     L = VectorDQNLearner(a.envs, dev, variant="ddqn", lr=1e-3, eps_start=0.95, eps_final=0.1,
                          eps_decay=decay, gamma=0.7, batch_size=512, capacity=2_000_000,

@@ -150,6 +150,32 @@ int mz_act(mz_handle* h, const float* eps_dev, float eps_all, const int64_t* gre
 /* Expand n packed windows (window_bits layout) to f32 [n][3][15][15]. */
 int mz_expand_window(const uint32_t* bits_dev, float* out_dev, int32_t n, void* stream);
 
+/* Maze bank: regeneration on win (update_maze, simple_maze_env.py:81-94, called from
+ * off_policy_trainer.py:190-202) copies a maze generated ahead of time instead of building one
+ * inside mz_reset_done (one build is a ~1 ms serial chain: carve loop + two level-synchronous
+ * BFS; a copy is a few microseconds). Two banks of `slots` mazes per algorithm in algo_mask
+ * (bit a = algorithm id a), all of size `dim`; the caller consumes one (mz_bank_use) while it
+ * refills the other (mz_bank_fill, e.g. on a side stream ordered after the consuming launches).
+ * Mazes: Philox seed ^ ((3*bank + algo + 1) << 56) + slot + (fill epoch << 32). An exhausted
+ * bank, or an instance whose algorithm / size the bank lacks, falls back to building in place. */
+int mz_bank_create(mz_handle* h, int32_t slots, int32_t dim, uint32_t algo_mask);
+/* Rebuild the slots of `bank` consumed since its last fill (every slot on the first fill). */
+int mz_bank_fill(mz_handle* h, int32_t bank, uint64_t seed, void* stream);
+/* Bank consumed by later mz_reset_done(regen_won) launches; -1 = none (build in place). */
+int mz_bank_use(mz_handle* h, int32_t bank);
+/* Consumed-slot counters of `bank` per algorithm id -> out3_dev [3] int32 (device). */
+int mz_bank_consumed(mz_handle* h, int32_t bank, int32_t* out3_dev, void* stream);
+
+/* Fused conv stem of the DQN/DDQN Q-network for acting (dqn_agent.py:19-57 forward,
+ * ddqn_agent.py:18-52): from n packed windows (window_bits layout) and obs6 [n][6] f32, writes
+ * feat_dev [n][ld] bf16 = [MaxPool2(Dropout(LeakyReLU(Conv3x3(window) + b))) flattened (1,568,
+ * channel-major) | obs6 (6) | zeros], the input row of the first Linear layer.
+ * conv_w_dev f32 [32][3][3][3], conv_b_dev f32 [32]; drop_p = 0 (DQN) or the Dropout p (DDQN in
+ * train mode), masks drawn from (seed, counter); ld in 1576..1600, multiple of 8. */
+int mz_q_front(const uint32_t* bits_dev, const float* obs6_dev, int32_t n, const float* conv_w_dev,
+               const float* conv_b_dev, float drop_p, uint64_t seed, uint64_t counter,
+               uint16_t* feat_dev, int32_t ld, void* stream);
+
 /* Set the per-instance algorithm ids used by regeneration (BaseMazeEnv.ALGORITHM is global in
  * the reference, base_maze_env.py:17,60-64; here it is per instance). algo_dev [B] or NULL. */
 int mz_set_algorithm(mz_handle* h, const uint8_t* algo_dev, int32_t algo_all, void* stream);

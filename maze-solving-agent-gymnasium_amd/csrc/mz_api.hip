@@ -17,12 +17,27 @@
 #include "mz_common.h"
 #include "mz_kernels.h"
 
+struct MzBankStore {  // two banks x the enabled algorithms x K slots (mz_bank_*)
+  int K = 0, dim = 0, nA = 0;
+  uint32_t amask = 0;
+  uint32_t* cells = nullptr;   // [2][nA][K][P*P]
+  uint32_t* planes = nullptr;  // [2][nA][K][P*PW]
+  uint32_t* meta0 = nullptr;   // [2][nA][K]
+  uint32_t* meta1 = nullptr;
+  int* heads = nullptr;        // [2][3] consumed slots per algorithm id
+  uint8_t* s_visits = nullptr; // scratch the build writes and nobody reads: [K][VP], [K] ...
+  uint32_t *s_posw = nullptr, *s_stw = nullptr, *s_curw = nullptr;
+  uint8_t *s_last = nullptr, *s_algo = nullptr;
+  uint32_t epoch[2] = {0u, 0u};
+};
+
 struct mz_handle {
   mz_config cfg;
   MzDev d;
   std::vector<void*> allocs;
   uint8_t* staging = nullptr;
   size_t staging_bytes = 0;
+  MzBankStore bank;
 };
 
 namespace {
@@ -303,6 +318,108 @@ int mz_act(mz_handle* h, const float* eps_dev, float eps_all, const int64_t* gre
 int mz_expand_window(const uint32_t* bits_dev, float* out_dev, int32_t n, void* stream) {
   if (!bits_dev || !out_dev || n < 0) return fail(MZ_EINVAL, "bad arguments");
   MZ_HIP(mz_launch_expand(bits_dev, out_dev, n, static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
+int mz_q_front(const uint32_t* bits_dev, const float* obs6_dev, int32_t n, const float* conv_w_dev,
+               const float* conv_b_dev, float drop_p, uint64_t seed, uint64_t counter,
+               uint16_t* feat_dev, int32_t ld, void* stream) {
+  if (!bits_dev || !obs6_dev || !conv_w_dev || !conv_b_dev || !feat_dev || n < 0)
+    return fail(MZ_EINVAL, "bad arguments");
+  if (ld < 1576 || ld > 1600 || ld % 8 != 0) return fail(MZ_EINVAL, "feature stride %d", ld);
+  if (!(drop_p >= 0.0f && drop_p < 1.0f)) return fail(MZ_EINVAL, "dropout p %g", (double)drop_p);
+  MZ_HIP(mz_launch_qfront(bits_dev, obs6_dev, n, conv_w_dev, conv_b_dev, drop_p, seed, counter,
+                          feat_dev, ld, static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
+int mz_bank_create(mz_handle* h, int32_t slots, int32_t dim, uint32_t algo_mask) {
+  if (!h) return fail(MZ_EINVAL, "null handle");
+  if (h->bank.K) return fail(MZ_EINVAL, "the handle already has a maze bank");
+  if (slots < 1) return fail(MZ_EINVAL, "bank slots %d", slots);
+  if (algo_mask == 0 || algo_mask > 7u) return fail(MZ_EINVAL, "algorithm mask %u", algo_mask);
+  int rc = check_dim(h, dim);
+  if (rc) return rc;
+  DeviceGuard g(h->cfg.device);
+  MzBankStore& b = h->bank;
+  const MzDev& d = h->d;
+  const int nA = __builtin_popcount(algo_mask);
+  const size_t S = 2 * (size_t)nA * slots, K = (size_t)slots;
+  if ((rc = alloc(h, &b.cells, S * d.P * d.P)) || (rc = alloc(h, &b.planes, S * d.P * d.PW)) ||
+      (rc = alloc(h, &b.meta0, S)) || (rc = alloc(h, &b.meta1, S)) || (rc = alloc(h, &b.heads, 6)) ||
+      (rc = alloc(h, &b.s_visits, K * d.VP)) || (rc = alloc(h, &b.s_posw, K)) ||
+      (rc = alloc(h, &b.s_stw, K)) || (rc = alloc(h, &b.s_curw, K)) || (rc = alloc(h, &b.s_last, K)) ||
+      (rc = alloc(h, &b.s_algo, K)))
+    return rc;
+  int full[6];  // first fill builds every slot of the algorithms the bank holds
+  for (int i = 0; i < 6; ++i) full[i] = ((algo_mask >> (i % 3)) & 1u) ? slots : 0;
+  MZ_HIP(hipMemcpy(b.heads, full, sizeof full, hipMemcpyHostToDevice));
+  b.K = slots;
+  b.dim = dim;
+  b.nA = nA;
+  b.amask = algo_mask;
+  return MZ_OK;
+}
+
+int mz_bank_fill(mz_handle* h, int32_t bank, uint64_t seed, void* stream) {
+  if (!h || !h->bank.K) return fail(MZ_EINVAL, "no maze bank (mz_bank_create)");
+  if (bank != 0 && bank != 1) return fail(MZ_EINVAL, "bank %d", bank);
+  DeviceGuard g(h->cfg.device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  MzBankStore& b = h->bank;
+  const size_t K = (size_t)b.K, P = (size_t)h->d.P;
+  for (int a = 0; a < 3; ++a) {
+    if (!((b.amask >> a) & 1u)) continue;
+    const size_t blk = ((size_t)bank * b.nA + mz_bank_aidx(b.amask, a)) * K;
+    MzDev bd = h->d;  // same pitch / flags; instance arrays = this block's slots + scratch
+    bd.B = b.K;
+    bd.cells = b.cells + blk * P * P;
+    bd.planes = b.planes + blk * P * h->d.PW;
+    bd.meta0 = b.meta0 + blk;
+    bd.meta1 = b.meta1 + blk;
+    bd.visits = b.s_visits;
+    bd.posw = b.s_posw;
+    bd.stw = b.s_stw;
+    bd.curw = b.s_curw;
+    bd.last_term = b.s_last;
+    bd.algo = b.s_algo;
+    bd.bk_K = 0;
+    int* head = b.heads + 3 * bank + a;
+    const uint64_t key = seed ^ ((uint64_t)(3 * bank + a + 1) << 56);
+    MZ_HIP(mz_launch_bank_fill(bd, head, b.K, a, b.dim, key, b.epoch[bank], s));
+    MZ_HIP(hipMemsetAsync(head, 0, sizeof(int), s));
+  }
+  b.epoch[bank] += 1;
+  return MZ_OK;
+}
+
+int mz_bank_use(mz_handle* h, int32_t bank) {
+  if (!h) return fail(MZ_EINVAL, "null handle");
+  MzDev& d = h->d;
+  if (bank < 0) {
+    d.bk_K = 0;
+    return MZ_OK;
+  }
+  const MzBankStore& b = h->bank;
+  if (!b.K) return fail(MZ_EINVAL, "no maze bank (mz_bank_create)");
+  if (bank > 1) return fail(MZ_EINVAL, "bank %d", bank);
+  const size_t blk = (size_t)bank * b.nA * b.K, P = (size_t)d.P;
+  d.bk_K = b.K;
+  d.bk_dim = b.dim;
+  d.bk_amask = b.amask;
+  d.bk_cells = b.cells + blk * P * P;
+  d.bk_planes = b.planes + blk * P * d.PW;
+  d.bk_meta0 = b.meta0 + blk;
+  d.bk_meta1 = b.meta1 + blk;
+  d.bk_head = b.heads + 3 * bank;
+  return MZ_OK;
+}
+
+int mz_bank_consumed(mz_handle* h, int32_t bank, int32_t* out3_dev, void* stream) {
+  if (!h || !h->bank.K || !out3_dev || bank < 0 || bank > 1) return fail(MZ_EINVAL, "bad arguments");
+  DeviceGuard g(h->cfg.device);
+  MZ_HIP(hipMemcpyAsync(out3_dev, h->bank.heads + 3 * bank, 3 * sizeof(int32_t),
+                        hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)));
   return MZ_OK;
 }
 

@@ -44,7 +44,22 @@ struct MzDev {
   const double* pen_visit;  // [256] 0.0 - (1 - exp(-0.2 k))   (base_maze_env.py:194)
   const double* pen_inv;    // [256] 0.0 - (1 - exp(-0.15 k))  (base_maze_env.py:200)
   int* ticket;              // exit ticket of k_reset_list (done-count consumption)
+  // Active maze bank (mz_bank_*): mazes generated ahead of time that a win copies in instead
+  // of building one inside the reset launch. Slot j of algorithm a lives at index
+  // bk_aidx(a) * bk_K + j of the bank arrays; bk_head[a] counts the slots consumed so far.
+  int bk_K;                 // slots per algorithm; 0 = no bank in use
+  int bk_dim;               // maze size of the bank's mazes
+  uint32_t bk_amask;        // algorithms the bank holds (bit a)
+  const uint32_t* bk_cells; // [slots][P*P]
+  const uint32_t* bk_planes;// [slots][P*PW]
+  const uint32_t* bk_meta0; // [slots]
+  const uint32_t* bk_meta1; // [slots]
+  int* bk_head;             // [3]
 };
+
+__host__ __device__ inline int mz_bank_aidx(uint32_t amask, int a) {
+  return __builtin_popcount(amask & ((1u << a) - 1u));
+}
 
 struct MzAct {  // fused epsilon-greedy act (dqn_agent.py:104-116)
   const float* eps;

@@ -386,6 +386,45 @@ __global__ __launch_bounds__(WAVE) void k_reset_list(MzDev d, const int32_t* idx
   }
 }
 
+// Copy the next unconsumed bank maze of algorithm a into instance e (cells + plane rows + meta;
+// reset_one then rebuilds the per-episode state). Returns false (caller builds in place) when no
+// bank is in use, the bank does not hold algorithm a or size N, or it is exhausted.
+__device__ bool bank_take(const MzDev& d, int e, int a, int N) {
+  if (d.bk_K == 0 || N != d.bk_dim || !((d.bk_amask >> a) & 1u)) return false;
+  int slot = 0;
+  if (threadIdx.x == 0) slot = atomicAdd(&d.bk_head[a], 1);
+  slot = __shfl(slot, 0);
+  if (slot >= d.bk_K) return false;
+  const size_t src = (size_t)mz_bank_aidx(d.bk_amask, a) * d.bk_K + slot, es = (size_t)e;
+  const size_t pp = (size_t)d.P * d.P;
+  const uint32_t* cs = d.bk_cells + src * pp;
+  uint32_t* cd = d.cells + es * pp;
+  for (size_t i = threadIdx.x; i < pp; i += WAVE) cd[i] = cs[i];
+  const size_t pw = (size_t)d.P * d.PW;
+  const uint32_t* ps = d.bk_planes + src * pw;
+  uint32_t* pd = d.planes + es * pw;
+  for (size_t i = threadIdx.x; i < pw; i += WAVE) pd[i] = ps[i];
+  if (threadIdx.x == 0) {
+    d.meta0[e] = d.bk_meta0[src];
+    d.meta1[e] = d.bk_meta1[src];
+  }
+  __syncthreads();  // reset_one reads meta0 / the start cell word written above
+  return true;
+}
+
+// Fill one bank block (algorithm `algo`, `bd` = MzDev view whose instance arrays are the block's
+// slots): rebuild the slots consumed since the last fill (all of them when *head >= K).
+__global__ __launch_bounds__(WAVE) void k_bank_fill(MzDev bd, const int* head, int K, int algo,
+                                                    int dim, uint64_t seed, uint32_t epoch) {
+  extern __shared__ __align__(16) uint8_t lds[];
+  const int used = min(*head, K);
+  for (int j = blockIdx.x; j < used; j += gridDim.x) {
+    mz_build_one(bd, j, bd.toroidal, true, algo, seed + (uint64_t)j + ((uint64_t)epoch << 32), dim,
+                 nullptr, 0, 0, 0, 0, lds);
+    __syncthreads();
+  }
+}
+
 // Auto-reset by flag scan: each wave looks at 64 instances' done flags (one coalesced load),
 // then resets its done instances cooperatively, one after another — waves with nothing to do
 // exit at once, no device list or counter is involved. With regen, instances whose last step
@@ -403,8 +442,10 @@ __global__ __launch_bounds__(WAVE) void k_reset_done(MzDev d, int regen, uint64_
     bal &= bal - 1;
     const int ej = blockIdx.x * WAVE + j;
     if (regen && d.last_term[ej]) {
-      mz_build_one(d, ej, TOR, true, d.algo[ej], seed + (uint64_t)ej + ((uint64_t)epoch << 32),
-                   (int)(d.meta0[ej] & 0xFF), nullptr, 0, 0, 0, 0, lds);
+      const int a = d.algo[ej], N = (int)(d.meta0[ej] & 0xFF);
+      if (!bank_take(d, ej, a, N))
+        mz_build_one(d, ej, TOR, true, a, seed + (uint64_t)ej + ((uint64_t)epoch << 32), N,
+                     nullptr, 0, 0, 0, 0, lds);
       __syncthreads();  // this workgroup's global stores are visible to it past the barrier
     }
     reset_one<TOR, ENRICH>(d, ej, o, wsh);
@@ -578,6 +619,16 @@ hipError_t mz_launch_reset_done(const MzDev& d, int regen, uint64_t seed, uint32
   if (d.toroidal) { if (d.enrich) MZ_RD(true, true); else MZ_RD(true, false); }
   else { if (d.enrich) MZ_RD(false, true); else MZ_RD(false, false); }
 #undef MZ_RD
+  return hipGetLastError();
+}
+
+hipError_t mz_launch_bank_fill(const MzDev& bd, const int* head, int K, int algo, int dim,
+                               uint64_t seed, uint32_t epoch, hipStream_t s) {
+  const size_t lds = mz_build_lds_bytes(bd.P);
+  hipError_t ae = mz_lds_attr(reinterpret_cast<const void*>(k_bank_fill), lds);
+  if (ae != hipSuccess) return ae;
+  hipLaunchKernelGGL(k_bank_fill, dim3(mz_grid_for(K)), dim3(WAVE), lds, s, bd, head, K, algo, dim,
+                     seed, epoch);
   return hipGetLastError();
 }
 

@@ -1,4 +1,5 @@
-// mz_kernels.h — launchers of the device kernels (mz_env.hip), used by the C ABI (mz_api.hip).
+// mz_kernels.h — launchers of the device kernels (mz_env.hip, mz_qnet.hip), used by the C ABI
+// (mz_api.hip).
 #pragma once
 #include "mz_common.h"
 
@@ -20,3 +21,8 @@ hipError_t mz_launch_reset_done(const MzDev& d, int regen, uint64_t seed, uint32
 hipError_t mz_launch_mask(const MzDev& d, int probs, float* out4, hipStream_t s);
 hipError_t mz_launch_act(const MzDev& d, const MzAct& ap, hipStream_t s);
 hipError_t mz_launch_expand(const uint32_t* bits, float* out, int n, hipStream_t s);
+hipError_t mz_launch_qfront(const uint32_t* bits, const float* obs6, int n, const float* w,
+                            const float* b, float drop_p, uint64_t seed, uint64_t counter,
+                            uint16_t* out, int ld, hipStream_t s);
+hipError_t mz_launch_bank_fill(const MzDev& bd, const int* head, int K, int algo, int dim,
+                               uint64_t seed, uint32_t epoch, hipStream_t s);

@@ -11,7 +11,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(ROOT, "csrc")
 LIBDIR = os.path.join(PKG, "_lib")
 LIB = os.path.join(LIBDIR, "libmazerl.so")
-SOURCES = ["mz_env.hip", "mz_api.hip", "mz_difficulty.hip"]
+SOURCES = ["mz_env.hip", "mz_api.hip", "mz_difficulty.hip", "mz_qnet.hip"]
 DEPS = SOURCES + ["mz_common.h", "mz_kernels.h", "mz_build.inc.h"]
 HEADER = os.path.join(os.path.dirname(ROOT), "include", "mazerl.h")
 

@@ -150,14 +150,26 @@ class VectorDQNLearner:
     def __init__(self, num_envs, device, variant="ddqn", lr=1e-3, eps_start=0.95, eps_final=0.1,
                  eps_decay=8000.0, gamma=0.7, batch_size=128, capacity=1_000_000,
                  updates_per_step=1, target_every=100, hidden_dim=1024, h_channels=32,
-                 act_bf16=True, t_max=150, updates_per_epoch=100, allreduce=None, seed=0):
+                 act_bf16=True, t_max=150, updates_per_epoch=100, allreduce=None, seed=0,
+                 use_graph=True):
         self.device = torch.device(device)
         torch.manual_seed(seed)
         self.variant = variant
         self.source = QNet(3, 6, 4, h_channels, hidden_dim, variant).to(self.device)
         self.target = QNet(3, 6, 4, h_channels, hidden_dim, variant).to(self.device)
         self.target.load_state_dict(self.source.state_dict())
-        self.opt = optim.AdamW(self.source.parameters(), lr)
+        # One update (sample -> expand -> loss -> backward -> clamp -> AdamW) is ~150 small
+        # kernels: on one GPU it is captured once into a HIP graph and replayed (capturable
+        # AdamW with a device-side lr, so the cosine schedule still applies).
+        self.use_graph = bool(use_graph) and self.device.type == "cuda" and allreduce is None
+        if self.use_graph:
+            self.opt = optim.AdamW(self.source.parameters(),
+                                   torch.tensor(float(lr), device=self.device), capturable=True)
+        else:
+            self.opt = optim.AdamW(self.source.parameters(), lr)
+        self._graph = None
+        self._graph_loss = None
+        self._eager_updates = 0
         self.sched = lr_scheduler.CosineAnnealingLR(self.opt, T_max=t_max, eta_min=1e-5)
         from ..replay import DeviceReplay
         self.replay = DeviceReplay(capacity, self.device)
@@ -170,12 +182,26 @@ class VectorDQNLearner:
         self.steps_done = torch.zeros(num_envs, dtype=torch.float32, device=self.device)
         self.n_updates = 0
         self.last_loss = torch.zeros((), device=self.device)
+        self.fused = None
+        if self.device.type == "cuda" and act_bf16:
+            from .fused import FusedQ
+            self.fused = FusedQ(self.source, seed=seed)
+
+    @property
+    def supports_bits(self):
+        return self.fused is not None
 
     def epsilon(self):
         return self.eps_final + (self.eps_start - self.eps_final) * torch.exp(-self.steps_done / self.eps_decay)
 
     @torch.no_grad()
-    def greedy(self, obs6, window):
+    def greedy(self, obs6, window, bits=None):
+        """argmax_a Q_source(s) for every instance. With packed window bits on the GPU the acting
+        forward is the fused HIP stem + bf16 GEMMs (agents/fused.py); otherwise torch."""
+        if bits is not None and self.fused is not None:
+            return self.fused(obs6, bits).float().argmax(1)
+        if window is None:
+            raise ValueError("greedy() needs the f32 window or window bits on the GPU")
         if self.act_bf16 and self.device.type == "cuda":
             with torch.autocast("cuda", dtype=torch.bfloat16):
                 q = self.source((obs6, window))
@@ -187,13 +213,39 @@ class VectorDQNLearner:
         if len(self.replay) < self.batch_size:
             return None
         for _ in range(self.updates_per_step):
-            state, a, r, nxt = self.replay.sample(self.batch_size, expand)
-            loss = q_loss(self.source, self.target, state, a, r, nxt, self.gamma, self.variant == "ddqn")
-            learner_update(self.source, self.opt, loss, allreduce=self.allreduce)
-            self.last_loss = loss.detach()
+            if self.use_graph:
+                self._graph_update(expand)
+            else:
+                self.last_loss = self._one_update(expand, static=False)
             self.n_updates += 1
             if self.n_updates % self.target_every == 0:
                 self.target.load_state_dict(self.source.state_dict())
             if self.n_updates % self.updates_per_epoch == 0:
                 self.sched.step()
         return self.last_loss
+
+    def _one_update(self, expand, static):
+        state, a, r, nxt = self.replay.sample(self.batch_size, expand, static=static)
+        loss = q_loss(self.source, self.target, state, a, r, nxt, self.gamma, self.variant == "ddqn")
+        learner_update(self.source, self.opt, loss, allreduce=self.allreduce)
+        return loss.detach()
+
+    def _graph_update(self, expand, warmup=3):
+        if self._graph is None:
+            if self._eager_updates < warmup:  # real updates on a side stream before capture
+                s = torch.cuda.Stream(self.device)
+                s.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(s):
+                    self.last_loss = self._one_update(expand, static=True)
+                torch.cuda.current_stream(self.device).wait_stream(s)
+                self._eager_updates += 1
+                return
+            self.opt.zero_grad(set_to_none=True)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._graph_loss = self._one_update(expand, static=True)
+            self._graph = g
+        self._graph.replay()
+        self.last_loss = self._graph_loss
+        if self.fused is not None:
+            self.fused.invalidate()  # graph replays leave the params' _version untouched

@@ -1,0 +1,137 @@
+"""Acting forward of the Q / actor-critic networks straight from packed windows.
+
+The reference acts with `source_net(state)` (dqn_agent.py:113-116; ddqn_agent.py, nets never in
+eval mode — SURVEY Q13; ppo_agent.py ActorCriticNet.act). Vectorised over 65,536 instances the
+conv stem dominated the training step through PyTorch (f32 window + transposes + bf16 conv
+output + separate LeakyReLU / Dropout / MaxPool passes, ~4 ms per vector step). Here:
+
+  mz_q_front (HIP, csrc/mz_qnet.hip)   88-byte window bits + obs6 -> bf16 [n, 1600] fc1 input
+                                       (conv as bf16 MFMA, LeakyReLU, Dropout, MaxPool fused)
+  Linear -> act -> Linear -> act -> Linear   bf16 GEMMs (hipBLASLt), f32 accumulation
+
+Same precision class as the autocast(bf16) acting path it replaces (bf16 weights and
+activations); the update path (q_loss / PPO losses) stays f32 through torch. Dropout masks come
+from the kernel's own counter-based hash (P(drop) = 13107/65536 for p = 0.2), not torch's RNG.
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import _native as N
+
+LD = 1600          # fc1 input row: 1,568 conv features | 6 obs | 26 zeros (16-B aligned rows)
+CONV_OUT = 1568
+
+
+def _act_fn(m):
+    if isinstance(m, nn.LeakyReLU):
+        return lambda h: F.leaky_relu_(h, m.negative_slope)
+    if isinstance(m, nn.ReLU):
+        return F.relu_
+    raise TypeError(f"unsupported activation {type(m).__name__}")
+
+
+class _Head:
+    """bf16 copy of a Linear -> act -> Linear -> act -> Linear stack; the first weight padded to LD
+    columns. Refreshed when the f32 parameters changed: eager optimizer steps bump `_version`;
+    updates replayed from a captured HIP graph do not, so their owner calls invalidate()."""
+
+    def __init__(self, seq):
+        self.seq = seq
+        self.lin = [m for m in seq if isinstance(m, nn.Linear)]
+        self.acts = [_act_fn(m) for m in seq if not isinstance(m, nn.Linear)]
+        assert len(self.lin) == 3 and len(self.acts) == 2
+        l0 = self.lin[0]
+        if l0.in_features > LD:
+            raise ValueError(f"first Linear has {l0.in_features} inputs > {LD}")
+        self.w0 = torch.zeros(l0.out_features, LD, dtype=torch.bfloat16, device=l0.weight.device)
+        self._ver = None
+        self._w = None
+
+    def invalidate(self):
+        self._ver = None
+
+    def _refresh(self):
+        ver = tuple(p._version for l in self.lin for p in (l.weight, l.bias))
+        if ver == self._ver and self._w is not None:
+            return
+        l0, l1, l2 = self.lin
+        self.w0[:, :l0.in_features].copy_(l0.weight.detach())
+        self._w = [(self.w0, l0.bias.detach().to(torch.bfloat16)),
+                   (l1.weight.detach().to(torch.bfloat16), l1.bias.detach().to(torch.bfloat16)),
+                   (l2.weight.detach().to(torch.bfloat16), l2.bias.detach().to(torch.bfloat16))]
+        self._ver = ver
+
+    def __call__(self, feat):
+        self._refresh()
+        (w0, b0), (w1, b1), (w2, b2) = self._w
+        h = self.acts[0](F.linear(feat, w0, b0))
+        h = self.acts[1](F.linear(h, w1, b1))
+        return F.linear(h, w2, b2)
+
+
+class FusedStem:
+    """Conv2d(3->32, 3x3, p1) -> LeakyReLU -> [Dropout] -> MaxPool2d(2) -> flatten || obs6."""
+
+    def __init__(self, conv_seq, seed=0):
+        mods = list(conv_seq)
+        self.conv = mods[0]
+        assert isinstance(self.conv, nn.Conv2d) and tuple(self.conv.weight.shape) == (32, 3, 3, 3), \
+            "the fused stem implements the reference's Conv2d(3, 32, 3, padding=1)"
+        assert isinstance(mods[1], nn.LeakyReLU) and mods[1].negative_slope == 0.01
+        self.dropout = next((m for m in mods if isinstance(m, nn.Dropout)), None)
+        assert isinstance(mods[-1], nn.MaxPool2d)
+        self.seed = seed
+        self.counter = 0
+        self.lib = N.load()
+
+    def __call__(self, obs6, bits):
+        n = bits.shape[0]
+        dev = bits.device
+        if dev.type != "cuda":
+            raise RuntimeError("the fused acting stem runs on the GPU only")
+        assert bits.dtype == torch.int32 and bits.shape[1] == 22 and bits.is_contiguous()
+        obs6 = obs6.contiguous()
+        assert obs6.dtype == torch.float32 and obs6.shape == (n, 6)
+        w = self.conv.weight.detach().contiguous()
+        b = self.conv.bias.detach().contiguous()
+        p = float(self.dropout.p) if (self.dropout is not None and self.dropout.training) else 0.0
+        feat = torch.empty(n, LD, dtype=torch.bfloat16, device=dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        N.check(self.lib.mz_q_front(bits.data_ptr(), obs6.data_ptr(), n, w.data_ptr(), b.data_ptr(),
+                                    p, self.seed, self.counter, feat.data_ptr(), LD, stream))
+        self.counter += 1
+        return feat
+
+
+class FusedQ:
+    """QNet acting forward (DQN / DDQN) on window bits -> Q values [n, 4] (bf16)."""
+
+    def __init__(self, qnet, seed=0):
+        self.stem = FusedStem(qnet.conv, seed)
+        self.head = _Head(qnet.fc)
+
+    def invalidate(self):
+        self.head.invalidate()
+
+    @torch.no_grad()
+    def __call__(self, obs6, bits):
+        return self.head(self.stem(obs6, bits))
+
+
+class FusedActorCritic:
+    """ActorCriticNet forward on window bits -> (logits [n, 4], value [n, 1]) (bf16)."""
+
+    def __init__(self, net, seed=0):
+        self.stem = FusedStem(net.conv, seed)
+        self.actor = _Head(net.actor_head)
+        self.critic = _Head(net.critic_head)
+
+    def invalidate(self):
+        self.actor.invalidate()
+        self.critic.invalidate()
+
+    @torch.no_grad()
+    def __call__(self, obs6, bits):
+        feat = self.stem(obs6, bits)
+        return self.actor(feat), self.critic(feat)

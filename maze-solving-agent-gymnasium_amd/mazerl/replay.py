@@ -50,6 +50,7 @@ class DeviceReplay:
         self.swn = torch.zeros(C, window_words, dtype=torch.int32, **kw)
         self.ptr = 0
         self.size = 0
+        self.size_dev = torch.zeros((), dtype=torch.float64, **kw)  # for graph-captured sampling
         self._gen = torch.Generator(device=self.device)
         self._gen.manual_seed(0x5EED)
 
@@ -78,14 +79,23 @@ class DeviceReplay:
         self.s6n.index_copy_(0, idx, s6n)
         self.swn.index_copy_(0, idx, swn)
         self.ptr = (self.ptr + n) % self.capacity
-        self.size = min(self.size + n, self.capacity)
+        size = min(self.size + n, self.capacity)
+        if size != self.size:
+            self.size_dev.fill_(float(size))
+        self.size = size
 
     def sample_indices(self, batch):
         return torch.randint(0, self.size, (batch,), device=self.device, generator=self._gen)
 
-    def sample(self, batch, expand):
+    def sample_indices_static(self, batch):
+        """Uniform indices from the device-side size (no host value baked in): usable inside a
+        captured HIP graph. float64 uniforms from the default generator (graph-safe)."""
+        u = torch.rand(batch, dtype=torch.float64, device=self.device)
+        return (u * self.size_dev).to(torch.int64).clamp_(max=self.capacity - 1)
+
+    def sample(self, batch, expand, static=False):
         """Returns ((s6, window), a, r, (s6', window')) with f32 windows from `expand(bits)`."""
-        i = self.sample_indices(batch)
+        i = self.sample_indices_static(batch) if static else self.sample_indices(batch)
         bits = torch.cat((self.sw.index_select(0, i), self.swn.index_select(0, i)), 0)
         w = expand(bits)
         return ((self.s6.index_select(0, i), w[:batch]), self.a.index_select(0, i),

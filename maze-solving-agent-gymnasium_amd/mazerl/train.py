@@ -51,7 +51,8 @@ def main(argv=None):
     else:
         algo = a.algo
     env = VectorMazeEnv(B, a.dim, enrich=True, device=dev, algorithm=algo,
-                        seed=0x5EED0000 + rank * B, done_list=False, pos=True)
+                        seed=0x5EED0000 + rank * B, done_list=False, pos=True,
+                        window=False, window_bits=True)  # acting reads the bits (agents/fused.py)
     env.set_algorithm(algo if isinstance(algo, str) else algo.to(torch.uint8))
     decay = a.eps_decay or ((a.dim - 1) * (a.dim - 1) // 2) * 5 / 40.0
     learner = VectorDQNLearner(B, dev, variant=a.variant, lr=a.lr, eps_start=a.eps_start,

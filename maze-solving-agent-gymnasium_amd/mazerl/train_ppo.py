@@ -38,7 +38,7 @@ def main(argv=None):
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     env = make_env(a.envs, dims, toroidal=True, algorithm=a.algo, seed=0x5EED0000 + rank * a.envs,
-                   device=dev, done_list=False, reward64=True)
+                   device=dev, done_list=False, reward64=True, window=False, window_bits=True)
     tr = VectorPPOTrainer(env, dev, gamma=a.gamma, batch_size=a.batch, ppo_steps=a.ppo_steps,
                           pool_size=a.pool, seed=a.seed,
                           allreduce=GradAllReduce() if world > 1 else None)

@@ -53,12 +53,22 @@ class VectorPPOTrainer:
         self.updates = 0
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed)
+        self.fused = None
+        if self.device.type == "cuda" and act_bf16:
+            from ..agents.fused import FusedActorCritic
+            self.fused = FusedActorCritic(self.net, seed=seed)
+
+    @property
+    def supports_bits(self):
+        return self.fused is not None
 
     @torch.no_grad()
     def _act(self):
         env = self.env
         state = (env.obs6, env.window)
-        if self.act_bf16 and self.device.type == "cuda":
+        if self.fused is not None and env.window_bits is not None:
+            logits, value = self.fused(env.obs6, env.window_bits)
+        elif self.act_bf16 and self.device.type == "cuda":
             with torch.autocast("cuda", dtype=torch.bfloat16):
                 logits, value = self.net(state)
         else:
@@ -157,6 +167,9 @@ class VectorPPOTrainer:
         return time.perf_counter() - t0
 
     @torch.no_grad()
-    def greedy(self, obs6, window):
-        logits, _ = self.net((obs6, window))
+    def greedy(self, obs6, window, bits=None):
+        if bits is not None and self.fused is not None:
+            logits, _ = self.fused(obs6, bits)
+        else:
+            logits, _ = self.net((obs6, window))
         return torch.argmax(F.softmax(logits.float(), dim=-1), dim=-1)

@@ -2,13 +2,15 @@
 
 VectorOffPolicyTrainer.train() is NeuralOffPolicyTrainer.train (lib/trainers/off_policy_trainer.py
 :144-225) over B instances at once. Per vector step:
-  greedy  = argmax Q_source(obs)                      (bf16 MFMA GEMMs, dqn_agent.py:113-116)
+  greedy  = argmax Q_source(obs)   fused HIP conv stem on the window bits + bf16 MFMA GEMMs
+                                                      (agents/fused.py, dqn_agent.py:113-116)
   step    = fused epsilon-greedy act + env step       (one k_step launch, per-instance epsilon)
   replay  <- (s, a, r, s') for every instance, s' = the step's (terminal) observation; terminal
              transitions bootstrap like the reference's
   bookkeeping: steps_done += 1, = 0 on a win (off_policy_trainer.py:192); wins/episodes counters
   auto-reset: winners get a new maze (update_maze, :202), truncated instances restart the same
-             maze (reset, :153) — one flag-scan kernel
+             maze (reset, :153) — one flag-scan kernel; new mazes are copied from a bank of
+             pre-generated mazes (refilled in bulk on a side stream)
   K learner updates (replay ratio), target sync / cosine step per update count.
 evaluate() is NeuralOffPolicyTrainer.test(new=True)/infer (:228-299): fresh mazes, one episode
 each, win = terminated; greedy (eps = 0) or the reference's epsilon protocol (Q14).
@@ -21,8 +23,13 @@ from ..vector_env import ALGOS, VectorMazeEnv
 
 
 class VectorOffPolicyTrainer:
-    def __init__(self, env, learner, seed=0, regen_won=True, curriculum=False, allreduce_stats=None):
+    def __init__(self, env, learner, seed=0, regen_won=True, curriculum=False, allreduce_stats=None,
+                 bank=True):
         self.env, self.learner = env, learner
+        if regen_won and bank:
+            # winners' new mazes come from a bank refilled on a side stream (VectorMazeEnv.
+            # enable_bank): a maze build is a ~1 ms serial chain that would stall the step
+            env.enable_bank(algorithms=[0, 1, 2] if curriculum else None)
         self.seed = seed
         self.regen_won = regen_won
         self.curriculum = curriculum
@@ -39,7 +46,7 @@ class VectorOffPolicyTrainer:
 
     def vector_step(self):
         env, L = self.env, self.learner
-        greedy = L.greedy(env.obs6, env.window)
+        greedy = L.greedy(env.obs6, env.window, env.window_bits)
         s6 = env.obs6.clone()
         sw = env.window_bits.clone()
         env.step_act(eps=L.epsilon(), greedy=greedy, seed=self.seed, counter=self.counter)
@@ -100,15 +107,16 @@ def evaluate(learner, num_mazes, dim, algorithm="r-prim", seed=0x7E57, eps=0.0, 
              device=None, max_vector_steps=None):
     """Fraction of `num_mazes` fresh mazes solved in one episode (terminated before truncation).
     `dim` may be a list of sizes (instance i gets dim[i % len])."""
+    bits = getattr(learner, "supports_bits", False)
     env = make_env(num_mazes, dim, toroidal=toroidal, algorithm=algorithm, seed=seed,
-                   device=device, done_list=False, pos=False)
+                   device=device, done_list=False, pos=False, window=not bits, window_bits=True)
     dim = max(dim) if not isinstance(dim, int) else dim
     finished = torch.zeros(num_mazes, dtype=torch.bool, device=env.device)
     won = torch.zeros(num_mazes, dtype=torch.bool, device=env.device)
     limit = max_vector_steps or (dim - 1) * (dim - 1) + 2  # > any max_steps
     k = 0
     while k < limit:
-        greedy = learner.greedy(env.obs6, env.window)
+        greedy = learner.greedy(env.obs6, env.window, env.window_bits)
         acts = env.act(eps=eps, greedy=greedy, seed=seed, counter=k)
         acts = torch.where(finished, torch.full_like(acts, -1), acts)
         env.step(acts)

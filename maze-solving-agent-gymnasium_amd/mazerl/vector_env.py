@@ -62,6 +62,8 @@ class VectorMazeEnv:
             done_count=_ptr(self.done_count) if done_list else None)
         self.seed = int(seed)
         self.epoch = 0
+        self._bank = None
+        self.algos_in_use = set()  # algorithm ids regeneration may ask for (sizes the bank)
         self._count_zero = True  # done_count is 0 (fresh, or consumed by reset_done)
         if generate:
             self.generate(algorithm=algorithm)
@@ -92,12 +94,15 @@ class VectorMazeEnv:
         algo_t, algo_all = None, 0
         if isinstance(algorithm, str):
             algo_all = ALGOS[algorithm]
+            self.algos_in_use.add(algo_all)
         elif isinstance(algorithm, int):
             algo_all = int(algorithm)
+            self.algos_in_use.add(algo_all)
         else:
             algo_t = torch.as_tensor(algorithm, dtype=torch.uint8, device=self.device)
             if algo_t.numel() != n:
                 raise ValueError("per-instance algorithm ids must match the env list")
+            self.algos_in_use.update(ALGOS.values())
         N.check(self.lib.mz_generate(self._h, _ptr(ids), n, _ptr(algo_t), algo_all, dim,
                                      seed & 0xFFFFFFFFFFFFFFFF, self._stream()))
         return self
@@ -117,9 +122,11 @@ class VectorMazeEnv:
     def set_algorithm(self, algorithm):
         if isinstance(algorithm, str):
             N.check(self.lib.mz_set_algorithm(self._h, None, ALGOS[algorithm], self._stream()))
+            self.algos_in_use = {ALGOS[algorithm]}
         else:
             t = torch.as_tensor(algorithm, dtype=torch.uint8, device=self.device)
             N.check(self.lib.mz_set_algorithm(self._h, _ptr(t), 0, self._stream()))
+            self.algos_in_use = set(ALGOS.values())
 
     # ---------------------------------------------------------------------------------------
     def reset(self):
@@ -141,13 +148,66 @@ class VectorMazeEnv:
 
     def reset_done(self, regen_won=False, seed=None):
         """Auto-reset every instance whose last step ended terminated|truncated (flag scan, no
-        list); with regen_won the winners get a new maze first (win -> update_maze)."""
+        list); with regen_won the winners get a new maze first (win -> update_maze) — copied
+        from the maze bank when one is enabled (enable_bank)."""
         if regen_won:
             self.epoch += 1
         N.check(self.lib.mz_reset_done(self._h, int(bool(regen_won)),
                                        (self.seed if seed is None else int(seed)) & 0xFFFFFFFFFFFFFFFF,
                                        self.epoch & 0xFFFFFFFF, N.C.byref(self._out),
                                        self._stream()))
+        if regen_won and self._bank is not None:
+            self._bank_tick()
+
+    # ---------------------------------------------------------------------------------------
+    # Maze bank: winners' new mazes are generated ahead of time, in bulk, on a side stream.
+    def enable_bank(self, slots=None, swap_every=8, algorithms=None, seed=0xBA4C0000):
+        """Two banks of `slots` mazes per algorithm (size maze_dim): reset_done(regen_won=True)
+        consumes the active one; every `swap_every` such calls the banks swap and the retired
+        one is refilled on a side stream (ordered after the launches that consumed it; the main
+        stream waits for a refill only when that bank comes back). Default slots: B / 8."""
+        if self._bank is not None:
+            return
+        K = int(slots or max(64, self.num_envs // 8))
+        if algorithms is None:
+            mask = sum(1 << i for i in self.algos_in_use) or 7
+        else:
+            ids = [ALGOS[a] if isinstance(a, str) else int(a) for a in algorithms]
+            mask = sum(1 << i for i in set(ids))
+        N.check(self.lib.mz_bank_create(self._h, K, self.maze_dim, mask))
+        self._bank = dict(K=K, swap=int(swap_every), calls=0, cur=0, seed=int(seed),
+                          side=torch.cuda.Stream(self.device), ready=[None, None])
+        st = self._stream()
+        for b in (0, 1):
+            N.check(self.lib.mz_bank_fill(self._h, b, self._bank["seed"], st))
+        N.check(self.lib.mz_bank_use(self._h, 0))
+
+    def _bank_tick(self):
+        bk = self._bank
+        bk["calls"] += 1
+        if bk["calls"] % bk["swap"]:
+            return
+        old, new = bk["cur"], 1 - bk["cur"]
+        main = torch.cuda.current_stream(self.device)
+        if bk["ready"][new] is not None:
+            main.wait_event(bk["ready"][new])
+        N.check(self.lib.mz_bank_use(self._h, new))
+        bk["cur"] = new
+        consumed = torch.cuda.Event()
+        consumed.record(main)
+        side = bk["side"]
+        side.wait_event(consumed)
+        N.check(self.lib.mz_bank_fill(self._h, old, bk["seed"], side.cuda_stream))
+        ev = torch.cuda.Event()
+        ev.record(side)
+        bk["ready"][old] = ev
+
+    def bank_consumed(self, bank=None):
+        """int32 [3]: slots of `bank` (default: the active one) consumed per algorithm id."""
+        out = torch.zeros(3, dtype=torch.int32, device=self.device)
+        b = self._bank["cur"] if bank is None else int(bank)
+        N.check(self.lib.mz_bank_consumed(self._h, b, out.data_ptr(), self._stream()))
+        return out
 
     def reset_done_list(self, regen_won=False, seed=None):
         """Auto-reset from the step's device done list (consumes done_count)."""
