@@ -168,8 +168,10 @@ int mz_bank_consumed(mz_handle* h, int32_t bank, int32_t* out3_dev, void* stream
 
 /* Fused conv stem of the DQN/DDQN Q-network for acting (dqn_agent.py:19-57 forward,
  * ddqn_agent.py:18-52): from n packed windows (window_bits layout) and obs6 [n][6] f32, writes
- * feat_dev [n][ld] bf16 = [MaxPool2(Dropout(LeakyReLU(Conv3x3(window) + b))) flattened (1,568,
- * channel-major) | obs6 (6) | zeros], the input row of the first Linear layer.
+ * feat_dev [n][ld] bf16 = [MaxPool2(Dropout(LeakyReLU(Conv3x3(window) + b))) (1,568 values,
+ * position-major: element q*32 + c = channel c at pooled position q; torch's flatten order is
+ * c*49 + q, so fc1's weight columns are permuted once by the caller) | obs6 (6) | zeros], the
+ * input row of the first Linear layer.
  * conv_w_dev f32 [32][3][3][3], conv_b_dev f32 [32]; drop_p = 0 (DQN) or the Dropout p (DDQN in
  * train mode), masks drawn from (seed, counter); ld in 1576..1600, multiple of 8. */
 int mz_q_front(const uint32_t* bits_dev, const float* obs6_dev, int32_t n, const float* conv_w_dev,

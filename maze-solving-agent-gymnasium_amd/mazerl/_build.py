@@ -2,9 +2,13 @@
 
 hipcc cross-compiles for gfx950 without a GPU. -ffp-contract=off keeps every double reward /
 score / max_steps expression rounded like CPython (the kernels also use explicit __d*_rn ops).
+Each source compiles to its own object (in parallel), so a file can carry extra flags:
+mz_qnet.hip (bf16 acting stem, no double / NaN semantics involved) is built with
+-ffinite-math-only, which drops the NaN canonicalisation fmaxf puts on every MFMA result.
 """
 import os
 import subprocess
+from concurrent.futures import ThreadPoolExecutor
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
@@ -12,6 +16,8 @@ CSRC = os.path.join(ROOT, "csrc")
 LIBDIR = os.path.join(PKG, "_lib")
 LIB = os.path.join(LIBDIR, "libmazerl.so")
 SOURCES = ["mz_env.hip", "mz_api.hip", "mz_difficulty.hip", "mz_qnet.hip"]
+EXTRA_FLAGS = {"mz_qnet.hip": ["-ffinite-math-only"]}
+BASE_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall"]
 DEPS = SOURCES + ["mz_common.h", "mz_kernels.h", "mz_build.inc.h"]
 HEADER = os.path.join(os.path.dirname(ROOT), "include", "mazerl.h")
 
@@ -33,9 +39,22 @@ def build(force=False, verbose=False):
     if not force and not stale():
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
+    objdir = os.path.join(LIBDIR, "obj")
+    os.makedirs(objdir, exist_ok=True)
+
+    def compile_one(f):
+        obj = os.path.join(objdir, f + ".o")
+        cmd = [hipcc()] + BASE_FLAGS + EXTRA_FLAGS.get(f, []) + ["-c", "-o", obj,
+                                                                os.path.join(CSRC, f)]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+        return obj
+
+    with ThreadPoolExecutor(max_workers=min(4, len(SOURCES))) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
     tmp = LIB + ".tmp"
-    cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-Wall", "-o", tmp] + [os.path.join(CSRC, f) for f in SOURCES]
+    cmd = [hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp] + objs
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

@@ -45,8 +45,9 @@ def learner_update(net, optimizer, loss, clamp=1.0, allreduce=None):
     loss.backward()
     if allreduce is not None:
         allreduce(net)  # average grads over ranks, then clamp (single-GPU semantics)
-    for p in net.parameters():
-        p.grad.data.clamp_(-clamp, clamp)
+    grads = [p.grad for p in net.parameters() if p.grad is not None]
+    torch._foreach_clamp_min_(grads, -clamp)  # == p.grad.data.clamp_(-1, 1) per parameter
+    torch._foreach_clamp_max_(grads, clamp)   # (dqn_agent.py:155-156), two launches in total
     optimizer.step()
 
 
@@ -164,7 +165,8 @@ class VectorDQNLearner:
         self.use_graph = bool(use_graph) and self.device.type == "cuda" and allreduce is None
         if self.use_graph:
             self.opt = optim.AdamW(self.source.parameters(),
-                                   torch.tensor(float(lr), device=self.device), capturable=True)
+                                   torch.tensor(float(lr), device=self.device), capturable=True,
+                                   fused=True)
         else:
             self.opt = optim.AdamW(self.source.parameters(), lr)
         self._graph = None

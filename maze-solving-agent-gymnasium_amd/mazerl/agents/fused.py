@@ -6,7 +6,8 @@ conv stem dominated the training step through PyTorch (f32 window + transposes +
 output + separate LeakyReLU / Dropout / MaxPool passes, ~4 ms per vector step). Here:
 
   mz_q_front (HIP, csrc/mz_qnet.hip)   88-byte window bits + obs6 -> bf16 [n, 1600] fc1 input
-                                       (conv as bf16 MFMA, LeakyReLU, Dropout, MaxPool fused)
+                                       (conv as bf16 MFMA, LeakyReLU, Dropout, MaxPool fused;
+                                       features position-major, fc1 columns permuted to match)
   Linear -> act -> Linear -> act -> Linear   bf16 GEMMs (hipBLASLt), f32 accumulation
 
 Same precision class as the autocast(bf16) acting path it replaces (bf16 weights and
@@ -21,6 +22,12 @@ from .. import _native as N
 
 LD = 1600          # fc1 input row: 1,568 conv features | 6 obs | 26 zeros (16-B aligned rows)
 CONV_OUT = 1568
+
+
+def feature_perm(device=None):
+    """The kernel writes conv features position-major (q * 32 + c); torch's flatten is
+    channel-major (c * 49 + q). perm[f'] = torch index of kernel feature f'."""
+    return torch.arange(CONV_OUT, device=device).view(32, 49).t().reshape(-1)
 
 
 def _act_fn(m):
@@ -45,6 +52,7 @@ class _Head:
         if l0.in_features > LD:
             raise ValueError(f"first Linear has {l0.in_features} inputs > {LD}")
         self.w0 = torch.zeros(l0.out_features, LD, dtype=torch.bfloat16, device=l0.weight.device)
+        self.perm = feature_perm(l0.weight.device)
         self._ver = None
         self._w = None
 
@@ -56,7 +64,9 @@ class _Head:
         if ver == self._ver and self._w is not None:
             return
         l0, l1, l2 = self.lin
-        self.w0[:, :l0.in_features].copy_(l0.weight.detach())
+        w = l0.weight.detach()
+        self.w0[:, :CONV_OUT].copy_(w.index_select(1, self.perm))  # kernel feature order
+        self.w0[:, CONV_OUT:l0.in_features].copy_(w[:, CONV_OUT:])
         self._w = [(self.w0, l0.bias.detach().to(torch.bfloat16)),
                    (l1.weight.detach().to(torch.bfloat16), l1.bias.detach().to(torch.bfloat16)),
                    (l2.weight.detach().to(torch.bfloat16), l2.bias.detach().to(torch.bfloat16))]

@@ -49,10 +49,12 @@ def front(bits, obs6, w, b, p=0.0, seed=0, counter=0, ld=1600):
 
 
 def reference(bits, obs6, w, b):
+    """fp32 torch stem in the kernel's feature order (position-major, agents/fused.py)."""
+    from mazerl.agents.fused import feature_perm
     win = bits_to_window(bits)
     y = F.conv2d(win, w.to(torch.bfloat16).float(), b, padding=1)
-    y = F.max_pool2d(F.leaky_relu(y, 0.01), 2)
-    return torch.cat((y.flatten(1), obs6), 1)
+    y = F.max_pool2d(F.leaky_relu(y, 0.01), 2).flatten(1)
+    return torch.cat((y[:, feature_perm(y.device)], obs6), 1)
 
 
 @pytest.mark.parametrize("n,ld", [(1, 1600), (7, 1576), (1001, 1600), (4096, 1584)])
