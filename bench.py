@@ -1,17 +1,21 @@
 #!/usr/bin/env python3
 """Headline benchmark: env steps/sec on 40x40-cell (81x81 grid) r-prim mazes (BASELINE.json).
 
-One "step" = one vector step of the hot path over every instance on the GPU:
-  k_step with the fused reference masked-exploration act (dqn_agent.py:110-112) +
-     BaseMazeEnv.step + Enrich obs (reward, terminated/truncated, obs6, f32 3x15x15 window)
-  -> k_reset_list (auto-reset of the instances that just finished, base_maze_env.py:136-161)
+One "step" = one vector step of the hot path over every instance on the GPU, ONE launch:
+  k_step with the fused reference masked-exploration act (dqn_agent.py:104-116) +
+     BaseMazeEnv.step + Enrich obs (reward, terminated/truncated, obs6, f32 3x15x15 window),
+     with autoreset: instances whose previous step ended are reset in the same launch
+     (BaseMazeEnv.reset, base_maze_env.py:136-161 — the trainer's env.reset() after an episode)
 Workload: configs[2] of BASELINE.json — 65,536 instances of 81x81-grid r-prim mazes per GPU,
 generated on the GPU before the timed region (generation is reported separately).
 Multi-GPU: one process per GPU (torchrun), independent env shards (no data-path collective),
 weak scaling; value = all ranks' env steps / max-over-ranks wall time.
 
-Extra JSON fields: roofline of k_step (HIP events on the launch stream), cpu_baseline (the CPU
-oracle in reference-cost mode, A* per find_path, timed on host cores — rank 0, N=1 only).
+Extra JSON fields: roofline of k_step (one HIP event pair on the launch stream around the whole
+timed region — one k_step launch per step, so elapsed / steps is its average launch duration
+including the back-to-back launch gap; a pair around every launch would drain the queue each
+time and add ~3 us), cpu_baseline (the CPU oracle in reference-cost mode, A* per
+find_path, timed on host cores — rank 0, N=1 only).
 """
 import argparse
 import json
@@ -117,38 +121,33 @@ def main():
     gen_s = time.perf_counter() - t0
     stream = torch.cuda.current_stream(dev)
 
-    def vstep(k, ev=None):
-        # fused act + step (one launch), then auto-reset of the finished instances
-        if ev is not None:
-            ev[0].record(stream)
-        env.step_act(eps=1.0, seed=0xBE7C4 + rank, counter=k)
-        if ev is not None:
-            ev[1].record(stream)
-        env.reset_done()
+    def vstep(k):
+        # one launch: fused act + step, autoreset of the instances that finished last step
+        env.step_act(eps=1.0, seed=0xBE7C4 + rank, counter=k, autoreset=True)
 
     for k in range(a.warmup):
         vstep(k)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(a.steps)]
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev0.record(stream)
     for k in range(a.steps):
-        vstep(a.warmup + k, evs[k])
+        vstep(a.warmup + k)
+    ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    step_ms = [s.elapsed_time(e) for s, e in evs]
+    avg_kernel_ms = ev0.elapsed_time(ev1) / a.steps
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     total_steps = B * a.steps * world
     value = total_steps / el
-    avg_kernel_ms = sum(step_ms) / len(step_ms)
     achieved = ALG_BYTES_PER_STEP * B / (avg_kernel_ms * 1e-3) / 1e9
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_k_step.json")
@@ -173,11 +172,12 @@ def main():
             "dtype": "int32",
             "data": "synthetic (GPU-generated r-prim mazes, Philox seeds 0x5EED0000 + instance id)",
             "config": {"workload": f"{B} x 40x40-cell ({a.dim}x{a.dim} grid) {a.algo} Enrich mazes "
-                                   f"per GPU: fused act+env step (f32 3x15x15 window) + auto-reset",
+                                   f"per GPU: fused act + env step (f32 3x15x15 window) with autoreset, one launch per step",
                        "envs_per_gpu": B, "grid": a.dim, "algo": a.algo, "parallelism": f"dp{world} env shards"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_step", "avg_kernel_ms": avg_kernel_ms,
+                         "timing": "HIP events around the timed region on the launch stream",
                          "alg_bytes_per_instance_step": ALG_BYTES_PER_STEP},
             "generation": {"mazes": B, "seconds": round(gen_s, 3), "mazes_per_s": B / gen_s,
                            "note": "first build incl. module load; excluded from value"},

@@ -128,10 +128,24 @@ int mz_reset_done(mz_handle* h, int32_t regen_won, uint64_t seed, uint32_t epoch
  * :224-262) / the Enrich window (maze_handler.py:4-99). */
 int mz_step(mz_handle* h, const int32_t* actions_dev, const mz_step_out* out, void* stream);
 
-/* Fused act + step (one launch): each instance takes the epsilon-greedy action of mz_act
- * (below) and steps; actions_out_dev [B] (nullable) receives the actions taken.
- * flags: MZ_STEP_COUNT_ZEROED = out->done_count is already 0 (skip the memset). */
+/* flags of mz_step_ex / mz_step_act:
+ *   MZ_STEP_COUNT_ZEROED  out->done_count is already 0 (skip the memset).
+ *   MZ_STEP_AUTORESET     an instance whose previous step ended terminated|truncated is reset
+ *                         by this launch instead of stepping (BaseMazeEnv.reset,
+ *                         base_maze_env.py:136-161, same maze: the reference trainer's
+ *                         env.reset() at the top of the next episode,
+ *                         off_policy_trainer.py:153). Its action is ignored (actions_out = -1),
+ *                         reward 0, terminated = truncated = 0, outputs = the reset
+ *                         observation. One launch per vector step instead of step +
+ *                         mz_reset_done. */
 #define MZ_STEP_COUNT_ZEROED 1
+#define MZ_STEP_AUTORESET 2
+/* mz_step with flags. */
+int mz_step_ex(mz_handle* h, const int32_t* actions_dev, const mz_step_out* out, int32_t flags,
+               void* stream);
+
+/* Fused act + step (one launch): each instance takes the epsilon-greedy action of mz_act
+ * (below) and steps; actions_out_dev [B] (nullable) receives the actions taken. */
 int mz_step_act(mz_handle* h, const float* eps_dev, float eps_all, const int64_t* greedy_dev,
                 uint64_t seed, uint64_t counter, int32_t* actions_out_dev, const mz_step_out* out,
                 int32_t flags, void* stream);

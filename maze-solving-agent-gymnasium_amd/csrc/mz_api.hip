@@ -272,21 +272,29 @@ int mz_reset_done(mz_handle* h, int32_t regen_won, uint64_t seed, uint32_t epoch
   return MZ_OK;
 }
 
-int mz_step(mz_handle* h, const int32_t* actions_dev, const mz_step_out* out, void* stream) {
+int mz_step_ex(mz_handle* h, const int32_t* actions_dev, const mz_step_out* out, int32_t flags,
+               void* stream) {
   if (!h || !actions_dev) return fail(MZ_EINVAL, "bad arguments");
+  if (flags & ~(MZ_STEP_COUNT_ZEROED | MZ_STEP_AUTORESET)) return fail(MZ_EINVAL, "flags %d", flags);
   int rc = check_out(out);
   if (rc) return rc;
   DeviceGuard g(h->cfg.device);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (out && out->done_count) MZ_HIP(hipMemsetAsync(out->done_count, 0, sizeof(int32_t), s));
-  MZ_HIP(mz_launch_step(h->d, actions_dev, nullptr, to_dev(out), s));
+  if (out && out->done_count && !(flags & MZ_STEP_COUNT_ZEROED))
+    MZ_HIP(hipMemsetAsync(out->done_count, 0, sizeof(int32_t), s));
+  MZ_HIP(mz_launch_step(h->d, actions_dev, nullptr, (flags & MZ_STEP_AUTORESET) != 0, to_dev(out), s));
   return MZ_OK;
+}
+
+int mz_step(mz_handle* h, const int32_t* actions_dev, const mz_step_out* out, void* stream) {
+  return mz_step_ex(h, actions_dev, out, 0, stream);
 }
 
 int mz_step_act(mz_handle* h, const float* eps_dev, float eps_all, const int64_t* greedy_dev,
                 uint64_t seed, uint64_t counter, int32_t* actions_out_dev, const mz_step_out* out,
                 int32_t flags, void* stream) {
   if (!h) return fail(MZ_EINVAL, "null handle");
+  if (flags & ~(MZ_STEP_COUNT_ZEROED | MZ_STEP_AUTORESET)) return fail(MZ_EINVAL, "flags %d", flags);
   int rc = check_out(out);
   if (rc) return rc;
   DeviceGuard g(h->cfg.device);
@@ -294,7 +302,7 @@ int mz_step_act(mz_handle* h, const float* eps_dev, float eps_all, const int64_t
   if (out && out->done_count && !(flags & MZ_STEP_COUNT_ZEROED))
     MZ_HIP(hipMemsetAsync(out->done_count, 0, sizeof(int32_t), s));
   MzAct ap{eps_dev, eps_all, greedy_dev, seed, counter, actions_out_dev};
-  MZ_HIP(mz_launch_step(h->d, nullptr, &ap, to_dev(out), s));
+  MZ_HIP(mz_launch_step(h->d, nullptr, &ap, (flags & MZ_STEP_AUTORESET) != 0, to_dev(out), s));
   return MZ_OK;
 }
 

@@ -183,12 +183,13 @@ __device__ inline void dir_mask(uint32_t pw, uint32_t cw, bool tor, bool probs, 
 
 // epsilon-greedy with the reference exploration distribution (dqn_agent.py:104-116):
 // u < eps -> np.random.choice(4, p = mask / mask.sum()) by inverse CDF, else greedy.
-__device__ inline int act_sample(const MzAct& ap, int e, uint32_t pw, uint32_t cw, bool tor) {
+// ep / greedy: the instance's epsilon and greedy action (greedy < 0: always explore).
+__device__ inline int act_draw(const MzAct& ap, int e, float ep, int greedy, uint32_t pw,
+                               uint32_t cw, bool tor) {
   uint32_t u[4];
   mz_philox(ap.seed, MZ_ACT_STREAM ^ ((uint64_t)e << 32), ap.counter, u);
   const float ue = (float)(u[0] >> 8) * (1.0f / 16777216.0f);
-  const float ep = ap.eps ? ap.eps[e] : ap.eps_all;
-  if (ap.greedy && !(ue < ep)) return (int)ap.greedy[e];
+  if (greedy >= 0 && !(ue < ep)) return greedy;
   float m[4];
   dir_mask(pw, cw, tor, true, m);
   const float tot = m[0] + m[1] + m[2] + m[3];
@@ -199,78 +200,263 @@ __device__ inline int act_sample(const MzAct& ap, int e, uint32_t pw, uint32_t c
   return a;
 }
 
+__device__ inline int act_sample(const MzAct& ap, int e, uint32_t pw, uint32_t cw, bool tor) {
+  return act_draw(ap, e, ap.eps ? ap.eps[e] : ap.eps_all, ap.greedy ? (int)ap.greedy[e] : -1, pw,
+                  cw, tor);
+}
+
+// Plane words of one row: euclidean = the (open, visited) pairs of words W0 and W0 + 1
+// (columns 32*W0 .. 32*W0 + 63); toroidal = the whole row (NW <= 4 pairs).
+template <bool TOR>
+__device__ inline void load_row(const MzDev& d, size_t e, int R, int W0, uint32_t* w) {
+  const uint2* row = reinterpret_cast<const uint2*>(d.planes + (e * d.P + R) * d.PW);
+  if (!TOR) {
+    const uint2 a = row[W0], b = row[W0 + 1];
+    w[0] = a.x; w[1] = a.y; w[2] = b.x; w[3] = b.y;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint2 a = make_uint2(0u, 0u);
+      if (k < d.NW) a = row[k];
+      w[2 * k] = a.x;
+      w[2 * k + 1] = a.y;
+    }
+  }
+}
+
+// Window row R (first column C0) from its plane words: the three 15-bit channel rows of
+// get_mask_tensor (maze_handler.py:82-99) as in win_row above. Euclidean words start at column
+// 32*W0 <= C0 (C0 - 32*W0 <= 48).
+template <bool TOR>
+__device__ inline void win_bits(const uint32_t* w, int N, int R, int C0, int W0, int gr, int gc,
+                                int vr, int vc, bool vso, uint32_t& ch0, uint32_t& ch1,
+                                uint32_t& ch2) {
+  uint32_t open15, vis15, gmask = 0;
+  if (!TOR) {
+    const int sh = C0 - 32 * W0;
+    open15 = ext15(w[0], w[2], sh);
+    vis15 = vso ? 0u : ext15(w[1], w[3], sh);
+    if (R == vr) vis15 |= 1u << (vc - C0);
+    if (R == gr && gc >= C0 && gc < C0 + 15) gmask = 1u << (gc - C0);
+  } else {
+    const uint32_t ow[4] = {w[0], w[2], w[4], w[6]}, vw[4] = {w[1], w[3], w[5], w[7]};
+    open15 = row15_wrap(ow, C0, N);
+    vis15 = vso ? 0u : row15_wrap(vw, C0, N);
+    if (R == vr) vis15 |= wrap_colmask(vc, C0, N);
+    if (R == gr) gmask = wrap_colmask(gc, C0, N);
+  }
+  ch0 = ~open15 & 0x7FFFu;
+  ch1 = open15 & ~gmask;
+  ch2 = open15 & ~vis15;
+}
+
+// Rows and columns of the two windows a step can end in — around (r, c) if the agent stays,
+// around (tr, tc) if it moves (tr, tc one step away, or equal) — as one 16-row band:
+//   geo = R0 | W0 << 8 | offA << 12 | offB << 13 | vert << 14 | N << 16   (window X's row i is
+//         band row offX + i; band row k is grid row R0 + k, wrapped on the torus; vert = the
+//         band needs its 16th row)
+//   col = C0A | C0B << 8                                                   (first columns)
+template <bool TOR>
+__device__ inline void win_band(int r, int c, int tr, int tc, int N, int& geo, int& col) {
+  int R0, offA = 0, offB = 0, C0A, C0B, W0 = 0;
+  if (!TOR) {
+    const int sA = mz_win_start(r, N), sB = mz_win_start(tr, N);
+    R0 = min(sA, sB);
+    offA = sA - R0;
+    offB = sB - R0;
+    C0A = mz_win_start(c, N);
+    C0B = mz_win_start(tc, N);
+    W0 = min(C0A, C0B) >> 5;
+  } else {
+    const int rA = mz_wrap(r - 7, N);
+    R0 = rA;
+    if (tr != r) {
+      if (tr == mz_wrap(r + 1, N)) offB = 1;
+      else { R0 = mz_wrap(rA - 1, N); offA = 1; }
+    }
+    C0A = mz_wrap(c - 7, N);
+    C0B = mz_wrap(tc - 7, N);
+  }
+  geo = R0 | (W0 << 8) | (offA << 12) | (offB << 13) | ((offA | offB) << 14) | (N << 16);
+  col = C0A | (C0B << 8);
+}
+
+#define WIN_IT (IPW * 16 / WAVE)  // band rows per lane: lane l of pass it = instance 4*it + l/16, row l%16
+
 // ------------------------------------------------------------------------------------------
-template <bool TOR, bool ENRICH, bool ACT>
+// One vector step, 32 instances per 64-lane wave, with two dependent global round trips:
+//   level 1  per-instance state (5 coalesced u32 + eps/greedy or the given action), and the
+//            reward tables into LDS;
+//   level 2  target-cell word and its visit count (one lane per instance), and the 16-row
+//            plane band that holds BOTH windows the step can end in (agent stays / agent
+//            moves; one lane per band row, 16-B loads) — the move itself is decided by the
+//            target cell word that arrives in the same round trip;
+//   then     reward / counters (BaseMazeEnv.step, base_maze_env.py:163-210), the Enrich window
+//            assembled bit by bit in LDS from band rows picked with a lane shuffle (row i of
+//            the chosen window = band row off + i), and only then every global store: state,
+//            outputs, and the 32 windows as f32 with 16-B stores (1 KiB per wave instruction).
+//            No wait in the kernel ever covers a store.
+// AR (autoreset): an instance whose previous step ended terminated|truncated is reset by this
+// launch instead of stepping (BaseMazeEnv.reset, :136-161: same maze, agent at start, visits
+// cleared; the trainer's env.reset() after a finished episode) — its action is ignored
+// (actions_out = -1), reward 0, terminated = truncated = 0, obs = the reset observation.
+template <bool TOR, bool ENRICH, bool ACT, bool AR>
 __global__ __launch_bounds__(WAVE) void k_step(MzDev d, const int32_t* __restrict__ act, MzAct ap,
                                                MzOut o) {
   __shared__ uint32_t cat[CAT_WORDS];
-  __shared__ int4 prm[IPW];  // per instance: (r | c<<8 | N<<16, gr | gc<<8, vr, vc)
+  __shared__ __align__(16) double pen[512];  // pen_visit[256] | pen_inv[256]
   const int lane = threadIdx.x;
   const int e0 = blockIdx.x * IPW;
   const int nb = min(IPW, d.B - e0);
-  if (ENRICH)
-    for (int i = lane; i < CAT_WORDS; i += WAVE) cat[i] = 0u;
-  bool done = false;
   const int e = e0 + lane;
-  if (lane < nb) {
-    const size_t es = (size_t)e;
-    const uint32_t m0 = d.meta0[e], m1 = d.meta1[e];
-    uint32_t pw = d.posw[e], sw = d.stw[e], cw = d.curw[e];
-    int araw;
+  const size_t es = (size_t)e;
+  const bool live = lane < nb;
+
+  // ---- level 1
+  uint32_t m0 = 0u, m1 = 0u, pw = 0u, sw = 0u, cw = 0u;
+  float ep = 0.f;
+  int greedy = -1, araw = -1;
+  if (live) {
+    m0 = d.meta0[e]; m1 = d.meta1[e]; pw = d.posw[e]; sw = d.stw[e]; cw = d.curw[e];
     if (ACT) {
-      araw = act_sample(ap, e, pw, cw, TOR);
-      if (ap.act_out) ap.act_out[e] = araw;
+      ep = ap.eps ? ap.eps[e] : ap.eps_all;
+      if (ap.greedy) greedy = (int)ap.greedy[e];
     } else {
       araw = act[e];
     }
-    const int a = araw & 3;
-    const int N = m0 & 0xFF, gr = m1 & 0xFF, gc = (m1 >> 8) & 0xFF, maxs = m1 >> 16;
-    int r = pw & 0xFF, c = (pw >> 8) & 0xFF, nm = (pw >> 16) & 3, la = (pw >> 18) & 3;
-    int steps = sw & 0xFFFF, inv = (sw >> 16) & 0xFF;
-    double rew = 0.0;
-    bool term = false, trunc = false;
-    int vr = -1, vc = -1;
-    if (araw >= 0) {  // araw < 0: observe only (no transition, obs of the current state)
-      int nr = r + mz_dr(a), nc = c + mz_dc(a);
-      bool inb;
-      if (TOR) { nr = mz_wrap(nr, N); nc = mz_wrap(nc, N); inb = true; }
-      else inb = 0 < nr && nr < N - 1 && 0 < nc && nc < N - 1;  // maze_view.py:169 (Q3)
-      const uint32_t ncw = inb ? d.cells[es * d.P * d.P + (size_t)nr * d.P + nc] : 0u;
-      const bool moved = (ncw & MZ_CELL_OPEN) != 0u;
-      if (moved) {
-        const size_t vi = es * d.VP + (size_t)nr * d.P + nc;
-        const int cnt = d.visits[vi];
-        if (cnt == 0) {
-          // first entry: non_visited[cell] = 0 (base_maze_env.py:184)
-          vr = nr; vc = nc;
-          atomicOr(&d.planes[(es * d.P + nr) * d.PW + 2 * (nc >> 5) + 1], 1u << (nc & 31));
-          if (nr == gr && nc == gc) { rew = 1.0; term = true; }  // :185-187
-          else {  // (old_dist - new_dist) * 0.5 - 0.05 with len = D + 1 (:189-192)
-            const int dold = (int)(cw & MZ_CELL_D_MASK), dnew = (int)(ncw & MZ_CELL_D_MASK);
-            rew = __dsub_rn(__dmul_rn((double)(dold - dnew), 0.5), 0.05);
-          }
-        } else {
-          rew = d.pen_visit[cnt];  // :194
-        }
-        d.visits[vi] = (uint8_t)min(cnt + 1, 255);
-        inv = 0;
-        nm = min(nm + 1, 2);
-        la = a;
-        r = nr; c = nc; cw = ncw;
-      } else {
-        inv = min(inv + 1, 255);
-        rew = d.pen_inv[inv];  // :199-200
+  }
+  {
+    const uint4* pv = reinterpret_cast<const uint4*>(d.pen_visit);
+    const uint4* pi = reinterpret_cast<const uint4*>(d.pen_inv);
+    const uint4 t0 = pv[lane], t1 = pv[lane + WAVE], t2 = pi[lane], t3 = pi[lane + WAVE];
+    uint4* pl = reinterpret_cast<uint4*>(pen);
+    pl[lane] = t0; pl[lane + WAVE] = t1; pl[2 * WAVE + lane] = t2; pl[3 * WAVE + lane] = t3;
+  }
+  if (ENRICH)
+    for (int i = lane; i < CAT_WORDS; i += WAVE) cat[i] = 0u;
+
+  const int N = m0 & 0xFF, sr = (m0 >> 16) & 0xFF, sc = m0 >> 24;
+  const int gr = m1 & 0xFF, gc = (m1 >> 8) & 0xFF, maxs = m1 >> 16;
+  int r = pw & 0xFF, c = (pw >> 8) & 0xFF, nm = (pw >> 16) & 3, la = (pw >> 18) & 3;
+  int steps = sw & 0xFFFF, inv = (sw >> 16) & 0xFF;
+  const bool rst = AR && live && ((pw >> 20) & 1u);
+  if (ACT && live && !rst) araw = act_draw(ap, e, ep, greedy, pw, cw, TOR);
+  const int a = araw & 3;
+  const bool trans = live && !rst && araw >= 0;  // araw < 0: observe only (obs of current state)
+  // the cell the agent ends in if its move is legal (reset: the start cell)
+  int tr = r, tc = c;
+  bool inb = rst;
+  if (rst) { tr = sr; tc = sc; }
+  else if (trans) {
+    tr = r + mz_dr(a); tc = c + mz_dc(a);
+    if (TOR) { tr = mz_wrap(tr, N); tc = mz_wrap(tc, N); inb = true; }
+    else inb = 0 < tr && tr < N - 1 && 0 < tc && tc < N - 1;  // maze_view.py:169 (Q3)
+    if (!inb) { tr = r; tc = c; }
+  }
+
+  // ---- level 2
+  uint32_t ncw = 0u;
+  int cnt = 0;
+  if (inb) {
+    ncw = d.cells[es * d.P * d.P + (size_t)tr * d.P + tc];
+    if (!rst) cnt = d.visits[es * d.VP + (size_t)tr * d.P + tc];
+  }
+  constexpr int RW = TOR ? 8 : 4;
+  uint32_t wv[WIN_IT][RW];  // band row words
+  int geo = 0, col = 0;
+  if (ENRICH) {
+    if (live) win_band<TOR>(rst ? tr : r, rst ? tc : c, tr, tc, N, geo, col);  // reset: start only
+#pragma unroll
+    for (int it = 0; it < WIN_IT; ++it) {
+      const int j = it * (WAVE / 16) + (lane >> 4), k = lane & 15;
+      const int g = __shfl(geo, j);
+      if (j < nb && (k < 15 || ((g >> 14) & 1))) {
+        const int n_ = (g >> 16) & 0xFF, R0 = g & 0xFF;
+        load_row<TOR>(d, (size_t)(e0 + j), TOR ? mz_wrap(R0 + k, n_) : R0 + k, (g >> 8) & 0xF,
+                      wv[it]);
       }
-      steps = min(steps + 1, 65535);
-      trunc = steps > maxs;  // :205-208
-      if (trunc) rew = -1.0;
-      done = term || trunc;
-      d.posw[e] = (uint32_t)r | ((uint32_t)c << 8) | ((uint32_t)nm << 16) | ((uint32_t)la << 18) |
-                  ((uint32_t)done << 20);
-      d.stw[e] = (uint32_t)steps | ((uint32_t)inv << 16);
-      d.curw[e] = cw;
-      d.last_term[e] = term;
     }
+  }
+  __syncthreads();  // pen[] (single-wave workgroup: an LDS wait, no s_barrier)
+
+  // ---- transition (BaseMazeEnv.step) or reset
+  double rew = 0.0;
+  bool term = false, trunc = false, done = false, sel = false;
+  int vr = -1, vc = -1;
+  if (rst) {
+    r = sr; c = sc; cw = ncw; nm = 0; la = 0; steps = 0; inv = 0;
+    sel = true; vr = sr; vc = sc;  // visited = {start} (base_maze_env.py:148-149)
+  } else if (trans) {
+    if (ncw & MZ_CELL_OPEN) {  // moved (ncw = 0 when out of bounds)
+      if (cnt == 0) {
+        // first entry: non_visited[cell] = 0 (base_maze_env.py:184); plane bit set below
+        vr = tr; vc = tc;
+        if (tr == gr && tc == gc) { rew = 1.0; term = true; }  // :185-187
+        else {  // (old_dist - new_dist) * 0.5 - 0.05 with len = D + 1 (:189-192)
+          const int dold = (int)(cw & MZ_CELL_D_MASK), dnew = (int)(ncw & MZ_CELL_D_MASK);
+          rew = __dsub_rn(__dmul_rn((double)(dold - dnew), 0.5), 0.05);
+        }
+      } else {
+        rew = pen[cnt];  // :194
+      }
+      inv = 0;
+      nm = min(nm + 1, 2);
+      la = a;
+      r = tr; c = tc; cw = ncw;
+      sel = true;
+    } else {
+      inv = min(inv + 1, 255);
+      rew = pen[256 + inv];  // :199-200
+    }
+    steps = min(steps + 1, 65535);
+    trunc = steps > maxs;  // :205-208
+    if (trunc) rew = -1.0;
+    done = term || trunc;
+  }
+
+  // ---- window bits in LDS (compute only: every global store of the step comes after, so no
+  // wait in this kernel ever covers a store)
+  if (ENRICH) {
+    const int ps = (int)sel | ((int)rst << 1) | ((vr + 1) << 8) | ((vc + 1) << 16);
+    const int pg = gr | (gc << 8);
+#pragma unroll
+    for (int it = 0; it < WIN_IT; ++it) {
+      const int j = it * (WAVE / 16) + (lane >> 4), i = lane & 15;
+      const int s_ = __shfl(ps, j), g = __shfl(geo, j), cc = __shfl(col, j), gg = __shfl(pg, j);
+      const bool useb = s_ & 1;
+      const int off = useb ? ((g >> 13) & 1) : ((g >> 12) & 1);
+      uint32_t w[RW];
+#pragma unroll
+      for (int k = 0; k < RW; ++k) w[k] = (uint32_t)__shfl((int)wv[it][k], (lane + off) & (WAVE - 1));
+      if (j < nb && i < 15) {
+        const int n_ = (g >> 16) & 0xFF, R0 = g & 0xFF;
+        const int R = TOR ? mz_wrap(R0 + i + off, n_) : R0 + i + off;
+        const int C0 = useb ? ((cc >> 8) & 0xFF) : (cc & 0xFF);
+        uint32_t c0, c1, c2;
+        win_bits<TOR>(w, n_, R, C0, (g >> 8) & 0xF, gg & 0xFF, (gg >> 8) & 0xFF,
+                      ((s_ >> 8) & 0xFF) - 1, ((s_ >> 16) & 0xFF) - 1, (s_ >> 1) & 1, c0, c1, c2);
+        const int base = j * 675 + i * 15;
+        cat_put(cat, base, c0);
+        cat_put(cat, base + 225, c1);
+        cat_put(cat, base + 450, c2);
+      }
+    }
+  }
+
+  // ---- stores: state, per-instance outputs, then the windows
+  if (rst || trans) {
+    d.posw[e] = (uint32_t)r | ((uint32_t)c << 8) | ((uint32_t)nm << 16) | ((uint32_t)la << 18) |
+                ((uint32_t)done << 20);
+    d.stw[e] = (uint32_t)steps | ((uint32_t)inv << 16);
+    d.curw[e] = cw;
+    d.last_term[e] = term;
+    if (sel && !rst) {
+      if (vr >= 0) atomicOr(&d.planes[(es * d.P + tr) * d.PW + 2 * (tc >> 5) + 1], 1u << (tc & 31));
+      d.visits[es * d.VP + (size_t)tr * d.P + tc] = (uint8_t)min(cnt + 1, 255);
+    }
+  }
+  if (live) {
+    if (ACT && ap.act_out) ap.act_out[e] = rst ? -1 : araw;
     int br, bc;
     best_dir(r, c, cw, N, TOR, br, bc);
     if (o.reward) o.reward[e] = (float)rew;
@@ -280,8 +466,31 @@ __global__ __launch_bounds__(WAVE) void k_step(MzDev d, const int32_t* __restric
     if (o.pos) { o.pos[2 * es] = r; o.pos[2 * es + 1] = c; }
     if (o.best_dir) { o.best_dir[2 * es] = br; o.best_dir[2 * es + 1] = bc; }
     if (o.obs6) write_obs6<ENRICH>(o.obs6 + 6 * es, r, c, gr, gc, br, bc, N);
-    if (ENRICH) prm[lane] = make_int4(r | (c << 8) | (N << 16), gr | (gc << 8), vr, vc);
   }
+  if (ENRICH) {
+    __syncthreads();
+    if (o.window_bits) store_window_bits(cat, o.window_bits + (size_t)e0 * MZ_WINDOW_WORDS, nb, lane);
+    if (o.window) store_window_f32(cat, o.window + (size_t)e0 * 675, nb, lane);
+  }
+
+  if (AR) {  // reset instances: visits[:] = 0, visited plane = {start} (wave-cooperative)
+    unsigned long long bal = __ballot(rst);
+    const int sp = sr | (sc << 8);
+    while (bal) {
+      const int j = __ffsll((long long)bal) - 1;
+      bal &= bal - 1;
+      const int q = __shfl(sp, j), srj = q & 0xFF, scj = (q >> 8) & 0xFF;
+      const size_t ej = (size_t)(e0 + j);
+      uint4* v4 = reinterpret_cast<uint4*>(d.visits + ej * d.VP);
+      for (int k = lane; k < d.VP / 16; k += WAVE) v4[k] = make_uint4(0u, 0u, 0u, 0u);
+      for (int k = lane; k < d.P * d.NW; k += WAVE) {
+        const int R = k / d.NW, w = k - R * d.NW;
+        d.planes[(ej * d.P + R) * d.PW + 2 * w + 1] =
+            (R == srj && w == (scj >> 5)) ? (1u << (scj & 31)) : 0u;
+      }
+    }
+  }
+
   // done-list compaction: wave ballot + one atomic per wave
   if (o.done_idx) {
     const unsigned long long bal = __ballot(done);
@@ -291,24 +500,6 @@ __global__ __launch_bounds__(WAVE) void k_step(MzDev d, const int32_t* __restric
       base = __shfl(base, 0);
       if (done) o.done_idx[base + __popcll(bal & ((1ull << lane) - 1ull))] = e;
     }
-  }
-  if (ENRICH) {
-    __syncthreads();
-    for (int p = lane; p < nb * 15; p += WAVE) {
-      const int j = p / 15, i = p - 15 * j;
-      const int4 q = prm[j];
-      uint32_t c0, c1, c2;
-      win_row(d, (size_t)(e0 + j), TOR, (q.x >> 16) & 0xFF, q.x & 0xFF, (q.x >> 8) & 0xFF,
-              q.y & 0xFF, (q.y >> 8) & 0xFF, q.z, q.w, false, i, c0, c1, c2);
-      const int base = j * 675 + i * 15;
-      cat_put(cat, base, c0);
-      cat_put(cat, base + 225, c1);
-      cat_put(cat, base + 450, c2);
-    }
-    __syncthreads();
-    if (o.window_bits) store_window_bits(cat, o.window_bits + (size_t)e0 * MZ_WINDOW_WORDS, nb, lane);
-    if (o.window)
-      store_window_f32(cat, o.window + (size_t)e0 * 675, nb, lane);
   }
 }
 
@@ -572,20 +763,30 @@ hipError_t mz_launch_regen(const MzDev& d, const int32_t* idx, const int32_t* co
   return hipGetLastError();
 }
 
-hipError_t mz_launch_step(const MzDev& d, const int32_t* act, const MzAct* ap, const MzOut& o,
-                          hipStream_t s) {
+template <bool T, bool E>
+void launch_step_te(const MzDev& d, const int32_t* act, const MzAct& a, bool has_act, bool ar,
+                    const MzOut& o, hipStream_t s) {
   dim3 grid((d.B + IPW - 1) / IPW), block(WAVE);
+  if (has_act) {
+    if (ar) hipLaunchKernelGGL((k_step<T, E, true, true>), grid, block, 0, s, d, act, a, o);
+    else hipLaunchKernelGGL((k_step<T, E, true, false>), grid, block, 0, s, d, act, a, o);
+  } else {
+    if (ar) hipLaunchKernelGGL((k_step<T, E, false, true>), grid, block, 0, s, d, act, a, o);
+    else hipLaunchKernelGGL((k_step<T, E, false, false>), grid, block, 0, s, d, act, a, o);
+  }
+}
+
+hipError_t mz_launch_step(const MzDev& d, const int32_t* act, const MzAct* ap, bool autoreset,
+                          const MzOut& o, hipStream_t s) {
   MzAct a{};
   if (ap) a = *ap;
-#define MZ_ST(T, E, A) hipLaunchKernelGGL((k_step<T, E, A>), grid, block, 0, s, d, act, a, o)
-  if (ap) {
-    if (d.toroidal) { if (d.enrich) MZ_ST(true, true, true); else MZ_ST(true, false, true); }
-    else { if (d.enrich) MZ_ST(false, true, true); else MZ_ST(false, false, true); }
+  if (d.toroidal) {
+    if (d.enrich) launch_step_te<true, true>(d, act, a, ap != nullptr, autoreset, o, s);
+    else launch_step_te<true, false>(d, act, a, ap != nullptr, autoreset, o, s);
   } else {
-    if (d.toroidal) { if (d.enrich) MZ_ST(true, true, false); else MZ_ST(true, false, false); }
-    else { if (d.enrich) MZ_ST(false, true, false); else MZ_ST(false, false, false); }
+    if (d.enrich) launch_step_te<false, true>(d, act, a, ap != nullptr, autoreset, o, s);
+    else launch_step_te<false, false>(d, act, a, ap != nullptr, autoreset, o, s);
   }
-#undef MZ_ST
   return hipGetLastError();
 }
 

@@ -9,8 +9,8 @@ hipError_t mz_launch_build(const MzDev& d, const int32_t* env_ids, int32_t n, bo
                            const uint8_t* grids, const int32_t* start_goal, hipStream_t s);
 hipError_t mz_launch_regen(const MzDev& d, const int32_t* idx, const int32_t* count,
                            int32_t n_static, uint64_t seed, uint32_t epoch, hipStream_t s);
-hipError_t mz_launch_step(const MzDev& d, const int32_t* act, const MzAct* ap, const MzOut& o,
-                          hipStream_t s);
+hipError_t mz_launch_step(const MzDev& d, const int32_t* act, const MzAct* ap, bool autoreset,
+                          const MzOut& o, hipStream_t s);
 hipError_t mz_launch_reset_list(const MzDev& d, const int32_t* idx, int32_t* count,
                                 int32_t n_static, const MzOut& o, hipStream_t s);
 hipError_t mz_launch_meta(const MzDev& d, int32_t* out, hipStream_t s);

@@ -30,10 +30,11 @@ class EnvInfo(C.Structure):
 
 
 MZ_STEP_COUNT_ZEROED = 1
+MZ_STEP_AUTORESET = 2
 MZ_ERRORS = {-1: ValueError, -2: ValueError, -3: RuntimeError, -4: MemoryError, -5: ValueError}
 
 EXPORTS = ["mz_last_error", "mz_device_count", "mz_create", "mz_destroy", "mz_load_mazes",
-           "mz_generate", "mz_reset_all", "mz_reset_list", "mz_reset_done", "mz_step", "mz_direction_mask",
+           "mz_generate", "mz_reset_all", "mz_reset_list", "mz_reset_done", "mz_step", "mz_step_ex", "mz_direction_mask",
            "mz_act", "mz_step_act", "mz_expand_window", "mz_set_algorithm", "mz_query", "mz_get_grid",
            "mz_difficulty", "mz_get_meta", "mz_discounted_returns", "mz_q_front",
            "mz_bank_create", "mz_bank_fill", "mz_bank_use", "mz_bank_consumed"]
@@ -68,6 +69,7 @@ def load(build_if_missing=True):
                                 C.POINTER(StepOut), vp]
     L.mz_reset_done.argtypes = [vp, C.c_int32, C.c_uint64, C.c_uint32, C.POINTER(StepOut), vp]
     L.mz_step.argtypes = [vp, vp, C.POINTER(StepOut), vp]
+    L.mz_step_ex.argtypes = [vp, vp, C.POINTER(StepOut), C.c_int32, vp]
     L.mz_direction_mask.argtypes = [vp, C.c_int32, vp, vp]
     L.mz_act.argtypes = [vp, vp, C.c_float, vp, C.c_uint64, C.c_uint64, vp, vp]
     L.mz_step_act.argtypes = [vp, vp, C.c_float, vp, C.c_uint64, C.c_uint64, vp,

@@ -213,21 +213,28 @@ class VectorMazeEnv:
         """Auto-reset from the step's device done list (consumes done_count)."""
         self.reset_list(self.done_idx, self.done_count, regen_won=regen_won, seed=seed)
 
-    def step(self, actions):
-        """actions: int tensor [B] on the device (negative = observe only)."""
+    def step(self, actions, autoreset=False):
+        """actions: int tensor [B] on the device (negative = observe only). With autoreset,
+        instances whose previous step ended are reset by this launch instead (action ignored,
+        reward 0, reset observation) — the trainer's env.reset() folded into the next step."""
         a = actions if (actions.dtype == torch.int32 and actions.device == self.device) else \
             actions.to(device=self.device, dtype=torch.int32)
         a = a.contiguous()
-        N.check(self.lib.mz_step(self._h, a.data_ptr(), N.C.byref(self._out), self._stream()))
+        flags = N.MZ_STEP_AUTORESET if autoreset else 0
+        N.check(self.lib.mz_step_ex(self._h, a.data_ptr(), N.C.byref(self._out), flags,
+                                    self._stream()))
         self._count_zero = False
         return self.obs(), self.reward, self.truncated, self.terminated, {}
 
-    def step_act(self, eps=1.0, greedy=None, seed=0, counter=0, actions_out=None):
-        """Fused epsilon-greedy act + step in one launch (actions taken -> actions_out)."""
+    def step_act(self, eps=1.0, greedy=None, seed=0, counter=0, actions_out=None, autoreset=False):
+        """Fused epsilon-greedy act + step in one launch (actions taken -> actions_out; -1 for
+        the instances an autoreset step resets)."""
         out = self.actions if actions_out is None else actions_out
         eps_t = eps if torch.is_tensor(eps) else None
         g = None if greedy is None else greedy.to(dtype=torch.int64).contiguous()
         flags = N.MZ_STEP_COUNT_ZEROED if self._count_zero else 0
+        if autoreset:
+            flags |= N.MZ_STEP_AUTORESET
         N.check(self.lib.mz_step_act(self._h, _ptr(eps_t), float(eps) if eps_t is None else 0.0,
                                      _ptr(g), seed & 0xFFFFFFFFFFFFFFFF,
                                      counter & 0xFFFFFFFFFFFFFFFF, out.data_ptr(),

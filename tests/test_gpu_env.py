@@ -225,3 +225,46 @@ def test_regen_on_win(mazerl):
             assert q["max_steps"] == O.max_steps(g, (q["start_r"], q["start_c"]), (q["goal_r"], q["goal_c"]))
     assert changed >= len(won) - 1
     env.close()
+
+
+@pytest.mark.parametrize("tor,dim,B", [(False, 15, 192), (False, 21, 192), (True, 17, 192),
+                                       (True, 29, 128)])
+def test_autoreset_step_vs_oracle(mazerl, tor, dim, B):
+    """MZ_STEP_AUTORESET (one launch per vector step): an instance whose previous step ended is
+    reset by the next launch (action ignored, reported as -1, reward 0, reset observation);
+    every other instance steps with its sampled action. Replayed through the oracle, which
+    calls reset() exactly where the reference trainer does (off_policy_trainer.py:153)."""
+    import pyoracle as O
+    env = mazerl.VectorMazeEnv(B, dim, toroidal=tor, enrich=True, reward64=True, seed=4242)
+    ors = []
+    for i in range(B):
+        q = env.query(i)
+        o = O.Env(env.grid(i), (q["start_r"], q["start_c"]), (q["goal_r"], q["goal_c"]), tor, True)
+        o.reset()
+        ors.append(o)
+    was_done = np.zeros(B, bool)
+    resets = 0
+    for k in range(400):
+        env.step_act(eps=1.0, seed=21, counter=k, autoreset=True)
+        a = env.actions.cpu().numpy()
+        r64 = env.reward64.cpu().numpy()
+        te, tr = env.terminated.cpu().numpy(), env.truncated.cpu().numpy()
+        pos, bd = env.pos.cpu().numpy(), env.best_dir.cpu().numpy()
+        win = env.window.cpu().numpy()
+        bits = env.expand_window(env.window_bits).cpu().numpy()
+        for i in range(B):
+            if was_done[i]:
+                assert a[i] == -1, (k, i)
+                o = ors[i].reset()
+                resets += 1
+            else:
+                assert 0 <= a[i] < 4, (k, i)
+                o = ors[i].step(int(a[i]))
+            assert r64[i] == o["reward"], (k, i)
+            assert bool(te[i]) == o["terminated"] and bool(tr[i]) == o["truncated"], (k, i)
+            assert tuple(pos[i]) == o["pos"] and tuple(bd[i]) == o["best_dir"], (k, i)
+            np.testing.assert_array_equal(win[i], o["window"].astype(np.float32))
+            np.testing.assert_array_equal(bits[i], win[i])
+            was_done[i] = o["terminated"] or o["truncated"]
+    assert resets > 0
+    env.close()
