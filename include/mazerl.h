@@ -102,6 +102,27 @@ int mz_load_mazes(mz_handle* h, const uint8_t* grids_host, int32_t dim,
 int mz_generate(mz_handle* h, const int32_t* env_ids_dev, int32_t n, const uint8_t* algo_dev,
                 int32_t algo_all, int32_t dim, uint64_t seed, void* stream);
 
+/* rng of mz_generate_ex:
+ *   MZ_RNG_PHILOX   Philox4x32 stream seed + env_id (as mz_generate): every random choice of the
+ *                   reference is drawn uniformly over the same candidates (distribution parity).
+ *   MZ_RNG_CPYTHON  CPython-exact: instance env_id gets the maze the reference builds with
+ *                   `random.seed(seed + env_id); gen_maze((dim, dim), algo)` (toroidal:
+ *                   gen_maze_no_border), bit for bit — MT19937 draws and CPython 3.10 set
+ *                   iteration order emulated on the GPU (maze_generation.py:6-185). */
+#define MZ_RNG_PHILOX 0
+#define MZ_RNG_CPYTHON 1
+int mz_generate_ex(mz_handle* h, const int32_t* env_ids_dev, int32_t n, const uint8_t* algo_dev,
+                   int32_t algo_all, int32_t dim, uint64_t seed, int32_t rng, void* stream);
+
+/* One CPython-exact maze for instance `env` from an explicit Python random state:
+ * state_host[625] = random.getstate()[1] (624 MT19937 words + index), advanced in place exactly
+ * as gen_maze((dim, dim), algo) would advance Python's global random (the caller writes it back
+ * with random.setstate). Used by the single-env drop-in classes so that random.seed(s) before
+ * construction gives the reference's maze (base_maze_env.py:78-97 draws six candidates from the
+ * global stream). Synchronous. */
+int mz_generate_state(mz_handle* h, int32_t env, int32_t dim, int32_t algo, uint32_t* state_host,
+                      void* stream);
+
 /* Reset every instance / a device list of instances (e.g. step's done_idx/done_count) and
  * write their reset observations into `out`. Replaces BaseMazeEnv.reset (base_maze_env.py:136-161).
  * A non-NULL count_dev is consumed: the kernel sets it to 0 once every workgroup has read it,

@@ -217,23 +217,60 @@ int mz_load_mazes(mz_handle* h, const uint8_t* grids_host, int32_t dim,
   MZ_HIP(hipMemcpyAsync(dg, grids_host, n * cells, hipMemcpyHostToDevice, s));
   MZ_HIP(hipMemcpyAsync(dsg, sg_host, 16 * (size_t)n, hipMemcpyHostToDevice, s));
   if (env_ids_host) MZ_HIP(hipMemcpyAsync(dids, env_ids_host, 4 * (size_t)n, hipMemcpyHostToDevice, s));
-  MZ_HIP(mz_launch_build(h->d, env_ids_host ? dids : nullptr, n, false, nullptr, 0, dim, 0, dg, dsg, s));
+  MZ_HIP(mz_launch_build(h->d, env_ids_host ? dids : nullptr, n, false, nullptr, 0, dim, 0, dg, dsg,
+                         0, nullptr, s));
   MZ_HIP(hipStreamSynchronize(s));
+  return MZ_OK;
+}
+
+int mz_generate_ex(mz_handle* h, const int32_t* env_ids_dev, int32_t n, const uint8_t* algo_dev,
+                   int32_t algo_all, int32_t dim, uint64_t seed, int32_t rng, void* stream) {
+  if (!h) return fail(MZ_EINVAL, "null handle");
+  if (!env_ids_dev) n = h->d.B;
+  if (n < 0 || n > h->d.B) return fail(MZ_EINVAL, "n out of range");
+  if (!algo_dev && (algo_all < 0 || algo_all > 2)) return fail(MZ_EINVAL, "algorithm id %d", algo_all);
+  if (rng != MZ_RNG_PHILOX && rng != MZ_RNG_CPYTHON) return fail(MZ_EINVAL, "rng %d", rng);
+  int rc = check_dim(h, dim);
+  if (rc) return rc;
+  DeviceGuard g(h->cfg.device);
+  MZ_HIP(mz_launch_build(h->d, env_ids_dev, n, true, algo_dev, algo_all, dim, seed, nullptr,
+                         nullptr, rng == MZ_RNG_CPYTHON ? 1 : 0, nullptr,
+                         static_cast<hipStream_t>(stream)));
   return MZ_OK;
 }
 
 int mz_generate(mz_handle* h, const int32_t* env_ids_dev, int32_t n, const uint8_t* algo_dev,
                 int32_t algo_all, int32_t dim, uint64_t seed, void* stream) {
-  if (!h) return fail(MZ_EINVAL, "null handle");
-  if (!env_ids_dev) n = h->d.B;
-  if (n < 0 || n > h->d.B) return fail(MZ_EINVAL, "n out of range");
-  if (!algo_dev && (algo_all < 0 || algo_all > 2)) return fail(MZ_EINVAL, "algorithm id %d", algo_all);
+  return mz_generate_ex(h, env_ids_dev, n, algo_dev, algo_all, dim, seed, MZ_RNG_PHILOX, stream);
+}
+
+int mz_generate_state(mz_handle* h, int32_t env, int32_t dim, int32_t algo, uint32_t* state_host,
+                      void* stream) {
+  if (!h || !state_host || env < 0 || env >= h->d.B) return fail(MZ_EINVAL, "bad arguments");
+  if (algo < 0 || algo > 2) return fail(MZ_EINVAL, "algorithm id %d", algo);
+  if (state_host[624] > 624u) return fail(MZ_EINVAL, "random state index %u", state_host[624]);
   int rc = check_dim(h, dim);
   if (rc) return rc;
-  if (h->d.toroidal && dim + 2 > MZ_MAX_DIM + 2) return fail(MZ_EINVAL_SHAPE, "dim too large");
   DeviceGuard g(h->cfg.device);
-  MZ_HIP(mz_launch_build(h->d, env_ids_dev, n, true, algo_dev, algo_all, dim, seed, nullptr,
-                         nullptr, static_cast<hipStream_t>(stream)));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const size_t need = 625 * sizeof(uint32_t) + 16;
+  if (need > h->staging_bytes) {
+    if (h->staging) MZ_HIP(hipFree(h->staging));
+    h->staging = nullptr;
+    MZ_HIP(hipMalloc(&h->staging, need));
+    h->staging_bytes = need;
+  }
+  uint32_t* dst = reinterpret_cast<uint32_t*>(h->staging);
+  int32_t* ids = reinterpret_cast<int32_t*>(h->staging + 625 * sizeof(uint32_t) + 4);
+  int err = 0;
+  MZ_HIP(hipMemcpyAsync(dst, state_host, 625 * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  MZ_HIP(hipMemcpyAsync(ids, &env, sizeof(int32_t), hipMemcpyHostToDevice, s));
+  MZ_HIP(hipMemsetAsync(h->d.ticket + MZ_TICKET_PYERR, 0, sizeof(int), s));
+  MZ_HIP(mz_launch_build(h->d, ids, 1, true, nullptr, algo, dim, 0, nullptr, nullptr, 2, dst, s));
+  MZ_HIP(hipMemcpyAsync(state_host, dst, 625 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  MZ_HIP(hipMemcpyAsync(&err, h->d.ticket + MZ_TICKET_PYERR, sizeof(int), hipMemcpyDeviceToHost, s));
+  MZ_HIP(hipStreamSynchronize(s));
+  if (err) return fail(MZ_EHIP, "CPython set emulation overflowed its table (flag %d)", err);
   return MZ_OK;
 }
 

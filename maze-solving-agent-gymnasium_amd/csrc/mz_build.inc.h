@@ -274,15 +274,71 @@ __device__ inline uint32_t mz_cell_word(const MzBuildLds& L, int N, bool tor, in
   return D | ((uint32_t)code << MZ_CELL_CODE_SHIFT) | MZ_CELL_OPEN | (nbm << MZ_CELL_NB_SHIFT);
 }
 
-// Builds maze + tables of instance e and resets it. generate: Philox generation with algo/seed;
+#include "mz_pygen.inc.h"
+
+// LDS of a build launch: the build region, plus the CPython-exact generation region when used
+__host__ __device__ inline size_t mz_build_lds_bytes_mode(int P, int pymode) {
+  return mz_build_lds_bytes(P) + (pymode ? mz_py_lds_bytes(P + 2) : 0);
+}
+
+__device__ inline MzPyLds mz_py_lds(uint8_t* base, const MzBuildLds& L, int G) {
+  MzPyLds Y;
+  Y.mt = reinterpret_cast<uint32_t*>(base);
+  Y.hdr = reinterpret_cast<int*>(base + 2512);
+  Y.cap_a = mz_py_cap_a(G);
+  Y.cap_b = mz_py_cap_b(G);
+  Y.ta = reinterpret_cast<uint16_t*>(base + 2560);
+  Y.tb = Y.ta + Y.cap_a;
+  Y.scratch = L.dist;  // dist + queue (contiguous, 4 G^2 bytes): free while generating
+  Y.G = G;
+  return Y;
+}
+
+#define MZ_PY_PHILOX 0  // Philox4x32 stream (seed), uniform choices over the same candidates
+#define MZ_PY_SEED 1    // CPython-exact from random.seed(seed)
+#define MZ_PY_STATE 2   // CPython-exact from the random.getstate() words in py_state (in/out)
+
+// Builds maze + tables of instance e and resets it. generate: generation with algo/seed
+// (pymode: MZ_PY_*; py_state [625] for MZ_PY_STATE, py_err set on a set-table overflow);
 // else import grid_src [N][N] with (sr,sc,gr,gc). Returns via d.meta*: all lanes must call.
 __device__ void mz_build_one(const MzDev& d, int e, bool tor, bool generate, int algo,
                              uint64_t seed, int N, const uint8_t* grid_src, int isr, int isc,
-                             int igr, int igc, uint8_t* lds) {
+                             int igr, int igc, uint8_t* lds, int pymode = MZ_PY_PHILOX,
+                             uint32_t* py_state = nullptr, int* py_err = nullptr) {
   const int lane = threadIdx.x;
   const MzBuildLds L = mz_build_lds(lds, d.P);
   int sr, sc, gr, gc;
-  if (generate) {
+  if (generate && pymode != MZ_PY_PHILOX) {
+    const int G = tor ? N + 2 : N;
+    for (int i = lane; i < G * G; i += 64) L.g[i] = 0;
+    const MzPyLds Y = mz_py_lds(lds + mz_build_lds_bytes(d.P), L, G);
+    if (lane == 0) {
+      if (pymode == MZ_PY_SEED) mz_mt_seed(Y.mt, seed);
+      else for (int i = 0; i < 625; ++i) Y.mt[i] = py_state[i];
+    }
+    __syncthreads();
+    const int s = mz_py_generate(L, Y, G, algo);
+    if (lane == 0) {
+      if (pymode == MZ_PY_STATE) for (int i = 0; i < 625; ++i) py_state[i] = Y.mt[i];
+      if (Y.hdr[6] && py_err) atomicOr(py_err, Y.hdr[6]);
+    }
+    int goal = mz_goal_select(L, G, s);
+    if (goal < 0) goal = s;
+    __syncthreads();
+    if (lane == 0) L.g[goal] = 2;
+    __syncthreads();
+    sr = s / G; sc = s - sr * G; gr = goal / G; gc = goal - gr * G;
+    if (tor) {  // crop the border (maze_generation.py:53-55)
+      for (int i = lane; i < N * N; i += 64) {
+        const int r = i / N, c = i - r * N;
+        L.dist[i] = L.g[(r + 1) * G + (c + 1)];
+      }
+      __syncthreads();
+      for (int i = lane; i < N * N; i += 64) L.g[i] = (uint8_t)L.dist[i];
+      __syncthreads();
+      sr -= 1; sc -= 1; gr -= 1; gc -= 1;
+    }
+  } else if (generate) {
     const int G = tor ? N + 2 : N;
     for (int i = lane; i < G * G; i += 64) L.g[i] = 0;
     __syncthreads();

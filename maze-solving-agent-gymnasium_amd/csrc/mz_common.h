@@ -27,6 +27,7 @@
 #define MZ_CELL_CODE_SHIFT 16
 #define MZ_CELL_OPEN (1u << 19)
 #define MZ_CELL_NB_SHIFT 20
+#define MZ_TICKET_PYERR 8
 
 struct MzDev {
   int B, P, VP, toroidal, enrich;
@@ -43,7 +44,8 @@ struct MzDev {
   uint8_t* last_term;       // per-instance: last step terminated (for regen_won)
   const double* pen_visit;  // [256] 0.0 - (1 - exp(-0.2 k))   (base_maze_env.py:194)
   const double* pen_inv;    // [256] 0.0 - (1 - exp(-0.15 k))  (base_maze_env.py:200)
-  int* ticket;              // exit ticket of k_reset_list (done-count consumption)
+  int* ticket;              // [16]: [0] exit ticket of k_reset_list (done-count consumption),
+                            // [MZ_TICKET_PYERR] CPython-generation set-table overflow flag
   // Active maze bank (mz_bank_*): mazes generated ahead of time that a win copies in instead
   // of building one inside the reset launch. Slot j of algorithm a lives at index
   // bk_aidx(a) * bk_K + j of the bank arrays; bk_head[a] counts the slots consumed so far.

@@ -648,14 +648,16 @@ __global__ __launch_bounds__(WAVE) void k_reset_done(MzDev d, int regen, uint64_
 __global__ __launch_bounds__(WAVE) void k_build(MzDev d, const int32_t* env_ids, int32_t n,
                                                 int generate, const uint8_t* algo_list,
                                                 int32_t algo_all, int32_t dim, uint64_t seed,
-                                                const uint8_t* grids, const int32_t* sg) {
+                                                const uint8_t* grids, const int32_t* sg,
+                                                int pymode, uint32_t* py_state) {
   extern __shared__ __align__(16) uint8_t lds[];
   for (int j = blockIdx.x; j < n; j += gridDim.x) {
     const int e = env_ids ? env_ids[j] : j;
     if (generate) {
       const int algo = algo_list ? algo_list[j] : algo_all;
       if (threadIdx.x == 0) d.algo[e] = (uint8_t)algo;
-      mz_build_one(d, e, d.toroidal, true, algo, seed + (uint64_t)e, dim, nullptr, 0, 0, 0, 0, lds);
+      mz_build_one(d, e, d.toroidal, true, algo, seed + (uint64_t)e, dim, nullptr, 0, 0, 0, 0, lds,
+                   pymode, py_state, d.ticket + MZ_TICKET_PYERR);
     } else {
       mz_build_one(d, e, d.toroidal, false, 0, 0, dim, grids + (size_t)j * dim * dim,
                    sg[4 * j], sg[4 * j + 1], sg[4 * j + 2], sg[4 * j + 3], lds);
@@ -744,12 +746,15 @@ size_t mz_build_lds_size(int P) { return mz_build_lds_bytes(P); }
 
 hipError_t mz_launch_build(const MzDev& d, const int32_t* env_ids, int32_t n, bool generate,
                            const uint8_t* algo_list, int32_t algo_all, int32_t dim, uint64_t seed,
-                           const uint8_t* grids, const int32_t* start_goal, hipStream_t s) {
+                           const uint8_t* grids, const int32_t* start_goal, int pymode,
+                           uint32_t* py_state, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipError_t ae = mz_lds_attr(reinterpret_cast<const void*>(k_build), mz_build_lds_bytes(d.P));
+  const size_t lds = mz_build_lds_bytes_mode(d.P, generate ? pymode : 0);
+  hipError_t ae = mz_lds_attr(reinterpret_cast<const void*>(k_build), lds);
   if (ae != hipSuccess) return ae;
-  hipLaunchKernelGGL(k_build, dim3(mz_grid_for(n)), dim3(WAVE), mz_build_lds_bytes(d.P), s, d,
-                     env_ids, n, (int)generate, algo_list, algo_all, dim, seed, grids, start_goal);
+  hipLaunchKernelGGL(k_build, dim3(mz_grid_for(n)), dim3(WAVE), lds, s, d, env_ids, n,
+                     (int)generate, algo_list, algo_all, dim, seed, grids, start_goal, pymode,
+                     py_state);
   return hipGetLastError();
 }
 

@@ -6,7 +6,8 @@
 size_t mz_build_lds_size(int P);
 hipError_t mz_launch_build(const MzDev& d, const int32_t* env_ids, int32_t n, bool generate,
                            const uint8_t* algo_list, int32_t algo_all, int32_t dim, uint64_t seed,
-                           const uint8_t* grids, const int32_t* start_goal, hipStream_t s);
+                           const uint8_t* grids, const int32_t* start_goal, int pymode,
+                           uint32_t* py_state, hipStream_t s);
 hipError_t mz_launch_regen(const MzDev& d, const int32_t* idx, const int32_t* count,
                            int32_t n_static, uint64_t seed, uint32_t epoch, hipStream_t s);
 hipError_t mz_launch_step(const MzDev& d, const int32_t* act, const MzAct* ap, bool autoreset,

@@ -31,10 +31,11 @@ class EnvInfo(C.Structure):
 
 MZ_STEP_COUNT_ZEROED = 1
 MZ_STEP_AUTORESET = 2
+MZ_RNG_PHILOX, MZ_RNG_CPYTHON = 0, 1
 MZ_ERRORS = {-1: ValueError, -2: ValueError, -3: RuntimeError, -4: MemoryError, -5: ValueError}
 
 EXPORTS = ["mz_last_error", "mz_device_count", "mz_create", "mz_destroy", "mz_load_mazes",
-           "mz_generate", "mz_reset_all", "mz_reset_list", "mz_reset_done", "mz_step", "mz_step_ex", "mz_direction_mask",
+           "mz_generate", "mz_generate_ex", "mz_generate_state", "mz_reset_all", "mz_reset_list", "mz_reset_done", "mz_step", "mz_step_ex", "mz_direction_mask",
            "mz_act", "mz_step_act", "mz_expand_window", "mz_set_algorithm", "mz_query", "mz_get_grid",
            "mz_difficulty", "mz_get_meta", "mz_discounted_returns", "mz_q_front",
            "mz_bank_create", "mz_bank_fill", "mz_bank_use", "mz_bank_consumed"]
@@ -64,6 +65,9 @@ def load(build_if_missing=True):
     L.mz_destroy.argtypes = [vp]
     L.mz_load_mazes.argtypes = [vp, vp, C.c_int32, vp, vp, C.c_int32, vp]
     L.mz_generate.argtypes = [vp, vp, C.c_int32, vp, C.c_int32, C.c_int32, C.c_uint64, vp]
+    L.mz_generate_ex.argtypes = [vp, vp, C.c_int32, vp, C.c_int32, C.c_int32, C.c_uint64,
+                                 C.c_int32, vp]
+    L.mz_generate_state.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, vp, vp]
     L.mz_reset_all.argtypes = [vp, C.POINTER(StepOut), vp]
     L.mz_reset_list.argtypes = [vp, vp, vp, C.c_int32, C.c_int32, C.c_uint64, C.c_uint32,
                                 C.POINTER(StepOut), vp]

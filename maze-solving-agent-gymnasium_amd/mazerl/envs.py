@@ -10,12 +10,14 @@ VectorMazeEnv: generation, step, reset, masks and windows all run in libmazerl.s
   ToroidalMazeEnv / ToroidalEnrichMazeEnv             toroidal_maze_env.py:15-172
   ToroidalVariableMazeEnv / ToroidalEnrichVariableMazeEnv  toroidal_variable_maze_env.py:15-194
 
-Randomness: like the reference, mazes depend on Python's global `random` state —
-each new maze's Philox seed is random.getrandbits(64); `random.seed(s)` before construction makes
-an env reproducible. `reset(seed=...)` ignores the seed, as the reference does. The algorithm is
-the class-wide BaseMazeEnv.ALGORITHM (set_algorithm changes it for every env, base_maze_env.py:60).
-New mazes follow the reference's best-of-6 rule (base_maze_env.py:78-97): six GPU-generated
-candidates, the first with the smallest McClendon difficulty (native mz_difficulty) is kept.
+Randomness: like the reference, mazes are drawn from Python's global `random`
+state, and exactly as the reference draws them: the GPU generator runs gen_maze with CPython's
+MT19937 stream and set iteration order (mz_generate_state), consuming the global stream draw for
+draw, so `random.seed(s)` before construction gives the reference's own maze.
+`reset(seed=...)` ignores the seed, as the reference does. The algorithm is the class-wide
+BaseMazeEnv.ALGORITHM (set_algorithm changes it for every env, base_maze_env.py:60). New mazes
+follow the reference's best-of-6 rule (base_maze_env.py:78-97): six candidates from the global
+stream, the first with the smallest McClendon difficulty (native mz_difficulty) is kept.
 """
 import random
 
@@ -118,8 +120,8 @@ class BaseMazeEnv(_EnvBase):
         generated on the GPU, the first with the smallest McClendon difficulty is kept."""
         best = None
         for _ in range(max(1, self.CANDIDATES)):
-            seed = random.getrandbits(64)
-            self._venv.generate(algorithm=ALGOS[BaseMazeEnv.ALGORITHM], dim=n, seed=seed)
+            # gen_maze / gen_maze_no_border from Python's global random, bit-exact
+            self._venv.generate_from_random(0, ALGOS[BaseMazeEnv.ALGORITHM], dim=n)
             self._pull()
             if self.CANDIDATES <= 1:
                 return

@@ -85,8 +85,12 @@ class VectorMazeEnv:
             pass
 
     # ---------------------------------------------------------------------------------------
-    def generate(self, env_ids=None, algorithm="r-prim", dim=None, seed=None):
-        """New mazes for env_ids (None = all): gen_maze(shape, algorithm) per instance."""
+    def generate(self, env_ids=None, algorithm="r-prim", dim=None, seed=None, rng="philox"):
+        """New mazes for env_ids (None = all): gen_maze(shape, algorithm) per instance.
+        rng="philox": Philox stream seed + env_id (every random choice uniform over the same
+        candidates as the reference); rng="cpython": bit-exact — instance i gets the maze of
+        `random.seed(seed + i); gen_maze((dim, dim), algorithm)` (MT19937 + CPython set order
+        emulated on the GPU)."""
         dim = int(dim or self.maze_dim)
         seed = self.seed if seed is None else int(seed)
         ids = None if env_ids is None else torch.as_tensor(env_ids, dtype=torch.int32, device=self.device)
@@ -103,8 +107,27 @@ class VectorMazeEnv:
             if algo_t.numel() != n:
                 raise ValueError("per-instance algorithm ids must match the env list")
             self.algos_in_use.update(ALGOS.values())
-        N.check(self.lib.mz_generate(self._h, _ptr(ids), n, _ptr(algo_t), algo_all, dim,
-                                     seed & 0xFFFFFFFFFFFFFFFF, self._stream()))
+        mode = {"philox": N.MZ_RNG_PHILOX, "cpython": N.MZ_RNG_CPYTHON}[rng]
+        N.check(self.lib.mz_generate_ex(self._h, _ptr(ids), n, _ptr(algo_t), algo_all, dim,
+                                        seed & 0xFFFFFFFFFFFFFFFF, mode, self._stream()))
+        return self
+
+    def generate_from_random(self, env_id=0, algorithm="r-prim", dim=None, rnd=None):
+        """One maze for instance env_id drawn from a Python random.Random (default: the global
+        `random` module) exactly as the reference's gen_maze((dim, dim), algorithm) would draw
+        it (toroidal handles: gen_maze_no_border); the generator's state is advanced the same
+        way (getstate -> GPU -> setstate)."""
+        import random as _random
+        import numpy as np
+        rnd = _random if rnd is None else rnd
+        dim = int(dim or self.maze_dim)
+        algo = ALGOS[algorithm] if isinstance(algorithm, str) else int(algorithm)
+        self.algos_in_use.add(algo)
+        version, words, gauss = rnd.getstate()
+        st = np.array(words, dtype=np.uint32)
+        N.check(self.lib.mz_generate_state(self._h, int(env_id), dim, algo, st.ctypes.data,
+                                           self._stream()))
+        rnd.setstate((version, tuple(int(x) for x in st), gauss))
         return self
 
     def load_mazes(self, grids, start_goal, env_ids=None):

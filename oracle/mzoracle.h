@@ -42,6 +42,18 @@ int mzo_max_steps(const uint8_t* grid, int H, int W, int toroidal, int sr, int s
 int mzo_generate(uint8_t* grid, int H, int W, int toroidal, int algo, uint64_t seed,
                  int* sr, int* sc, int* gr, int* gc);
 
+/* CPython-exact generation (mzpygen.c): gen_maze((N,N), algo) (toroidal: gen_maze_no_border)
+ * exactly as CPython 3.10 runs it from the random.Random state `state` (624 MT19937 words +
+ * the index, as in random.getstate()[1]); the state is advanced in place. Returns 0. */
+int mzo_generate_py(uint8_t* grid, int N, int toroidal, int algo, uint32_t* state, int* sr,
+                    int* sc, int* gr, int* gc);
+/* random.seed(seed) state for 0 <= seed < 2^64 (init_by_array) -> state[625] */
+void mzo_mt_seed(uint64_t seed, uint32_t* state);
+/* random._randbelow(n) on state (advances it) */
+uint32_t mzo_mt_below(uint32_t* state, uint32_t n);
+/* hash((a, b)) of CPython 3.10 for small non-negative ints, as uint64 */
+uint64_t mzo_tuple_hash(int a, int b);
+
 /* Philox4x32-10 block for (key, counter) -> 4 words (for RNG stream tests). */
 void mzo_philox(uint64_t key, uint64_t ctr_hi, uint64_t ctr_lo, uint32_t out[4]);
 

@@ -40,8 +40,8 @@ _lib = None
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(
-                os.path.join(HERE, "mzoracle.c")):
+        if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(
+                os.path.getmtime(os.path.join(HERE, f)) for f in ("mzoracle.c", "mzpygen.c", "mzoracle.h")):
             build()
         L = C.CDLL(LIB)
         u8p, i32p = C.POINTER(C.c_uint8), C.POINTER(C.c_int32)
@@ -53,6 +53,13 @@ def lib():
         L.mzo_generate.argtypes = [u8p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64,
                                    ip, ip, ip, ip]
         L.mzo_philox.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint32)]
+        u32p = C.POINTER(C.c_uint32)
+        L.mzo_generate_py.argtypes = [u8p, C.c_int, C.c_int, C.c_int, u32p, ip, ip, ip, ip]
+        L.mzo_mt_seed.argtypes = [C.c_uint64, u32p]
+        L.mzo_mt_below.argtypes = [u32p, C.c_uint32]
+        L.mzo_mt_below.restype = C.c_uint32
+        L.mzo_tuple_hash.argtypes = [C.c_int, C.c_int]
+        L.mzo_tuple_hash.restype = C.c_uint64
         L.mzo_env_init.argtypes = [C.POINTER(_Env), u8p] + [C.c_int] * 9
         L.mzo_env_free.argtypes = [C.POINTER(_Env)]
         L.mzo_env_reset.argtypes = [C.POINTER(_Env), C.POINTER(Obs)]
@@ -109,6 +116,27 @@ def generate(n, algo, seed, toroidal=False):
                             int(algo), C.c_uint64(seed), *[C.byref(o) for o in out])
     if rc:
         raise ValueError(f"mzo_generate failed rc={rc}")
+    return (out[0].value, out[1].value), (out[2].value, out[3].value), g
+
+
+def mt_state(seed):
+    """random.seed(seed)'s MT19937 state as uint32[625] (624 words + index)."""
+    st = np.zeros(625, np.uint32)
+    lib().mzo_mt_seed(C.c_uint64(seed), st.ctypes.data_as(C.POINTER(C.c_uint32)))
+    return st
+
+
+def generate_py(n, algo, state, toroidal=False):
+    """gen_maze((n,n), algo) (toroidal: gen_maze_no_border) as CPython runs it from the
+    random state `state` (uint32[625], advanced in place; or an int seed)."""
+    if not isinstance(state, np.ndarray):
+        state = mt_state(int(state))
+    g = np.zeros((n, n), np.uint8)
+    out = [C.c_int() for _ in range(4)]
+    rc = lib().mzo_generate_py(g.ctypes.data_as(C.POINTER(C.c_uint8)), n, int(toroidal), int(algo),
+                               state.ctypes.data_as(C.POINTER(C.c_uint32)), *[C.byref(o) for o in out])
+    if rc:
+        raise ValueError(f"mzo_generate_py failed rc={rc}")
     return (out[0].value, out[1].value), (out[2].value, out[3].value), g
 
 

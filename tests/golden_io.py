@@ -44,3 +44,18 @@ def traces():
         t["enrich"] = t["kind"] in (KIND_ENRICH, KIND_TOR_ENRICH, KIND_VAR_ENRICH)
         out.append(t)
     return out
+
+
+def envs():
+    """envs.npz: reference env constructors after random.seed(s) (make_golden_envs.py)."""
+    z = load("envs.npz")
+    kinds = [str(k) for k in z["kinds"]]
+    out = []
+    for i in range(len(z["n"])):
+        n = int(z["n"][i])
+        out.append(dict(kind=kinds[int(z["kind"][i])], ctor=int(z["ctor"][i]), algo=int(z["algo"][i]),
+                        seed=int(z["seed"][i]), n=n, grid=z["grid"][i, :n, :n].copy(),
+                        start=tuple(int(x) for x in z["start"][i]),
+                        goal=tuple(int(x) for x in z["goal"][i]),
+                        max_steps=int(z["max_steps"][i]), probe=int(z["probe"][i])))
+    return out

@@ -133,25 +133,21 @@ def test_q_agent_on_dropin_env_matches_reference(envs):
 
 def test_best_of_6_generation(envs):
     """generate_maze keeps the first of 6 candidates with the smallest difficulty
-    (base_maze_env.py:78-97); the candidates' seeds come from the global `random` state."""
-    from mazerl import VectorMazeEnv
+    (base_maze_env.py:78-97); the candidates come from the global `random` stream exactly as
+    gen_maze draws them (checked against the oracle's CPython restatement)."""
+    import pyoracle as O
     from mazerl.difficulty import maze_difficulty
     envs.BaseMazeEnv.ALGORITHM = "r-prim"
     random.seed(77)
     env = envs.SimpleMazeEnv((21, 21))
-    random.seed(77)
-    seeds = [random.getrandbits(64) for _ in range(6)]
-    v = VectorMazeEnv(1, 21, enrich=False, generate=False)
+    st = O.mt_state(77)
     cands = []
-    for s in seeds:
-        v.generate(algorithm="r-prim", dim=21, seed=s)
-        q = v.query(0)
-        g = v.grid(0)
-        cands.append((maze_difficulty(g, (q["start_r"], q["start_c"]), (q["goal_r"], q["goal_c"])), g))
+    for _ in range(6):
+        s, g, grid = O.generate_py(21, 0, st)
+        cands.append((maze_difficulty(grid, s, g), grid))
     best = min(range(6), key=lambda i: (cands[i][0], i))
     assert np.array_equal(np.array(env.maze_map), cands[best][1])
     assert env.get_maze_difficulty() == cands[best][0]
-    v.close()
     env.close()
 
 
@@ -175,3 +171,31 @@ def test_variable_env_growth(envs):
     obs, _ = tv.reset()
     assert obs["window"].shape == (3, 15, 15)
     tv.close()
+
+
+ENV_CLASS = {"simple": "SimpleMazeEnv", "simple_enrich": "SimpleEnrichMazeEnv",
+             "toroidal": "ToroidalMazeEnv", "toroidal_enrich": "ToroidalEnrichMazeEnv",
+             "simple_variable": "SimpleVariableMazeEnv",
+             "toroidal_variable": "ToroidalVariableMazeEnv"}
+
+
+def test_dropin_constructor_matches_reference_after_seed(envs):
+    """random.seed(s); Env(shape) builds the reference's own maze (tests/golden/envs.npz: the
+    reference's constructors, best-of-6 from the global stream) and leaves Python's global
+    random stream exactly where the reference leaves it."""
+    ALG = ["r-prim", "dfs", "prim&kill"]
+    saved = envs.BaseMazeEnv.ALGORITHM
+    try:
+        for e in G.envs():
+            envs.BaseMazeEnv.ALGORITHM = ALG[e["algo"]]
+            random.seed(e["seed"])
+            env = getattr(envs, ENV_CLASS[e["kind"]])((e["ctor"], e["ctor"]))
+            probe = random.getrandbits(32)
+            key = (e["kind"], e["ctor"], e["algo"], e["seed"])
+            assert env.maze_map == e["grid"].astype(int).tolist(), key
+            assert env._start_pos == e["start"] and tuple(env._target_location) == e["goal"], key
+            assert env.max_steps_taken == e["max_steps"], key
+            assert probe == e["probe"], key
+            env.close()
+    finally:
+        envs.BaseMazeEnv.ALGORITHM = saved

@@ -268,3 +268,55 @@ def test_autoreset_step_vs_oracle(mazerl, tor, dim, B):
             was_done[i] = o["terminated"] or o["truncated"]
     assert resets > 0
     env.close()
+
+
+@pytest.mark.parametrize("name,tor", [("gen_euclid.npz", False), ("gen_toroid.npz", True)])
+def test_cpython_generation_matches_reference_mazes(mazerl, name, tor):
+    """rng="cpython": instance i gets the maze of random.seed(seed + i); gen_maze(...) — checked
+    against the reference's own 240 golden mazes (3 algorithms x 5 sizes x 8 seeds)."""
+    ms = G.mazes(name)
+    maxn = max(m["n"] for m in ms)
+    env = mazerl.VectorMazeEnv(len(ms), maxn, toroidal=tor, enrich=False, generate=False)
+    for i, m in enumerate(ms):
+        env.generate(env_ids=[i], algorithm=m["algo"], dim=m["n"],
+                     seed=(m["seed"] - i) & 0xFFFFFFFFFFFFFFFF, rng="cpython")
+    for i, m in enumerate(ms):
+        q = env.query(i)
+        key = (m["algo"], m["n"], m["seed"])
+        np.testing.assert_array_equal(env.grid(i), m["grid"], err_msg=str(key))
+        assert (q["start_r"], q["start_c"]) == m["start"] and (q["goal_r"], q["goal_c"]) == m["goal"], key
+        assert q["max_steps"] == m["max_steps"], key
+    env.close()
+
+
+@pytest.mark.parametrize("tor,dim,B", [(False, 81, 192), (True, 41, 96), (False, 127, 12)])
+def test_cpython_generation_bulk_vs_oracle(mazerl, tor, dim, B):
+    """One launch, B instances per algorithm at the headline size (and the largest pitch):
+    every maze == the oracle's CPython restatement from random.seed(seed + i)."""
+    import pyoracle as O
+    for algo in (0, 1, 2):
+        env = mazerl.VectorMazeEnv(B, dim, toroidal=tor, enrich=False, generate=False)
+        seed = 777 + 1000 * algo
+        env.generate(algorithm=algo, seed=seed, rng="cpython")
+        for i in range(B):
+            s, g, grid = O.generate_py(dim, algo, seed + i, tor)
+            q = env.query(i)
+            np.testing.assert_array_equal(env.grid(i), grid, err_msg=str((algo, i)))
+            assert (q["start_r"], q["start_c"]) == s and (q["goal_r"], q["goal_c"]) == g
+        env.close()
+
+
+def test_generate_from_random_advances_python_stream(mazerl):
+    """generate_from_random consumes a random.Random exactly like gen_maze would."""
+    import random
+    import pyoracle as O
+    env = mazerl.VectorMazeEnv(2, 41, enrich=False, generate=False)
+    for algo in (0, 1, 2):
+        r = random.Random(99 + algo)
+        st = O.mt_state(99 + algo)
+        for k in range(3):
+            env.generate_from_random(k % 2, algo, dim=41, rnd=r)
+            s, g, grid = O.generate_py(41, algo, st)
+            np.testing.assert_array_equal(env.grid(k % 2), grid)
+            assert list(st) == list(r.getstate()[1])
+    env.close()
