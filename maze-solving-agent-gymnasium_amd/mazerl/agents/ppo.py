@@ -19,7 +19,6 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 import torch.optim as optim
-from torch.utils.data import DataLoader, TensorDataset
 
 WINDOW = (15, 15)
 
@@ -95,11 +94,16 @@ def ppo_losses(logp_old, logp_new, advantages, entropy, returns, value_pred, ent
 
 def optimize_model(net, optimizer, states, actions, logp, advantages, returns, entropy_coef,
                    batch_size, ppo_steps, allreduce=None):
-    ds = TensorDataset(states[0], states[1], actions.detach(), logp.detach(), advantages, returns)
-    loader = DataLoader(ds, batch_size, shuffle=False)
+    """The reference iterates DataLoader(TensorDataset(...), batch_size, shuffle=False)
+    (ppo_agent.py:214-216): consecutive, unshuffled minibatches with a short last one. The
+    same minibatches are taken here as slices (a DataLoader over device tensors would gather
+    and collate them row by row)."""
+    cols = (states[0], states[1], actions.detach(), logp.detach(), advantages, returns)
+    n = cols[0].shape[0]
     last = None
     for _ in range(ppo_steps):
-        for pos, win, act, lp_old, adv, ret in loader:
+        for i in range(0, n, batch_size):
+            pos, win, act, lp_old, adv, ret = (c[i:i + batch_size] for c in cols)
             lp_new, value, ent = net.evaluate((pos, win), act)
             pl, vl = ppo_losses(lp_old, lp_new, adv, ent, ret, value, entropy_coef)
             total = pl + 0.5 * vl
