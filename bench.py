@@ -106,7 +106,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
+        # RCCL ("nccl") on the 8-GPU node; MZ_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs
+        dist.init_process_group(os.environ.get("MZ_DIST_BACKEND", "nccl"), init_method="env://")
+    local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
