@@ -75,6 +75,52 @@ def win_rate(a, dev):
             "note": "fresh GPU-generated mazes never seen in training (test(new=True) protocol)"}
 
 
+BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X bf16 MFMA, dense (MI355X_MICROARCH.md)
+
+
+def q_head(dev, n, iters=50):
+    """The acting Q-network forward of the DDQN learner on n instances (north_star: MFMA for the
+    dense Q-head GEMMs): fused conv stem from window bits (k_qfront, bf16 MFMA) + fc1 1574->1024,
+    fc2 1024->512, fc3 512->4 bf16 GEMMs (hipBLASLt). HIP events on the launch stream; FLOPs are
+    algorithmic (conv 388,800 / sample, fc1 K = 1,574)."""
+    import torch
+    import torch.nn.functional as F
+    from mazerl.agents.fused import FusedQ
+    from mazerl.agents.nets import QNet
+    torch.manual_seed(0)
+    net = QNet(variant="ddqn").to(dev)
+    fq = FusedQ(net, seed=1)
+    g = torch.Generator(device=dev).manual_seed(0)
+    bits = torch.randint(0, 2**31 - 1, (n, 22), generator=g, device=dev, dtype=torch.int32)
+    obs6 = torch.rand(n, 6, generator=g, device=dev)
+    st = torch.cuda.current_stream(dev)
+
+    def timed(fn):
+        for _ in range(5):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(iters):
+            fn()
+        e1.record(st)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / iters
+
+    with torch.no_grad():
+        t_all = timed(lambda: fq(obs6, bits))
+        feat = fq.stem(obs6, bits)
+        w0, b0 = fq.head._w[0]
+        t_fc1 = timed(lambda: F.linear(feat, w0, b0))
+    f_fc1 = 2.0 * n * 1574 * 1024
+    f_all = n * (388800 + 2.0 * (1574 * 1024 + 1024 * 512 + 512 * 4))
+    return {"instances": n, "forward_ms": t_all, "fc1_ms": t_fc1,
+            "fc1_tflops": f_fc1 / (t_fc1 * 1e-3) / 1e12,
+            "fc1_mfma_frac": f_fc1 / (t_fc1 * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS,
+            "forward_tflops": f_all / (t_all * 1e-3) / 1e12,
+            "forward_mfma_frac": f_all / (t_all * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS,
+            "dtype": "bf16 (f32 accumulate)", "peak_tflops": BF16_DENSE_PEAK_TFLOPS}
+
+
 def cpu_baseline(env, seconds):
     """Oracle (oracle/mzoracle.c, 'port' of the reference algorithm at its cost model: heap A*
     for every find_path) timed on this host's cores on one of the benchmark's own mazes."""
@@ -191,6 +237,7 @@ def main():
     if rank == 0:
         if world == 1 and a.train_steps > 0:
             out["win_rate"] = win_rate(a, dev)
+            out["q_head"] = q_head(dev, B)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

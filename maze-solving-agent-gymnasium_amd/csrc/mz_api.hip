@@ -468,6 +468,17 @@ int mz_bank_consumed(mz_handle* h, int32_t bank, int32_t* out3_dev, void* stream
   return MZ_OK;
 }
 
+int mz_maze_metrics(mz_handle* h, const int32_t* env_ids_dev, int32_t n, double* out_dev,
+                    void* stream) {
+  if (!h || !out_dev) return fail(MZ_EINVAL, "bad arguments");
+  if (h->d.toroidal) return fail(MZ_EINVAL, "maze metrics are defined for euclidean mazes");
+  if (!env_ids_dev) n = h->d.B;
+  if (n < 0 || n > h->d.B) return fail(MZ_EINVAL, "n out of range");
+  DeviceGuard g(h->cfg.device);
+  MZ_HIP(mz_launch_metrics(h->d, env_ids_dev, n, out_dev, static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
 int mz_set_algorithm(mz_handle* h, const uint8_t* algo_dev, int32_t algo_all, void* stream) {
   if (!h) return fail(MZ_EINVAL, "null handle");
   DeviceGuard g(h->cfg.device);

@@ -153,11 +153,10 @@ std::vector<std::vector<int>> components(const Graph& G, const std::unordered_se
   return out;
 }
 
-}  // namespace
-
-extern "C" int mz_difficulty(const uint8_t* g, int32_t H, int32_t W, int32_t sr, int32_t sc,
-                             int32_t gr, int32_t gc, double* out) {
-  if (!g || !out || H < 3 || W < 3) return MZ_EINVAL;
+// difficulty_of_maze (:319-329) and complexity_of_maze (:311-317) of one euclidean grid
+int mcclendon(const uint8_t* g, int32_t H, int32_t W, int32_t sr, int32_t sc, int32_t gr,
+              int32_t gc, double* difficulty, double* complexity) {
+  if (!g || H < 3 || W < 3) return MZ_EINVAL;
   auto open = [&](int r, int c) { return g[r * W + c] != 0; };
   auto nbrs = [&](int v) {
     const int r = v / W, c = v % W;
@@ -285,7 +284,7 @@ extern "C" int mz_difficulty(const uint8_t* g, int32_t H, int32_t W, int32_t sr,
     if (!p.count(v)) rm_b.insert(v);
   const std::unordered_set<int> h0_nodes(s_nodes.begin(), s_nodes.end());
   std::vector<char> taken(hallways.size() + 1, 0);
-  double prod = 1.0;
+  double prod = 1.0, sum = 0.0;  // p = 1 / s = 0, over branches 1..m then branch 0
   for (const auto& comp : components(G, rm_b)) {
     const std::unordered_set<int> bset(comp.begin(), comp.end());
     double cx = 0.0;
@@ -304,9 +303,32 @@ extern "C" int mz_difficulty(const uint8_t* g, int32_t H, int32_t W, int32_t sr,
       any = true;
     }
     prod *= (any ? cx : 0.0) + 1;  // p *= complexity_of_branch(h) + 1
+    sum += any ? cx : 0.0;         // s += complexity_of_branch(b)
   }
-  prod *= hallway_complexity(H0, d_sol, h0_nodes);  // branch 0 = [0], multiplied last
-  if (!(prod > 0.0)) return MZ_EINVAL;  // math.log domain error in the reference
-  *out = std::log(prod);
+  const double c0 = hallway_complexity(H0, d_sol, h0_nodes);  // branch 0 = [0], last
+  prod *= c0;
+  sum += c0;
+  if (difficulty) {
+    if (!(prod > 0.0)) return MZ_EINVAL;  // math.log domain error in the reference
+    *difficulty = std::log(prod);
+  }
+  if (complexity) {
+    if (!(sum > 0.0)) return MZ_EINVAL;
+    *complexity = std::log(sum);
+  }
   return MZ_OK;
+}
+
+}  // namespace
+
+extern "C" int mz_difficulty(const uint8_t* g, int32_t H, int32_t W, int32_t sr, int32_t sc,
+                             int32_t gr, int32_t gc, double* out) {
+  if (!out) return MZ_EINVAL;
+  return mcclendon(g, H, W, sr, sc, gr, gc, out, nullptr);
+}
+
+extern "C" int mz_maze_complexity(const uint8_t* g, int32_t H, int32_t W, int32_t sr, int32_t sc,
+                                  int32_t gr, int32_t gc, double* difficulty, double* complexity) {
+  if (!difficulty && !complexity) return MZ_EINVAL;
+  return mcclendon(g, H, W, sr, sc, gr, gc, difficulty, complexity);
 }

@@ -27,3 +27,6 @@ hipError_t mz_launch_qfront(const uint32_t* bits, const float* obs6, int n, cons
                             uint16_t* out, int ld, hipStream_t s);
 hipError_t mz_launch_bank_fill(const MzDev& bd, const int* head, int K, int algo, int dim,
                                uint64_t seed, uint32_t epoch, hipStream_t s);
+size_t mz_metrics_lds_bytes(int P);
+hipError_t mz_launch_metrics(const MzDev& d, const int32_t* env_ids, int32_t n, double* out,
+                             hipStream_t s);

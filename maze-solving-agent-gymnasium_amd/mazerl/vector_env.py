@@ -302,6 +302,15 @@ class VectorMazeEnv:
         N.check(self.lib.mz_get_meta(self._h, out.data_ptr(), self._stream()))
         return out
 
+    def maze_metrics(self, env_ids=None, out=None):
+        """MetricsCalculator L, DE, D, AC, FDE, BDE of each listed instance's maze (euclidean),
+        computed on the GPU: float64 [n, 6] device tensor (metrics_calculator.py)."""
+        ids = None if env_ids is None else torch.as_tensor(env_ids, dtype=torch.int32, device=self.device)
+        n = self.num_envs if ids is None else int(ids.numel())
+        out = out if out is not None else torch.empty(n, 6, dtype=torch.float64, device=self.device)
+        N.check(self.lib.mz_maze_metrics(self._h, _ptr(ids), n, out.data_ptr(), self._stream()))
+        return out
+
     # ---------------------------------------------------------------------------------------
     def query(self, i):
         info = N.EnvInfo()

@@ -54,6 +54,10 @@ uint32_t mzo_mt_below(uint32_t* state, uint32_t n);
 /* hash((a, b)) of CPython 3.10 for small non-negative ints, as uint64 */
 uint64_t mzo_tuple_hash(int a, int b);
 
+/* MetricsCalculator (metrics_calculator.py) on the solution path of a perfect euclidean maze:
+ * out[6] = L, DE, D, AC, FDE, BDE (mzmetrics.c). Returns 0, or -1 if the goal is unreachable. */
+int mzo_metrics(const uint8_t* grid, int H, int W, int sr, int sc, int gr, int gc, double* out);
+
 /* Philox4x32-10 block for (key, counter) -> 4 words (for RNG stream tests). */
 void mzo_philox(uint64_t key, uint64_t ctr_hi, uint64_t ctr_lo, uint32_t out[4]);
 

@@ -41,7 +41,7 @@ def lib():
     global _lib
     if _lib is None:
         if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(
-                os.path.getmtime(os.path.join(HERE, f)) for f in ("mzoracle.c", "mzpygen.c", "mzoracle.h")):
+                os.path.getmtime(os.path.join(HERE, f)) for f in ("mzoracle.c", "mzpygen.c", "mzmetrics.c", "mzoracle.h")):
             build()
         L = C.CDLL(LIB)
         u8p, i32p = C.POINTER(C.c_uint8), C.POINTER(C.c_int32)
@@ -60,6 +60,7 @@ def lib():
         L.mzo_mt_below.restype = C.c_uint32
         L.mzo_tuple_hash.argtypes = [C.c_int, C.c_int]
         L.mzo_tuple_hash.restype = C.c_uint64
+        L.mzo_metrics.argtypes = [u8p] + [C.c_int] * 6 + [C.POINTER(C.c_double)]
         L.mzo_env_init.argtypes = [C.POINTER(_Env), u8p] + [C.c_int] * 9
         L.mzo_env_free.argtypes = [C.POINTER(_Env)]
         L.mzo_env_reset.argtypes = [C.POINTER(_Env), C.POINTER(Obs)]
@@ -138,6 +139,17 @@ def generate_py(n, algo, state, toroidal=False):
     if rc:
         raise ValueError(f"mzo_generate_py failed rc={rc}")
     return (out[0].value, out[1].value), (out[2].value, out[3].value), g
+
+
+def metrics(grid, start, goal):
+    """MetricsCalculator L, DE, D, AC, FDE, BDE of the solution path (euclidean, perfect maze)."""
+    g, gp = _u8(grid)
+    H, W = g.shape
+    out = (C.c_double * 6)()
+    rc = lib().mzo_metrics(gp, H, W, int(start[0]), int(start[1]), int(goal[0]), int(goal[1]), out)
+    if rc:
+        raise ValueError("goal unreachable")
+    return list(out)
 
 
 def philox(key, ctr_hi, ctr_lo):
