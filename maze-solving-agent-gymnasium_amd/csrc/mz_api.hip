@@ -25,7 +25,7 @@ struct MzBankStore {  // two banks x the enabled algorithms x K slots (mz_bank_*
   uint32_t* meta0 = nullptr;   // [2][nA][K]
   uint32_t* meta1 = nullptr;
   int* heads = nullptr;        // [2][3] consumed slots per algorithm id
-  uint8_t* s_visits = nullptr; // scratch the build writes and nobody reads: [K][VP], [K] ...
+  // scratch the build writes and nobody reads: [K] ...
   uint32_t *s_posw = nullptr, *s_stw = nullptr, *s_curw = nullptr;
   uint8_t *s_last = nullptr, *s_algo = nullptr;
   uint32_t epoch[2] = {0u, 0u};
@@ -140,7 +140,6 @@ int mz_create(const mz_config* cfg, mz_handle** out) {
   MzDev& d = h->d;
   d.B = cfg->num_envs;
   d.P = cfg->max_dim;
-  d.VP = (d.P * d.P + 15) & ~15;
   d.toroidal = cfg->toroidal != 0;
   d.enrich = cfg->enrich != 0;
   d.NW = (d.P + 31) / 32;
@@ -148,7 +147,7 @@ int mz_create(const mz_config* cfg, mz_handle** out) {
   const size_t B = (size_t)d.B, P = (size_t)d.P;
   int rc;
   if ((rc = alloc(h, &d.cells, B * P * P)) || (rc = alloc(h, &d.planes, B * P * (size_t)d.PW + 16)) ||
-      (rc = alloc(h, &d.visits, B * (size_t)d.VP)) || (rc = alloc(h, &d.meta0, B)) ||
+      (rc = alloc(h, &d.meta0, B)) ||
       (rc = alloc(h, &d.meta1, B)) || (rc = alloc(h, &d.posw, B)) || (rc = alloc(h, &d.stw, B)) ||
       (rc = alloc(h, &d.curw, B)) || (rc = alloc(h, &d.algo, B)) || (rc = alloc(h, &d.last_term, B)) ||
       (rc = alloc(h, &d.ticket, 16))) {
@@ -392,7 +391,7 @@ int mz_bank_create(mz_handle* h, int32_t slots, int32_t dim, uint32_t algo_mask)
   const size_t S = 2 * (size_t)nA * slots, K = (size_t)slots;
   if ((rc = alloc(h, &b.cells, S * d.P * d.P)) || (rc = alloc(h, &b.planes, S * d.P * d.PW)) ||
       (rc = alloc(h, &b.meta0, S)) || (rc = alloc(h, &b.meta1, S)) || (rc = alloc(h, &b.heads, 6)) ||
-      (rc = alloc(h, &b.s_visits, K * d.VP)) || (rc = alloc(h, &b.s_posw, K)) ||
+      (rc = alloc(h, &b.s_posw, K)) ||
       (rc = alloc(h, &b.s_stw, K)) || (rc = alloc(h, &b.s_curw, K)) || (rc = alloc(h, &b.s_last, K)) ||
       (rc = alloc(h, &b.s_algo, K)))
     return rc;
@@ -422,7 +421,6 @@ int mz_bank_fill(mz_handle* h, int32_t bank, uint64_t seed, void* stream) {
     bd.planes = b.planes + blk * P * h->d.PW;
     bd.meta0 = b.meta0 + blk;
     bd.meta1 = b.meta1 + blk;
-    bd.visits = b.s_visits;
     bd.posw = b.s_posw;
     bd.stw = b.s_stw;
     bd.curw = b.s_curw;

@@ -400,8 +400,6 @@ __device__ void mz_build_one(const MzDev& d, int e, bool tor, bool generate, int
       row[k] = make_uint2(o, v);
     }
   }
-  uint4* v4 = reinterpret_cast<uint4*>(d.visits + es * d.VP);
-  for (int i = lane; i < d.VP / 16; i += 64) v4[i] = make_uint4(0u, 0u, 0u, 0u);
   if (lane == 0) {
     // set_max_steps: ceil((((H-1)*(W-1)) - 1) * (len / CE)), CE = (H-1)*((W-1)//2) - 1
     const int len = (int)L.dist[sr * N + sc] + 1;

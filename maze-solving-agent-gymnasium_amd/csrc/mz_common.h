@@ -1,40 +1,51 @@
 // mz_common.h — shared layout + device helpers for the MI355X maze env (libmazerl.so).
 //
 // HBM layout (one handle = B env instances, pitch P = max_dim, planes padded to 128 bits/row):
-//   cells  u32 [B][P*P]  per-cell word:  D (bits 0-15, BFS distance to goal)
-//                                         | best-next code (16-18: action 0-3, 4 = stay)
-//                                         | open (19) | open-neighbour mask (20-23, per action)
+//   cells  u32 [B][P*P]  per-cell word:  D (bits 0-12, BFS distance to goal, < 8192 for P <= 127)
+//                                         | best-next code (13-15: action 0-3, 4 = stay)
+//                                         | open (16) | open-neighbour mask (17-20, per action)
+//                                         | visit count (21-28) | episode tag (29-31)
 //                        Everything the reference recomputes with A* every step
 //                        (_find_best_next_cell base_maze_env.py:224-262, find_path
 //                        simple_maze_env.py:70-79) is a function of the cell: computed once per
-//                        maze, gathered once per step.
+//                        maze, gathered once per step. The visit count (visited_cell.count,
+//                        :194; saturating at 255, exact since the penalties are -1.0 for k >= 188)
+//                        rides in the same word, so one gather serves both; it counts only when
+//                        its tag equals the instance's episode tag (stw bits 24-26), so a reset
+//                        bumps the tag instead of clearing the maze (a full clear every 8th reset).
 //   planes u32 [B][P][PW] per row, interleaved (open, visited) word pairs for columns 32k..32k+31,
 //                        PW = 2 * ceil(P / 32) (24 B rows at P = 81): [o0 v0 o1 v1 o2 v2];
 //                        visited = the reference's non_visited plane inverted
 //                        (base_maze_env.py:40-41,184). A window row needs 2 x 8 B loads.
-//   visits u8  [B][VP]   entries into each cell since reset (visited_cell.count, :194),
-//                        saturating at 255 (exact: penalties are -1.0 for k >= 188)
 //   SoA per instance (coalesced u32 each):
 //     meta0 = N | N<<8 (H,W) | sr<<16 | sc<<24     meta1 = gr | gc<<8 | max_steps<<16
 //     posw  = r | c<<8 | nm<<16 (min(len(visited_cell),2)) | last_action<<18 | done<<20
-//     stw   = steps (0-15) | invalid streak (16-23, saturating)
+//     stw   = steps (0-15) | invalid streak (16-23, saturating) | episode tag (24-26)
 //     curw  = cells word at the current position
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#define MZ_CELL_D_MASK 0xFFFFu
-#define MZ_CELL_CODE_SHIFT 16
-#define MZ_CELL_OPEN (1u << 19)
-#define MZ_CELL_NB_SHIFT 20
+#define MZ_CELL_D_MASK 0x1FFFu
+#define MZ_CELL_CODE_SHIFT 13
+#define MZ_CELL_OPEN (1u << 16)
+#define MZ_CELL_NB_SHIFT 17
+#define MZ_CELL_CNT_SHIFT 21
+#define MZ_CELL_TAG_SHIFT 29
+#define MZ_CELL_STATIC ((1u << MZ_CELL_CNT_SHIFT) - 1u)
+#define MZ_STW_TAG_SHIFT 24
+
+// visit count of cell word w for the episode tagged `tag`
+__host__ __device__ inline int mz_cell_count(uint32_t w, uint32_t tag) {
+  return (w >> MZ_CELL_TAG_SHIFT) == tag ? (int)((w >> MZ_CELL_CNT_SHIFT) & 0xFFu) : 0;
+}
 #define MZ_TICKET_PYERR 8
 
 struct MzDev {
-  int B, P, VP, toroidal, enrich;
+  int B, P, toroidal, enrich;
   int NW, PW;               // plane words per row per plane (ceil(P/32)) and row pitch (2*NW)
   uint32_t* cells;
   uint32_t* planes;
-  uint8_t* visits;
   uint32_t* meta0;
   uint32_t* meta1;
   uint32_t* posw;

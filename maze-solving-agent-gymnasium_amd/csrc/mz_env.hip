@@ -300,6 +300,13 @@ __device__ inline void win_band(int r, int c, int tr, int tc, int N, int& geo, i
 // launch instead of stepping (BaseMazeEnv.reset, :136-161: same maze, agent at start, visits
 // cleared; the trainer's env.reset() after a finished episode) — its action is ignored
 // (actions_out = -1), reward 0, terminated = truncated = 0, obs = the reset observation.
+// Every 8th reset of an instance its episode tag wraps to 0: drop all visit counts of its maze
+// (wave-cooperative; keeps the static cell bits), so no stale count can alias a later tag.
+__device__ inline void clear_counts(const MzDev& d, size_t e) {
+  uint32_t* c = d.cells + e * d.P * d.P;
+  for (int k = threadIdx.x; k < d.P * d.P; k += WAVE) c[k] &= MZ_CELL_STATIC;
+}
+
 template <bool TOR, bool ENRICH, bool ACT, bool AR>
 __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ act, const MzAct& ap,
                                   const MzOut& o, int e0, uint32_t* cat, double* pen, bool load_pen) {
@@ -352,12 +359,10 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
   }
 
   // ---- level 2
+  const uint32_t tag = (sw >> MZ_STW_TAG_SHIFT) & 7u;  // the episode's visit-count tag
   uint32_t ncw = 0u;
-  int cnt = 0;
-  if (inb) {
-    ncw = d.cells[es * d.P * d.P + (size_t)tr * d.P + tc];
-    if (!rst) cnt = d.visits[es * d.VP + (size_t)tr * d.P + tc];
-  }
+  if (inb) ncw = d.cells[es * d.P * d.P + (size_t)tr * d.P + tc];  // cell word + visit count
+  const int cnt = rst ? 0 : mz_cell_count(ncw, tag);
   constexpr int RW = TOR ? 8 : 4;
   uint32_t wv[WIN_IT][RW];  // band row words
   int geo = 0, col = 0;
@@ -380,8 +385,10 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
   double rew = 0.0;
   bool term = false, trunc = false, done = false, sel = false;
   int vr = -1, vc = -1;
+  uint32_t ntag = tag;
   if (rst) {
     r = sr; c = sc; cw = ncw; nm = 0; la = 0; steps = 0; inv = 0;
+    ntag = (tag + 1u) & 7u;  // visited_cell = [] (base_maze_env.py:159): a new count tag
     sel = true; vr = sr; vc = sc;  // visited = {start} (base_maze_env.py:148-149)
   } else if (trans) {
     if (ncw & MZ_CELL_OPEN) {  // moved (ncw = 0 when out of bounds)
@@ -444,12 +451,14 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
   if (rst || trans) {
     d.posw[e] = (uint32_t)r | ((uint32_t)c << 8) | ((uint32_t)nm << 16) | ((uint32_t)la << 18) |
                 ((uint32_t)done << 20);
-    d.stw[e] = (uint32_t)steps | ((uint32_t)inv << 16);
+    d.stw[e] = (uint32_t)steps | ((uint32_t)inv << 16) | (ntag << MZ_STW_TAG_SHIFT);
     d.curw[e] = cw;
     d.last_term[e] = term;
     if (sel && !rst) {
       if (vr >= 0) atomicOr(&d.planes[(es * d.P + tr) * d.PW + 2 * (tc >> 5) + 1], 1u << (tc & 31));
-      d.visits[es * d.VP + (size_t)tr * d.P + tc] = (uint8_t)min(cnt + 1, 255);
+      d.cells[es * d.P * d.P + (size_t)tr * d.P + tc] =  // visited_cell.append (:196)
+          (ncw & MZ_CELL_STATIC) | ((uint32_t)min(cnt + 1, 255) << MZ_CELL_CNT_SHIFT) |
+          (tag << MZ_CELL_TAG_SHIFT);
     }
   }
   if (live) {
@@ -470,21 +479,20 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
     if (o.window) store_window_f32(cat, o.window + (size_t)e0 * 675, nb, lane);
   }
 
-  if (AR) {  // reset instances: visits[:] = 0, visited plane = {start} (wave-cooperative)
+  if (AR) {  // reset instances: visited plane = {start}; counts cleared when the tag wraps
     unsigned long long bal = __ballot(rst);
-    const int sp = sr | (sc << 8);
+    const int sp = sr | (sc << 8) | ((int)ntag << 16);
     while (bal) {
       const int j = __ffsll((long long)bal) - 1;
       bal &= bal - 1;
       const int q = __shfl(sp, j), srj = q & 0xFF, scj = (q >> 8) & 0xFF;
       const size_t ej = (size_t)(e0 + j);
-      uint4* v4 = reinterpret_cast<uint4*>(d.visits + ej * d.VP);
-      for (int k = lane; k < d.VP / 16; k += WAVE) v4[k] = make_uint4(0u, 0u, 0u, 0u);
       for (int k = lane; k < d.P * d.NW; k += WAVE) {
         const int R = k / d.NW, w = k - R * d.NW;
         d.planes[(ej * d.P + R) * d.PW + 2 * w + 1] =
             (R == srj && w == (scj >> 5)) ? (1u << (scj & 31)) : 0u;
       }
+      if (((q >> 16) & 7) == 0) clear_counts(d, ej);
     }
   }
 
@@ -521,21 +529,21 @@ __device__ void reset_one(const MzDev& d, int e, const MzOut& o, uint32_t* wsh) 
   const uint32_t m0 = d.meta0[e], m1 = d.meta1[e];
   const int N = m0 & 0xFF, sr = (m0 >> 16) & 0xFF, sc = m0 >> 24;
   const int gr = m1 & 0xFF, gc = (m1 >> 8) & 0xFF;
-  // visits[:] = 0 (visited_cell = [], base_maze_env.py:159)
-  uint4* v4 = reinterpret_cast<uint4*>(d.visits + es * d.VP);
-  for (int i = lane; i < d.VP / 16; i += WAVE) v4[i] = make_uint4(0, 0, 0, 0);
+  const uint32_t cw = d.cells[es * d.P * d.P + (size_t)sr * d.P + sc];
+  // visited_cell = [] (base_maze_env.py:159): a new visit-count tag (all counts cleared on wrap)
+  const uint32_t ntag = ((d.stw[e] >> MZ_STW_TAG_SHIFT) + 1u) & 7u;
+  if (ntag == 0u) clear_counts(d, es);
   // visited plane = {start} (non_visited = open & ~start, :148-149): odd words of each row
   for (int k = lane; k < d.P * d.NW; k += WAVE) {
     const int R = k / d.NW, w = k - R * d.NW;
     const uint32_t v = (R == sr && w == (sc >> 5)) ? (1u << (sc & 31)) : 0u;
     d.planes[(es * d.P + R) * d.PW + 2 * w + 1] = v;
   }
-  const uint32_t cw = d.cells[es * d.P * d.P + (size_t)sr * d.P + sc];
   if (lane == 0) {
     int br, bc;
     best_dir(sr, sc, cw, N, TOR, br, bc);
     d.posw[e] = (uint32_t)sr | ((uint32_t)sc << 8);
-    d.stw[e] = 0u;
+    d.stw[e] = ntag << MZ_STW_TAG_SHIFT;
     d.curw[e] = cw;
     d.last_term[e] = 0;
     if (o.reward) o.reward[e] = 0.f;

@@ -332,11 +332,9 @@ __device__ inline void mz_py_inters(const MzBuildLds& L, const MzPySet& un, int 
   const int n = mz_py_nbrs2(G, cur, nb);
   uint16_t st[8];
   mz_ps_small(st, G, nb, n);
-  int nbu = 0;  // len(set(nbrs)) = n (distinct keys)
-  nbu = n;
   MzPySet res{it, ih, 8, G, nullptr};
   mz_ps_init(res);
-  if (nbu > un.h[2]) {  // iterate unmarked (the smaller operand) in table order
+  if (n > un.h[2]) {  // len(set(nbrs)) = n > len(unmarked): iterate unmarked in table order
     for (int i = 0; i <= un.h[0]; ++i) {
       const uint16_t t = un.t[i];
       if (t >= MZ_PS_DUMMY) continue;
