@@ -100,6 +100,12 @@ struct MzOut {
 __host__ __device__ inline int mz_dr(int a) { return a == 0 ? 1 : (a == 1 ? -1 : 0); }
 __host__ __device__ inline int mz_dc(int a) { return a == 2 ? 1 : (a == 3 ? -1 : 0); }
 __host__ __device__ inline int mz_wrap(int v, int n) { v %= n; return v < 0 ? v + n : v; }
+// v mod n for v within a few multiples of n (window offsets, +-1 moves): no integer division
+__host__ __device__ inline int mz_wrapn(int v, int n) {
+  while (v < 0) v += n;
+  while (v >= n) v -= n;
+  return v;
+}
 
 // ------------------------------------------------------------------------------------------
 // Philox4x32-10 — identical definition in oracle/mzoracle.c (mzo_philox).

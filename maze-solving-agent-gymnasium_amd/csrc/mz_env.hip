@@ -44,17 +44,15 @@ __device__ inline uint32_t row15_wrap(const uint32_t w[4], int s, int N) {
     return (a & ((1u << k) - 1u)) | ((b << k) & 0x7FFFu);
   }
   uint32_t v = 0;
-  for (int j = 0; j < 15; ++j) {
-    int col = (s + j) % N;
+  for (int j = 0, col = s; j < 15; ++j, col = (col + 1 == N) ? 0 : col + 1)
     v |= ((w[col >> 5] >> (col & 31)) & 1u) << j;
-  }
   return v;
 }
 
 // bits j in [0,15) with (C0 + j) mod N == col
 __device__ inline uint32_t wrap_colmask(int col, int C0, int N) {
   uint32_t m = 0;
-  for (int j = mz_wrap(col - C0, N); j < 15; j += N) m |= 1u << j;
+  for (int j = mz_wrapn(col - C0, N); j < 15; j += N) m |= 1u << j;
   return m;
 }
 
@@ -79,7 +77,7 @@ __device__ inline void win_row(const MzDev& d, size_t e, bool tor, int N, int r,
     if (!vso && R == vr) vis15 |= 1u << (vc - c0);
     if (R == gr && gc >= c0 && gc < c0 + 15) gmask = 1u << (gc - c0);
   } else {
-    const int R = mz_wrap(r + i - 7, N), C0 = mz_wrap(c - 7, N);
+    const int R = mz_wrapn(r + i - 7, N), C0 = mz_wrapn(c - 7, N);
     const uint2* row2 = reinterpret_cast<const uint2*>(d.planes + (e * d.P + R) * d.PW);
     uint32_t ow[4] = {0u, 0u, 0u, 0u}, vw[4] = {0u, 0u, 0u, 0u};
     for (int k = 0; k < d.NW; ++k) {
@@ -118,7 +116,7 @@ __device__ inline void best_dir(int r, int c, uint32_t cw, int N, bool tor, int&
   int code = (cw >> MZ_CELL_CODE_SHIFT) & 7;
   if (code > 3) { br = 0; bc = 0; return; }
   int nr = r + mz_dr(code), nc = c + mz_dc(code);
-  if (tor) { nr = mz_wrap(nr, N); nc = mz_wrap(nc, N); }
+  if (tor) { nr = mz_wrapn(nr, N); nc = mz_wrapn(nc, N); }
   br = r - nr;
   bc = c - nc;
 }
@@ -268,14 +266,14 @@ __device__ inline void win_band(int r, int c, int tr, int tc, int N, int& geo, i
     C0B = mz_win_start(tc, N);
     W0 = min(C0A, C0B) >> 5;
   } else {
-    const int rA = mz_wrap(r - 7, N);
+    const int rA = mz_wrapn(r - 7, N);
     R0 = rA;
     if (tr != r) {
-      if (tr == mz_wrap(r + 1, N)) offB = 1;
-      else { R0 = mz_wrap(rA - 1, N); offA = 1; }
+      if (tr == mz_wrapn(r + 1, N)) offB = 1;
+      else { R0 = mz_wrapn(rA - 1, N); offA = 1; }
     }
-    C0A = mz_wrap(c - 7, N);
-    C0B = mz_wrap(tc - 7, N);
+    C0A = mz_wrapn(c - 7, N);
+    C0B = mz_wrapn(tc - 7, N);
   }
   geo = R0 | (W0 << 8) | (offA << 12) | (offB << 13) | ((offA | offB) << 14) | (N << 16);
   col = C0A | (C0B << 8);
@@ -301,10 +299,13 @@ __device__ inline void win_band(int r, int c, int tr, int tc, int N, int& geo, i
 // cleared; the trainer's env.reset() after a finished episode) — its action is ignored
 // (actions_out = -1), reward 0, terminated = truncated = 0, obs = the reset observation.
 // Every 8th reset of an instance its episode tag wraps to 0: drop all visit counts of its maze
-// (wave-cooperative; keeps the static cell bits), so no stale count can alias a later tag.
-__device__ inline void clear_counts(const MzDev& d, size_t e) {
+// (rows < N; keeps the static cell bits), so no stale count can alias a later tag. No-return
+// atomic ANDs: the wave issues them and moves on (a load-mask-store loop would wait a round trip
+// per pass, and the slowest wave sets the launch time).
+__device__ inline void clear_counts(const MzDev& d, size_t e, int N) {
   uint32_t* c = d.cells + e * d.P * d.P;
-  for (int k = threadIdx.x; k < d.P * d.P; k += WAVE) c[k] &= MZ_CELL_STATIC;
+  for (int k = threadIdx.x; k < N * d.P; k += WAVE)
+    (void)__hip_atomic_fetch_and(&c[k], MZ_CELL_STATIC, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <bool TOR, bool ENRICH, bool ACT, bool AR>
@@ -353,7 +354,7 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
   if (rst) { tr = sr; tc = sc; }
   else if (trans) {
     tr = r + mz_dr(a); tc = c + mz_dc(a);
-    if (TOR) { tr = mz_wrap(tr, N); tc = mz_wrap(tc, N); inb = true; }
+    if (TOR) { tr = mz_wrapn(tr, N); tc = mz_wrapn(tc, N); inb = true; }
     else inb = 0 < tr && tr < N - 1 && 0 < tc && tc < N - 1;  // maze_view.py:169 (Q3)
     if (!inb) { tr = r; tc = c; }
   }
@@ -374,7 +375,7 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
       const int g = __shfl(geo, j);
       if (j < nb && (k < 15 || ((g >> 14) & 1))) {
         const int n_ = (g >> 16) & 0xFF, R0 = g & 0xFF;
-        load_row<TOR>(d, (size_t)(e0 + j), TOR ? mz_wrap(R0 + k, n_) : R0 + k, (g >> 8) & 0xF,
+        load_row<TOR>(d, (size_t)(e0 + j), TOR ? mz_wrapn(R0 + k, n_) : R0 + k, (g >> 8) & 0xF,
                       wv[it]);
       }
     }
@@ -434,7 +435,7 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
       for (int k = 0; k < RW; ++k) w[k] = (uint32_t)__shfl((int)wv[it][k], (lane + off) & (WAVE - 1));
       if (j < nb && i < 15) {
         const int n_ = (g >> 16) & 0xFF, R0 = g & 0xFF;
-        const int R = TOR ? mz_wrap(R0 + i + off, n_) : R0 + i + off;
+        const int R = TOR ? mz_wrapn(R0 + i + off, n_) : R0 + i + off;
         const int C0 = useb ? ((cc >> 8) & 0xFF) : (cc & 0xFF);
         uint32_t c0, c1, c2;
         win_bits<TOR>(w, n_, R, C0, (g >> 8) & 0xF, gg & 0xFF, (gg >> 8) & 0xFF,
@@ -481,18 +482,19 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
 
   if (AR) {  // reset instances: visited plane = {start}; counts cleared when the tag wraps
     unsigned long long bal = __ballot(rst);
-    const int sp = sr | (sc << 8) | ((int)ntag << 16);
+    const int sp = sr | (sc << 8) | ((int)ntag << 16) | (N << 19);
     while (bal) {
       const int j = __ffsll((long long)bal) - 1;
       bal &= bal - 1;
       const int q = __shfl(sp, j), srj = q & 0xFF, scj = (q >> 8) & 0xFF;
       const size_t ej = (size_t)(e0 + j);
-      for (int k = lane; k < d.P * d.NW; k += WAVE) {
+      const int Nj = (q >> 19) & 0xFF;
+      for (int k = lane; k < Nj * d.NW; k += WAVE) {  // rows >= N hold no open cell
         const int R = k / d.NW, w = k - R * d.NW;
         d.planes[(ej * d.P + R) * d.PW + 2 * w + 1] =
             (R == srj && w == (scj >> 5)) ? (1u << (scj & 31)) : 0u;
       }
-      if (((q >> 16) & 7) == 0) clear_counts(d, ej);
+      if (((q >> 16) & 7) == 0) clear_counts(d, ej, (q >> 19) & 0xFF);
     }
   }
 
@@ -532,9 +534,9 @@ __device__ void reset_one(const MzDev& d, int e, const MzOut& o, uint32_t* wsh) 
   const uint32_t cw = d.cells[es * d.P * d.P + (size_t)sr * d.P + sc];
   // visited_cell = [] (base_maze_env.py:159): a new visit-count tag (all counts cleared on wrap)
   const uint32_t ntag = ((d.stw[e] >> MZ_STW_TAG_SHIFT) + 1u) & 7u;
-  if (ntag == 0u) clear_counts(d, es);
+  if (ntag == 0u) clear_counts(d, es, N);
   // visited plane = {start} (non_visited = open & ~start, :148-149): odd words of each row
-  for (int k = lane; k < d.P * d.NW; k += WAVE) {
+  for (int k = lane; k < N * d.NW; k += WAVE) {  // rows >= N hold no open cell
     const int R = k / d.NW, w = k - R * d.NW;
     const uint32_t v = (R == sr && w == (sc >> 5)) ? (1u << (sc & 31)) : 0u;
     d.planes[(es * d.P + R) * d.PW + 2 * w + 1] = v;

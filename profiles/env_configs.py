@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Env-only throughput (fused act + step + autoreset, one k_step launch per vector step, f32
+window) for each BASELINE.json config on one GPU (per-GPU share of the multi-GPU configs).
+Prints one JSON line per config."""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "maze-solving-agent-gymnasium_amd"))
+
+import torch  # noqa: E402
+
+from mazerl.trainers.vector_trainer import make_env  # noqa: E402
+
+CONFIGS = [
+    ("cfg2: 4096 x 15x15 r-prim euclidean", 4096, [15], False, "r-prim"),
+    ("cfg3: 65536 x 81x81 r-prim (headline)", 65536, [81], False, "r-prim"),
+    ("cfg4 per GPU: 8192 x 81x81 mixed algorithms", 8192, [81], False, "mixed"),
+    ("cfg5 per GPU: 4096 x toroidal 17..79 variable", 4096, list(range(17, 80, 2)), True, "r-prim"),
+    ("cfg5 whole: 32768 x toroidal 17..79 variable (1 GPU)", 32768, list(range(17, 80, 2)), True, "r-prim"),
+]
+
+
+def main(steps=500):
+    ar_modes = [True, False] if "--both" in sys.argv else [True]
+    for (name, B, dims, tor, algo), ar in [(c, m) for c in CONFIGS for m in ar_modes]:
+        algorithm = algo if algo != "mixed" else torch.arange(B) % 3
+        env = make_env(B, dims, toroidal=tor, algorithm=algorithm, seed=0x5EED0000, device="cuda:0",
+                       window=True, window_bits=False, pos=False, done_list=False)
+        for k in range(30):
+            env.step_act(eps=1.0, seed=3, counter=k, autoreset=ar)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            env.step_act(eps=1.0, seed=3, counter=100 + k, autoreset=ar)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        print(json.dumps({"config": name, "autoreset": ar, "envs": B, "us_per_vector_step": round(dt * 1e6, 2),
+                          "env_steps_per_s": B / dt}), flush=True)
+        env.close()
+
+
+if __name__ == "__main__":
+    main()
