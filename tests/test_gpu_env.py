@@ -354,3 +354,37 @@ def test_many_episodes_reset_done_vs_oracle(mazerl, tor, dim):
         env.reset_done()
     assert episodes.min() >= 9, episodes.min()  # every instance wrapped its tag at least once
     env.close()
+
+
+@pytest.mark.parametrize("tor,dim,B", [(False, 127, 64), (True, 127, 48), (True, 5, 64),
+                                       (False, 15, 1), (True, 15, 33)])
+def test_extreme_sizes_vs_oracle(mazerl, tor, dim, B):
+    """Largest pitch (127: three plane word pairs + a fourth, 13-bit D), the smallest toroidal
+    grid (5 < window: rows and columns wrap several times), N = 15 (window == maze; toroidal
+    15 is the reference's Q8 crash, generic wrapped window here), a single instance and a
+    batch that is not a multiple of 32: stepping with autoreset vs the oracle."""
+    import pyoracle as O
+    env = mazerl.VectorMazeEnv(B, dim, toroidal=tor, enrich=True, reward64=True, seed=31337,
+                               algorithm="dfs")
+    ors = []
+    for i in range(B):
+        q = env.query(i)
+        o = O.Env(env.grid(i), (q["start_r"], q["start_c"]), (q["goal_r"], q["goal_c"]), tor, True)
+        o.reset()
+        ors.append(o)
+        assert o.max_steps == q["max_steps"]
+    was_done = np.zeros(B, bool)
+    for k in range(150):
+        env.step_act(eps=1.0, seed=9, counter=k, autoreset=True)
+        a = env.actions.cpu().numpy()
+        r64 = env.reward64.cpu().numpy()
+        pos, bd = env.pos.cpu().numpy(), env.best_dir.cpu().numpy()
+        win = env.window.cpu().numpy()
+        te, trn = env.terminated.cpu().numpy(), env.truncated.cpu().numpy()
+        for i in range(B):
+            o = ors[i].reset() if was_done[i] else ors[i].step(int(a[i]))
+            assert r64[i] == o["reward"], (k, i)
+            assert tuple(pos[i]) == o["pos"] and tuple(bd[i]) == o["best_dir"], (k, i)
+            np.testing.assert_array_equal(win[i], o["window"].astype(np.float32))
+            was_done[i] = bool(te[i]) or bool(trn[i])
+    env.close()
