@@ -241,8 +241,8 @@ int mz_difficulty(const uint8_t* grid_host, int32_t h, int32_t w, int32_t sr, in
 int mz_maze_complexity(const uint8_t* grid_host, int32_t h, int32_t w, int32_t sr, int32_t sc,
                        int32_t gr, int32_t gc, double* difficulty_out, double* complexity_out);
 
-/* The reference's maze-metric suite (MetricsCalculator, metrics_calculator.py, as used by
- * generation_algos_metrics_evaluations.py) for the listed euclidean instances (NULL = all B),
+/* The reference's maze-metric suite (MetricsCalculator, metrics_calculator.py:11-133, as used by
+ * generation_algos_metrics_evaluations.py:33-45) for the listed euclidean instances (NULL = all B),
  * computed on the GPU from the instances' mazes: out_dev [n][6] float64 = L, DE, D, AC, FDE, BDE
  * of the solution path (calculate_L / calculate_DE / calculate_D / calculate_DE_sub). */
 int mz_maze_metrics(mz_handle* h, const int32_t* env_ids_dev, int32_t n, double* out_dev,
