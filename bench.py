@@ -136,7 +136,9 @@ def cpu_baseline(env, seconds):
     per_env = max(20, int(rate * seconds / threads))
     t, n = O.bench(grid, start, goal, False, True, True, threads, per_env, threads, seed=2)
     tf, nf = O.bench(grid, start, goal, False, True, False, threads, per_env * 20, threads, seed=3)
+    t1, n1 = O.bench(grid, start, goal, False, True, True, 1, max(20, per_env // 4), 1, seed=4)
     return {"value": n / t, "unit": "env steps/s", "cores": threads, "kind": "port",
+            "single_core": {"value": n1 / t1, "steps": n1, "seconds": round(t1, 2)},
             "sample": f"{threads} envs x {per_env} steps (81x81 r-prim Enrich, masked-exploration "
                       f"actions, auto-reset), oracle in reference-cost mode (heap A* per find_path); "
                       f"{t:.1f} s",
