@@ -25,15 +25,15 @@ def parse(argv=None):
     ap.add_argument("--algo", default="r-prim", help="r-prim | dfs | prim&kill | mixed")
     ap.add_argument("--variant", default="ddqn")
     ap.add_argument("--steps", type=int, default=400, help="vector steps")
-    ap.add_argument("--updates-per-step", type=int, default=4)
-    ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--updates-per-step", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=2048)
     ap.add_argument("--lr", type=float, default=1e-3)
     ap.add_argument("--gamma", type=float, default=0.7)
     ap.add_argument("--eps-start", type=float, default=0.95)
     ap.add_argument("--eps-final", type=float, default=0.1)
     ap.add_argument("--eps-decay", type=float, default=None, help="default ((N-1)^2//2)*5 / 40")
     ap.add_argument("--capacity", type=int, default=2_000_000)
-    ap.add_argument("--target-every", type=int, default=50)
+    ap.add_argument("--target-every", type=int, default=13)
     ap.add_argument("--eval-mazes", type=int, default=1000)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--log-every", type=int, default=50)
