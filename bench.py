@@ -53,30 +53,51 @@ def parse():
     return ap.parse_args()
 
 
-def win_rate(a, dev):
+def win_rate(a, dev, rank=0, world=1):
     """Second half of the metric: train DDQN (reference DDQN net/loss, vectorised) on the same
     config, then the win-rate on `eval_mazes` fresh mazes, greedy and with the reference's
-    epsilon (0.1) protocol (off_policy_trainer.py:228-263)."""
+    epsilon (0.1) protocol (off_policy_trainer.py:228-263). With N ranks every rank
+    trains on its own env shard and the source-net gradients are averaged over RCCL once per
+    update (mazerl/distributed.py: one 8.56 MB bucket); rank 0 evaluates."""
     import torch
+    import torch.distributed as dist
     from mazerl import VectorMazeEnv
     from mazerl.agents.dqn import VectorDQNLearner
+    from mazerl.distributed import GradAllReduce, broadcast_params
     from mazerl.trainers.vector_trainer import VectorOffPolicyTrainer, evaluate
-    env = VectorMazeEnv(a.envs, a.dim, enrich=True, device=dev, algorithm=a.algo, seed=0xA11CE,
-                        done_list=False, window=False, window_bits=True)  # acting reads the bits
+    env = VectorMazeEnv(a.envs, a.dim, enrich=True, device=dev, algorithm=a.algo,
+                        seed=0xA11CE + rank * a.envs, done_list=False, window=False,
+                        window_bits=True)  # acting reads the bits
     decay = ((a.dim - 1) * (a.dim - 1) // 2) * 5 / 40.0
     L = VectorDQNLearner(a.envs, dev, variant="ddqn", lr=1e-3, eps_start=0.95, eps_final=0.1,
                          eps_decay=decay, gamma=0.7, batch_size=a.batch, capacity=2_000_000,
-                         updates_per_step=a.updates_per_step, target_every=a.target_every)
-    tr = VectorOffPolicyTrainer(env, L, seed=3)
+                         updates_per_step=a.updates_per_step, target_every=a.target_every,
+                         allreduce=GradAllReduce() if world > 1 else None)
+    if world > 1:
+        broadcast_params(L.source)
+        L.target.load_state_dict(L.source.state_dict())
+    tr = VectorOffPolicyTrainer(env, L, seed=3 + 7919 * rank)
     tr.train(20)  # warm-up: MIOpen / hipBLASLt first calls
+    if world > 1:
+        dist.barrier()
     secs = tr.train(a.train_steps)
+    if world > 1:
+        t = torch.tensor([secs], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        secs = float(t.item())
+    env.close()
+    if rank != 0:
+        return None
     g, _ = evaluate(L, a.eval_mazes, a.dim, a.algo, seed=0x7E570000, eps=0.0, device=dev)
     e, _ = evaluate(L, a.eval_mazes, a.dim, a.algo, seed=0x7E570000, eps=0.1, device=dev)
-    env.close()
     return {"greedy": g, "eps_0.1": e, "eval_mazes": a.eval_mazes, "variant": "ddqn",
-            "train_vector_steps": a.train_steps + 20, "train_seconds_steady": round(secs, 3),
-            "train_env_steps_per_s": a.envs * a.train_steps / secs,
+            "ranks": world, "train_vector_steps": a.train_steps + 20,
+            "train_seconds_steady": round(secs, 3),
+            "train_env_steps_per_s": a.envs * a.train_steps * world / secs,
             "updates": L.n_updates, "batch": a.batch, "updates_per_vector_step": a.updates_per_step,
+            "grad_allreduce": (f"{dist.get_backend()} ({'RCCL' if dist.get_backend() == 'nccl' else 'rehearsal'}), "
+                               "one 8.56 MB fp32 bucket per update between two graph replays")
+                              if world > 1 else None,
             "note": "fresh GPU-generated mazes never seen in training (test(new=True) protocol)"}
 
 
@@ -241,10 +262,12 @@ def main():
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(env, a.cpu_seconds)
     env.close()
-    if rank == 0:
-        if world == 1 and a.train_steps > 0:
-            out["win_rate"] = win_rate(a, dev)
+    if a.train_steps > 0:
+        wr = win_rate(a, dev, rank, world)  # every rank trains its shard (grad all-reduce)
+        if rank == 0:
+            out["win_rate"] = wr
             out["q_head"] = q_head(dev, B)
+    if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -40,15 +40,23 @@ def q_loss(source, target, state, action, reward, next_state, gamma, double):
     return F.mse_loss(q_sa, expected.unsqueeze(1))
 
 
-def learner_update(net, optimizer, loss, clamp=1.0, allreduce=None):
+def learner_backward(optimizer, loss):
     optimizer.zero_grad()
     loss.backward()
-    if allreduce is not None:
-        allreduce(net)  # average grads over ranks, then clamp (single-GPU semantics)
+
+
+def learner_step(net, optimizer, clamp=1.0):
     grads = [p.grad for p in net.parameters() if p.grad is not None]
     torch._foreach_clamp_min_(grads, -clamp)  # == p.grad.data.clamp_(-1, 1) per parameter
     torch._foreach_clamp_max_(grads, clamp)   # (dqn_agent.py:155-156), two launches in total
     optimizer.step()
+
+
+def learner_update(net, optimizer, loss, clamp=1.0, allreduce=None):
+    learner_backward(optimizer, loss)
+    if allreduce is not None:
+        allreduce(net)  # average grads over ranks, then clamp (single-GPU semantics)
+    learner_step(net, optimizer, clamp)
 
 
 class _AgentBase:
@@ -160,9 +168,11 @@ class VectorDQNLearner:
         self.target = QNet(3, 6, 4, h_channels, hidden_dim, variant).to(self.device)
         self.target.load_state_dict(self.source.state_dict())
         # One update (sample -> expand -> loss -> backward -> clamp -> AdamW) is ~150 small
-        # kernels: on one GPU it is captured once into a HIP graph and replayed (capturable
-        # AdamW with a device-side lr, so the cosine schedule still applies).
-        self.use_graph = bool(use_graph) and self.device.type == "cuda" and allreduce is None
+        # kernels: it is captured once into a HIP graph and replayed (capturable AdamW with a
+        # device-side lr, so the cosine schedule still applies). With a gradient all-reduce
+        # (N ranks) it is two graphs, backward + pack and unpack + clamp + AdamW, with the one
+        # RCCL all-reduce of the flat bucket launched between the replays.
+        self.use_graph = bool(use_graph) and self.device.type == "cuda"
         if self.use_graph:
             self.opt = optim.AdamW(self.source.parameters(),
                                    torch.tensor(float(lr), device=self.device), capturable=True,
@@ -233,6 +243,7 @@ class VectorDQNLearner:
         return loss.detach()
 
     def _graph_update(self, expand, warmup=3):
+        ar = self.allreduce
         if self._graph is None:
             if self._eager_updates < warmup:  # real updates on a side stream before capture
                 s = torch.cuda.Stream(self.device)
@@ -243,11 +254,28 @@ class VectorDQNLearner:
                 self._eager_updates += 1
                 return
             self.opt.zero_grad(set_to_none=True)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._graph_loss = self._one_update(expand, static=True)
-            self._graph = g
-        self._graph.replay()
+            if ar is None:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._graph_loss = self._one_update(expand, static=True)
+                self._graph = (g,)
+            else:
+                ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(ga):
+                    state, a, r, nxt = self.replay.sample(self.batch_size, expand, static=True)
+                    loss = q_loss(self.source, self.target, state, a, r, nxt, self.gamma,
+                                  self.variant == "ddqn")
+                    learner_backward(self.opt, loss)
+                    ar.pack(self.source)
+                    self._graph_loss = loss.detach()
+                with torch.cuda.graph(gb, pool=ga.pool()):
+                    ar.unpack(self.source)
+                    learner_step(self.source, self.opt)
+                self._graph = (ga, gb)
+        self._graph[0].replay()
+        if ar is not None:
+            ar.reduce()
+            self._graph[1].replay()
         self.last_loss = self._graph_loss
         if self.fused is not None:
             self.fused.invalidate()  # graph replays leave the params' _version untouched

@@ -27,14 +27,18 @@ def init_from_env(backend=None):
 
 
 class GradAllReduce:
-    """Callable(net): average the net's gradients over the process group in one flat bucket."""
+    """Callable(net): average the net's gradients over the process group in one flat bucket.
+
+    The three phases are also exposed separately so a HIP-graph-captured learner can replay
+    "backward + pack" and "unpack + clamp + AdamW" as two graphs with the collective between
+    them (agents/dqn.py): pack / unpack are plain device copies, reduce is the one all-reduce."""
 
     def __init__(self, group=None):
         self.group = group
         self.world = dist.get_world_size(group)
         self._flat = None
 
-    def __call__(self, net):
+    def pack(self, net):
         grads = [p.grad for p in net.parameters()]
         n = sum(g.numel() for g in grads)
         if self._flat is None or self._flat.numel() != n or self._flat.device != grads[0].device:
@@ -43,12 +47,21 @@ class GradAllReduce:
         for g in grads:
             self._flat[off:off + g.numel()].copy_(g.reshape(-1))
             off += g.numel()
+
+    def reduce(self):
         dist.all_reduce(self._flat, op=dist.ReduceOp.SUM, group=self.group)
-        self._flat.div_(self.world)
+
+    def unpack(self, net):
         off = 0
-        for g in grads:
-            g.copy_(self._flat[off:off + g.numel()].view_as(g))
+        for p in net.parameters():
+            g = p.grad
+            torch.div(self._flat[off:off + g.numel()].view_as(g), self.world, out=g)
             off += g.numel()
+
+    def __call__(self, net):
+        self.pack(net)
+        self.reduce()
+        self.unpack(net)
 
 
 def broadcast_params(net, src=0, group=None):

@@ -1,0 +1,79 @@
+"""The multi-GPU learner path on the GPU: two ranks (gloo, both on cuda:0 — the 8-GPU node runs
+the same code over RCCL) with different replay data. The HIP-graph-captured update (backward +
+pack graph, the all-reduce of the flat gradient bucket, unpack + clamp + AdamW graph) must track
+the eager all-reduce update (learner_update, dqn_agent.py:121-157 with the gradient average of
+SURVEY §8e) update for update, and both ranks must hold bit-identical weights afterwards.
+Tolerances as in test_learner_graph.py (capturable vs eager AdamW arithmetic)."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0")
+    import torch.distributed as dist
+    from mazerl import VectorMazeEnv
+    from mazerl.agents.dqn import VectorDQNLearner
+    from mazerl.distributed import GradAllReduce, broadcast_params, init_from_env
+    from test_learner_graph import _fill
+    init_from_env("gloo")
+    torch.cuda.set_device(0)
+    env = VectorMazeEnv(4, 21, enrich=True, device="cuda", seed=1)
+    mk = lambda g: VectorDQNLearner(4, "cuda", variant="ddqn", batch_size=32, capacity=64,  # noqa: E731
+                                    updates_per_step=1, target_every=4, updates_per_epoch=2,
+                                    seed=5 + rank, use_graph=g, allreduce=GradAllReduce())
+    A, B = mk(True), mk(False)
+    assert A.use_graph and not B.use_graph
+    broadcast_params(A.source)  # rank 1 started from other weights (seed 5 + rank)
+    A.target.load_state_dict(A.source.state_dict())
+    B.source.load_state_dict(A.source.state_dict())
+    B.target.load_state_dict(A.source.state_dict())
+    _fill(A, seed=10 + rank)  # different data per rank: the average matters
+    _fill(B, seed=10 + rank)
+    # Dropout(0.2) in train mode (Q13) would draw different masks in the two paths
+    A.source.eval(); A.target.eval(); B.source.eval(); B.target.eval()
+    losses = []
+    for _ in range(9):
+        la = A.update(env.expand_window)
+        lb = B.update(env.expand_window)
+        torch.cuda.synchronize()
+        losses.append((float(la), float(lb)))
+    assert A._graph is not None and len(A._graph) == 2
+    torch.save({"losses": losses,
+                "A": [p.detach().cpu() for p in A.source.parameters()],
+                "B": [p.detach().cpu() for p in B.source.parameters()]},
+               os.path.join(outdir, f"r{rank}.pt"))
+    env.close()
+    dist.destroy_process_group()
+
+
+def test_graph_allreduce_update_tracks_eager_two_ranks():
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        r = [torch.load(os.path.join(d, f"r{k}.pt"), weights_only=True) for k in range(2)]
+    for k in range(2):
+        for la, lb in r[k]["losses"]:
+            assert la == pytest.approx(lb, rel=1e-4, abs=1e-7)
+        for pa, pb in zip(r[k]["A"], r[k]["B"]):
+            assert torch.allclose(pa, pb, rtol=1e-5, atol=1e-5)
+    for pa0, pa1 in zip(r[0]["A"], r[1]["A"]):  # the average keeps the replicas identical
+        assert torch.equal(pa0, pa1)
+    for pb0, pb1 in zip(r[0]["B"], r[1]["B"]):
+        assert torch.equal(pb0, pb1)
+    # and the ranks' data differed: rank 0's and rank 1's first losses are not the same
+    assert r[0]["losses"][0][0] != r[1]["losses"][0][0]
