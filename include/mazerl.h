@@ -213,6 +213,26 @@ int mz_q_front(const uint32_t* bits_dev, const float* obs6_dev, int32_t n, const
                const float* conv_b_dev, float drop_p, uint64_t seed, uint64_t counter,
                uint16_t* feat_dev, int32_t ld, void* stream);
 
+/* The same conv stem in f32 for the LEARNER update (optimize_model, dqn_agent.py:121-157,
+ * ddqn_agent.py:113-152; forward dqn_agent.py:47-57), forward and backward, from packed windows:
+ * feat_dev [n][ld] f32 = [MaxPool2(Dropout(LeakyReLU(Conv3x3(window) + b))) in torch's flatten
+ * order (c*49 + q) | obs6], ld >= 1574, i.e. the f32 input of fc.0. drop_p = 0 (DQN) or the
+ * Dropout p (DDQN); the mask key is read from rng_dev (a device u64 the caller advances between
+ * calls, so a captured HIP graph draws fresh masks on every replay) mixed with `salt`.
+ * code_dev [n][1568] u8 (NULL when no backward follows): per feature the pooled argmax (bits
+ * 0-1) and its gradient class (bits 2-3: 0 dropped, 1 kept with a > 0, 2 kept with a <= 0). */
+int mz_stem_forward(const uint32_t* bits_dev, const float* obs6_dev, int32_t n,
+                    const float* conv_w_dev, const float* conv_b_dev, float drop_p,
+                    const uint64_t* rng_dev, uint32_t salt, float* feat_dev, int32_t ld,
+                    uint8_t* code_dev, void* stream);
+/* Conv weight / bias gradients from the gradient of the stem output gfeat_dev [n][ld] f32 (its
+ * first 1,568 columns) and the forward's code bytes: dw_dev [32][3][3][3], db_dev [32] f32
+ * (overwritten). partial_dev: workspace of mz_stem_workspace_floats(n) floats. */
+int mz_stem_backward(const uint32_t* bits_dev, const uint8_t* code_dev, const float* gfeat_dev,
+                     int32_t ld, int32_t n, float drop_p, float* partial_dev, float* dw_dev,
+                     float* db_dev, void* stream);
+int mz_stem_workspace_floats(int32_t n);
+
 /* Set the per-instance algorithm ids used by regeneration (BaseMazeEnv.ALGORITHM is global in
  * the reference, base_maze_env.py:17,60-64; here it is per instance). algo_dev [B] or NULL. */
 int mz_set_algorithm(mz_handle* h, const uint8_t* algo_dev, int32_t algo_all, void* stream);

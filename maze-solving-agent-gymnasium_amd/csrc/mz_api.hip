@@ -377,6 +377,34 @@ int mz_q_front(const uint32_t* bits_dev, const float* obs6_dev, int32_t n, const
   return MZ_OK;
 }
 
+int mz_stem_forward(const uint32_t* bits_dev, const float* obs6_dev, int32_t n,
+                    const float* conv_w_dev, const float* conv_b_dev, float drop_p,
+                    const uint64_t* rng_dev, uint32_t salt, float* feat_dev, int32_t ld,
+                    uint8_t* code_dev, void* stream) {
+  if (!bits_dev || !obs6_dev || !conv_w_dev || !conv_b_dev || !feat_dev || n < 0)
+    return fail(MZ_EINVAL, "bad arguments");
+  if (ld < 1574) return fail(MZ_EINVAL, "feature stride %d", ld);
+  if (!(drop_p >= 0.0f && drop_p < 1.0f)) return fail(MZ_EINVAL, "dropout p %g", (double)drop_p);
+  if (drop_p > 0.0f && !rng_dev) return fail(MZ_EINVAL, "dropout needs the device rng counter");
+  MZ_HIP(mz_launch_stem_fwd(bits_dev, obs6_dev, n, conv_w_dev, conv_b_dev, drop_p, rng_dev, salt,
+                            feat_dev, ld, code_dev, static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
+int mz_stem_backward(const uint32_t* bits_dev, const uint8_t* code_dev, const float* gfeat_dev,
+                     int32_t ld, int32_t n, float drop_p, float* partial_dev, float* dw_dev,
+                     float* db_dev, void* stream) {
+  if (!bits_dev || !code_dev || !gfeat_dev || !partial_dev || !dw_dev || !db_dev || n < 0)
+    return fail(MZ_EINVAL, "bad arguments");
+  if (ld < 1568) return fail(MZ_EINVAL, "gradient stride %d", ld);
+  if (!(drop_p >= 0.0f && drop_p < 1.0f)) return fail(MZ_EINVAL, "dropout p %g", (double)drop_p);
+  MZ_HIP(mz_launch_stem_bwd(bits_dev, code_dev, gfeat_dev, ld, n, drop_p, partial_dev, dw_dev,
+                            db_dev, static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
+int mz_stem_workspace_floats(int32_t n) { return n > 0 ? mz_stem_chunks(n) * 32 * 28 : 0; }
+
 int mz_bank_create(mz_handle* h, int32_t slots, int32_t dim, uint32_t algo_mask) {
   if (!h) return fail(MZ_EINVAL, "null handle");
   if (h->bank.K) return fail(MZ_EINVAL, "the handle already has a maze bank");

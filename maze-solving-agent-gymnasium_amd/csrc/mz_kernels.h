@@ -30,3 +30,10 @@ hipError_t mz_launch_bank_fill(const MzDev& bd, const int* head, int K, int algo
 size_t mz_metrics_lds_bytes(int P);
 hipError_t mz_launch_metrics(const MzDev& d, const int32_t* env_ids, int32_t n, double* out,
                              hipStream_t s);
+int mz_stem_chunks(int n);
+hipError_t mz_launch_stem_fwd(const uint32_t* bits, const float* obs6, int n, const float* w,
+                              const float* b, float drop_p, const uint64_t* rng, uint32_t salt,
+                              float* feat, int ld, uint8_t* code, hipStream_t s);
+hipError_t mz_launch_stem_bwd(const uint32_t* bits, const uint8_t* code, const float* g, int ld,
+                              int n, float drop_p, float* partial, float* dw, float* db,
+                              hipStream_t s);

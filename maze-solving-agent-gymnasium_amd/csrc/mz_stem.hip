@@ -1,0 +1,245 @@
+// mz_stem.hip — the Q-network's conv stem for the LEARNER update, f32, forward and backward,
+// straight from the replay's packed window bits.
+//
+// The reference's optimize_model (dqn_agent.py:121-157, ddqn_agent.py:113-152) runs the stem
+// Conv2d(3->32, 3x3, pad 1) -> LeakyReLU -> [Dropout(0.2): DDQN, always in train mode, SURVEY
+// Q13] -> MaxPool2d(2) -> flatten || obs6 (dqn_agent.py:47-57, ddqn_agent.py:18-52) in f32 on
+// [B, 3, 15, 15] windows. Through PyTorch that is an f32 expansion of the window, MIOpen conv
+// (+ NCHW<->NHWC transposes), separate activation / dropout / pooling passes over the 59 MB
+// [2048, 32, 15, 15] conv output, and their backward passes: ~0.8 ms of a 1.65 ms update at
+// batch 2,048. Here:
+//
+//   k_stem_fwd     one workgroup per 2 samples: the 22 window words -> padded 17-bit rows in LDS;
+//                  one thread per (sample, channel, pooled position) computes the 4 conv outputs
+//                  of its 2x2 pool window (the window is binary: a sum of the weights under set
+//                  bits, in weight order, + bias), LeakyReLU (x > 0 ? x : x * 0.01f), dropout
+//                  (x * keep * scale, keep from a counter hash), and the max in torch's scan
+//                  order (first strict maximum wins), writing the f32 fc1 input row
+//                  [feature c*49 + q (torch's flatten order) | obs6] and, when the caller needs
+//                  the backward, one code byte per feature: the argmax position (2 bits) and its
+//                  gradient class (0 dropped, 1 kept and a > 0, 2 kept and a <= 0);
+//   k_stem_bwd     grid (sample chunk of 64, channel): the conv-output gradient at the argmax
+//                  position, g * scale (dropout) then * 0.01f when a <= 0 (LeakyReLU backward),
+//                  exactly torch's elementwise chain, accumulated into the 27 weight + 1 bias
+//                  gradients of the channel over the chunk (the input is data: no input grad);
+//                  wave shuffles + LDS reduce to one partial per (chunk, channel);
+//   k_stem_reduce  the partials summed over chunks in a fixed order (deterministic).
+//
+// f32 throughout (the reference's precision); the conv / weight-gradient sums associate
+// differently from MIOpen's, so results agree with the torch stem within f32 rounding.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mz_kernels.h"
+
+namespace {
+
+constexpr int FEAT = 1568;   // 32 channels x 7 x 7 pooled positions
+constexpr int NPOOL = 49;
+constexpr int NOBS = 6;
+constexpr int WW = 22;       // window words per sample (675 bits)
+constexpr int PR = 17;       // padded rows per channel (rows 0 and 16 zero)
+constexpr int SPB = 2;       // samples per forward workgroup
+constexpr int CHUNK = 64;    // samples per backward workgroup
+constexpr int NACC = 28;     // 27 weights + bias per channel
+
+__device__ inline uint32_t hash32(uint32_t x) {  // lowbias32 (Wellons)
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
+// window bits of nsamp samples -> padded rows: rows[s][ch][pr] holds grid row pr - 1 of channel
+// ch with column c at bit c + 1 (bits 0 and 16 zero: the conv's zero padding)
+__device__ inline void load_rows(const uint32_t* __restrict__ bits, int n, int n0, int nsamp,
+                                 uint32_t (*wb)[WW], uint32_t (*rows)[3][PR]) {
+  const int tid = threadIdx.x;
+  for (int i = tid; i < nsamp * WW; i += blockDim.x) {
+    const int s = i / WW, k = i - s * WW;
+    wb[s][k] = n0 + s < n ? bits[(size_t)(n0 + s) * WW + k] : 0u;
+  }
+  __syncthreads();
+  for (int i = tid; i < nsamp * 3 * PR; i += blockDim.x) {
+    const int s = i / (3 * PR), rr = i - s * 3 * PR, ch = rr / PR, pr = rr - ch * PR;
+    uint32_t v = 0u;
+    if (pr >= 1 && pr <= 15) {
+      const int f0 = ch * 225 + (pr - 1) * 15, j = f0 >> 5;
+      const uint64_t w2 = ((uint64_t)(j + 1 < WW ? wb[s][j + 1] : 0u) << 32) | wb[s][j];
+      v = ((uint32_t)(w2 >> (f0 & 31)) & 0x7FFFu) << 1;
+    }
+    rows[s][ch][pr] = v;
+  }
+  __syncthreads();
+}
+
+template <bool DROP>
+__global__ __launch_bounds__(256) void k_stem_fwd(const uint32_t* __restrict__ bits,
+                                                  const float* __restrict__ obs6, int n,
+                                                  const float* __restrict__ w,
+                                                  const float* __restrict__ b, uint32_t thresh,
+                                                  float scale, const uint64_t* __restrict__ rng,
+                                                  uint32_t salt, float* __restrict__ feat, int ld,
+                                                  uint8_t* __restrict__ code) {
+  __shared__ float ws[32 * 27];
+  __shared__ float bs[32];
+  __shared__ uint32_t wb[SPB][WW];
+  __shared__ uint32_t rows[SPB][3][PR];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 32 * 27; i += blockDim.x) ws[i] = w[i];
+  if (tid < 32) bs[tid] = b[tid];
+  const int n0 = blockIdx.x * SPB;
+  load_rows(bits, n, n0, SPB, wb, rows);
+  uint32_t k0 = 0u, k1 = 0u;
+  if (DROP) {
+    const uint64_t key = *rng;  // device-side counter: a fresh mask per (graph-replayed) call
+    k0 = (uint32_t)key ^ (salt * 0x9E3779B9u);
+    k1 = (uint32_t)(key >> 32) + hash32(salt);
+  }
+  for (int i = tid; i < SPB * FEAT; i += blockDim.x) {
+    const int s = i / FEAT, j = i - s * FEAT, nn = n0 + s;
+    if (nn >= n) break;
+    const int c = j / NPOOL, q = j - c * NPOOL, py = q / 7, px = q - py * 7;
+    uint32_t h0 = 0u, h1 = 0u;
+    if (DROP) {
+      const uint32_t gid = 2u * ((uint32_t)nn * FEAT + j);
+      h0 = hash32(hash32(gid ^ k0) + k1);
+      h1 = hash32(hash32((gid + 1u) ^ k0) + k1);
+    }
+    const float* wc = ws + c * 27;
+    float m = -__builtin_inff();
+    int idx = 0, cls = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int y = 2 * py + (r >> 1), x = 2 * px + (r & 1);
+      float acc = 0.0f;
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch)
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          const uint32_t b3 = (rows[s][ch][y + ky] >> x) & 7u;  // columns x-1 .. x+1
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx)
+            if ((b3 >> kx) & 1u) acc += wc[ch * 9 + ky * 3 + kx];
+        }
+      const float a = acc + bs[c];
+      const float lk = a > 0.0f ? a : a * 0.01f;  // nn.LeakyReLU(negative_slope=0.01)
+      bool kept = true;
+      float v = lk;
+      if (DROP) {
+        const uint32_t u = ((r < 2 ? h0 : h1) >> (16 * (r & 1))) & 0xFFFFu;
+        kept = u >= thresh;
+        v = (lk * (kept ? 1.0f : 0.0f)) * scale;  // torch: src * mask * scale
+      }
+      if (v > m) {  // MaxPool2d: first strict maximum in (0,0) (0,1) (1,0) (1,1) order
+        m = v;
+        idx = r;
+        cls = kept ? (a > 0.0f ? 1 : 2) : 0;
+      }
+    }
+    feat[(size_t)nn * ld + j] = m;
+    if (code) code[(size_t)nn * FEAT + j] = (uint8_t)(idx | (cls << 2));
+  }
+  for (int i = tid; i < SPB * NOBS; i += blockDim.x) {  // || obs6 (torch.cat((fw, s), 1))
+    const int s = i / NOBS, k = i - s * NOBS, nn = n0 + s;
+    if (nn < n) feat[(size_t)nn * ld + FEAT + k] = obs6[(size_t)nn * NOBS + k];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_stem_bwd(const uint32_t* __restrict__ bits,
+                                                  const uint8_t* __restrict__ code,
+                                                  const float* __restrict__ g, int ld, int n,
+                                                  float scale, float* __restrict__ partial) {
+  __shared__ uint32_t wb[CHUNK][WW];
+  __shared__ uint32_t rows[CHUNK][3][PR];
+  __shared__ float red[4][NACC];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int chunk = blockIdx.x, c = blockIdx.y, n0 = chunk * CHUNK;
+  load_rows(bits, n, n0, CHUNK, wb, rows);
+  float acc[NACC];
+#pragma unroll
+  for (int k = 0; k < NACC; ++k) acc[k] = 0.0f;
+  for (int i = tid; i < CHUNK * NPOOL; i += blockDim.x) {
+    const int s = i / NPOOL, q = i - s * NPOOL, nn = n0 + s;
+    if (nn >= n) break;
+    const int j = c * NPOOL + q;
+    const uint32_t cd = code[(size_t)nn * FEAT + j];
+    const uint32_t cls = cd >> 2;
+    if (cls == 0u) continue;  // dropped: dropout backward gives 0
+    const float gs = g[(size_t)nn * ld + j] * scale;  // dropout backward: grad * mask * scale
+    const float gc = cls == 1u ? gs : gs * 0.01f;     // LeakyReLU backward
+    const int py = q / 7, px = q - py * 7;
+    const int y = 2 * py + (int)((cd >> 1) & 1u), x = 2 * px + (int)(cd & 1u);
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch)
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        const uint32_t b3 = (rows[s][ch][y + ky] >> x) & 7u;
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx)
+          if ((b3 >> kx) & 1u) acc[ch * 9 + ky * 3 + kx] += gc;
+      }
+    acc[27] += gc;
+  }
+#pragma unroll
+  for (int k = 0; k < NACC; ++k) {
+    float v = acc[k];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    if (lane == 0) red[wv][k] = v;
+  }
+  __syncthreads();
+  if (tid < NACC)
+    partial[((size_t)chunk * 32 + c) * NACC + tid] =
+        ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+}
+
+__global__ void k_stem_reduce(const float* __restrict__ partial, int chunks, float* __restrict__ dw,
+                              float* __restrict__ db) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 32 * NACC) return;
+  const int c = t / NACC, k = t - c * NACC;
+  float s = 0.0f;
+  for (int ch = 0; ch < chunks; ++ch) s += partial[((size_t)ch * 32 + c) * NACC + k];
+  if (k < 27) dw[c * 27 + k] = s;  // torch layout [32][3][3][3]: c*27 + ch*9 + ky*3 + kx
+  else db[c] = s;
+}
+
+}  // namespace
+
+int mz_stem_chunks(int n) { return (n + CHUNK - 1) / CHUNK; }
+
+hipError_t mz_launch_stem_fwd(const uint32_t* bits, const float* obs6, int n, const float* w,
+                              const float* b, float drop_p, const uint64_t* rng, uint32_t salt,
+                              float* feat, int ld, uint8_t* code, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  // keep iff a 16-bit uniform >= thresh: P(drop) = thresh / 65536 (0.2 -> 13107)
+  const uint32_t thresh = drop_p > 0.0f ? (uint32_t)(drop_p * 65536.0f + 0.5f) : 0u;
+  const float scale = drop_p > 0.0f ? (float)(1.0 / (1.0 - (double)drop_p)) : 1.0f;
+  const dim3 grid((n + SPB - 1) / SPB);
+  if (thresh)
+    hipLaunchKernelGGL(k_stem_fwd<true>, grid, dim3(256), 0, s, bits, obs6, n, w, b, thresh, scale,
+                       rng, salt, feat, ld, code);
+  else
+    hipLaunchKernelGGL(k_stem_fwd<false>, grid, dim3(256), 0, s, bits, obs6, n, w, b, 0u, 1.0f,
+                       rng, salt, feat, ld, code);
+  return hipGetLastError();
+}
+
+hipError_t mz_launch_stem_bwd(const uint32_t* bits, const uint8_t* code, const float* g, int ld,
+                              int n, float drop_p, float* partial, float* dw, float* db,
+                              hipStream_t s) {
+  const int chunks = mz_stem_chunks(n);
+  if (chunks == 0) {
+    const hipError_t e = hipMemsetAsync(dw, 0, 32 * 27 * sizeof(float), s);
+    return e != hipSuccess ? e : hipMemsetAsync(db, 0, 32 * sizeof(float), s);
+  }
+  const float scale = drop_p > 0.0f ? (float)(1.0 / (1.0 - (double)drop_p)) : 1.0f;
+  hipLaunchKernelGGL(k_stem_bwd, dim3(chunks, 32), dim3(256), 0, s, bits, code, g, ld, n, scale,
+                     partial);
+  hipLaunchKernelGGL(k_stem_reduce, dim3((32 * NACC + 255) / 256), dim3(256), 0, s, partial,
+                     chunks, dw, db);
+  return hipGetLastError();
+}

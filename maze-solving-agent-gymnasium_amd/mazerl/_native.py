@@ -38,7 +38,8 @@ EXPORTS = ["mz_last_error", "mz_device_count", "mz_create", "mz_destroy", "mz_lo
            "mz_generate", "mz_generate_ex", "mz_generate_state", "mz_reset_all", "mz_reset_list", "mz_reset_done", "mz_step", "mz_step_ex", "mz_direction_mask",
            "mz_act", "mz_step_act", "mz_expand_window", "mz_set_algorithm", "mz_query", "mz_get_grid",
            "mz_difficulty", "mz_maze_complexity", "mz_maze_metrics", "mz_get_meta", "mz_discounted_returns", "mz_q_front",
-           "mz_bank_create", "mz_bank_fill", "mz_bank_use", "mz_bank_consumed"]
+           "mz_bank_create", "mz_bank_fill", "mz_bank_use", "mz_bank_consumed",
+           "mz_stem_forward", "mz_stem_backward", "mz_stem_workspace_floats"]
 
 _lib = None
 
@@ -94,6 +95,10 @@ def load(build_if_missing=True):
     L.mz_bank_consumed.argtypes = [vp, C.c_int32, vp, vp]
     L.mz_q_front.argtypes = [vp, vp, C.c_int32, vp, vp, C.c_float, C.c_uint64, C.c_uint64, vp,
                              C.c_int32, vp]
+    L.mz_stem_forward.argtypes = [vp, vp, C.c_int32, vp, vp, C.c_float, vp, C.c_uint32, vp,
+                                  C.c_int32, vp, vp]
+    L.mz_stem_backward.argtypes = [vp, vp, vp, C.c_int32, C.c_int32, C.c_float, vp, vp, vp, vp]
+    L.mz_stem_workspace_floats.argtypes = [C.c_int32]
     for f in EXPORTS:
         if f != "mz_last_error":
             getattr(L, f).restype = C.c_int

@@ -29,13 +29,15 @@ from .nets import QNet
 
 
 def q_loss(source, target, state, action, reward, next_state, gamma, double):
-    """Loss of optimize_model for a batch: state = (obs6 [B,6], window [B,3,15,15])."""
+    """Loss of optimize_model for a batch: state = (obs6 [B,6], window [B,3,15,15] f32 or packed
+    int32 [B,22] on the GPU — QNet then runs the HIP stem)."""
     q_sa = source(state).gather(1, action.view(-1, 1))
-    if double:
-        best = source(next_state).max(1)[1].unsqueeze(1)
-        v_next = target(next_state).gather(1, best).squeeze(1).detach()
-    else:
-        v_next = target(next_state).max(1)[0].detach()
+    with torch.no_grad():  # the reference detaches V(s'); no graph is built for it here
+        if double:
+            best = source(next_state).max(1)[1].unsqueeze(1)
+            v_next = target(next_state).gather(1, best).squeeze(1).detach()
+        else:
+            v_next = target(next_state).max(1)[0].detach()
     expected = (v_next * gamma) + reward
     return F.mse_loss(q_sa, expected.unsqueeze(1))
 
@@ -160,7 +162,7 @@ class VectorDQNLearner:
                  eps_decay=8000.0, gamma=0.7, batch_size=128, capacity=1_000_000,
                  updates_per_step=1, target_every=100, hidden_dim=1024, h_channels=32,
                  act_bf16=True, t_max=150, updates_per_epoch=100, allreduce=None, seed=0,
-                 use_graph=True):
+                 use_graph=True, bit_stem=True):
         self.device = torch.device(device)
         torch.manual_seed(seed)
         self.variant = variant
@@ -173,6 +175,9 @@ class VectorDQNLearner:
         # (N ranks) it is two graphs, backward + pack and unpack + clamp + AdamW, with the one
         # RCCL all-reduce of the flat bucket launched between the replays.
         self.use_graph = bool(use_graph) and self.device.type == "cuda"
+        # the update's nets read the replay's packed windows through the HIP f32 stem
+        # (agents/stem.py) instead of expanding them to f32 for MIOpen
+        self.bit_stem = bool(bit_stem) and self.device.type == "cuda"
         if self.use_graph:
             self.opt = optim.AdamW(self.source.parameters(),
                                    torch.tensor(float(lr), device=self.device), capturable=True,
@@ -237,7 +242,8 @@ class VectorDQNLearner:
         return self.last_loss
 
     def _one_update(self, expand, static):
-        state, a, r, nxt = self.replay.sample(self.batch_size, expand, static=static)
+        state, a, r, nxt = self.replay.sample(self.batch_size, None if self.bit_stem else expand,
+                                              static=static)
         loss = q_loss(self.source, self.target, state, a, r, nxt, self.gamma, self.variant == "ddqn")
         learner_update(self.source, self.opt, loss, allreduce=self.allreduce)
         return loss.detach()
@@ -262,7 +268,8 @@ class VectorDQNLearner:
             else:
                 ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
                 with torch.cuda.graph(ga):
-                    state, a, r, nxt = self.replay.sample(self.batch_size, expand, static=True)
+                    state, a, r, nxt = self.replay.sample(
+                        self.batch_size, None if self.bit_stem else expand, static=True)
                     loss = q_loss(self.source, self.target, state, a, r, nxt, self.gamma,
                                   self.variant == "ddqn")
                     learner_backward(self.opt, loss)

@@ -6,6 +6,8 @@
 `QNet(variant="ddqn")` == agents/ddqn_agent.py:18-52: adds Dropout(0.2) after the conv
                           activation and uses ReLU in the second hidden layer; no Xavier init.
 Module names (conv.0, fc.0, fc.2, fc.4) match the reference so state_dicts interchange.
+Given packed windows (int32 [n, 22], the replay's storage) on the GPU, forward() runs the stem as
+one HIP kernel (agents/stem.py, csrc/mz_stem.hip) with its own backward.
 With window 15x15, h=32: 1568 conv features + 6 obs -> 1574 -> 1024 -> 512 -> 4
 (2,140,548 parameters, 4,665,024 FLOP per sample forward).
 
@@ -20,9 +22,14 @@ WINDOW = (15, 15)
 
 
 class QNet(nn.Module):
+    _count = 0  # construction order: the dropout-mask salt of the packed-window stem
+
     def __init__(self, in_channels=3, n_observations=6, n_actions=4, h_channels=32,
                  hidden_dim=1024, variant="dqn"):
         super().__init__()
+        QNet._count += 1
+        self._salt = QNet._count
+        self._stem_rng = None
         self.in_channels = in_channels
         self.variant = variant
         conv = [nn.Conv2d(in_channels, h_channels, kernel_size=3, stride=1, padding=1), nn.LeakyReLU()]
@@ -46,9 +53,23 @@ class QNet(nn.Module):
 
     def forward(self, x):
         s, w = x
+        if w.dtype == torch.int32 and w.dim() == 2:  # packed windows: the HIP f32 stem
+            return self.fc(self._bit_stem(s, w))
         fw = self.conv(w)
         fw = fw.view(fw.shape[0], -1)
         return self.fc(torch.cat((fw, s), dim=1))
+
+
+    def _bit_stem(self, s, bits):
+        from .stem import stem_features
+        p = 0.0
+        if self.training:
+            for m in self.conv:
+                if isinstance(m, nn.Dropout):
+                    p = float(m.p)
+        if p > 0 and (self._stem_rng is None or self._stem_rng.device != bits.device):
+            self._stem_rng = torch.zeros(1, dtype=torch.int64, device=bits.device)
+        return stem_features(bits, s, self.conv[0], p, self._stem_rng, self._salt)
 
 
 def count_params(net):

@@ -94,8 +94,12 @@ class DeviceReplay:
         return (u * self.size_dev).to(torch.int64).clamp_(max=self.capacity - 1)
 
     def sample(self, batch, expand, static=False):
-        """Returns ((s6, window), a, r, (s6', window')) with f32 windows from `expand(bits)`."""
+        """Returns ((s6, window), a, r, (s6', window')) with f32 windows from `expand(bits)`, or
+        the packed int32 windows themselves when expand is None (QNet's HIP stem reads them)."""
         i = self.sample_indices_static(batch) if static else self.sample_indices(batch)
+        if expand is None:
+            return ((self.s6.index_select(0, i), self.sw.index_select(0, i)), self.a.index_select(0, i),
+                    self.r.index_select(0, i), (self.s6n.index_select(0, i), self.swn.index_select(0, i)))
         bits = torch.cat((self.sw.index_select(0, i), self.swn.index_select(0, i)), 0)
         w = expand(bits)
         return ((self.s6.index_select(0, i), w[:batch]), self.a.index_select(0, i),
