@@ -15,6 +15,8 @@ VectorDQNLearner    the MI355X learner for VectorMazeEnv: device replay (HBM), b
                     act, K updates per vector step, optional DDP gradient all-reduce (RCCL) with
                     the clamp applied after averaging (single-GPU semantics).
 """
+import collections
+import copy
 import math
 import random
 
@@ -162,7 +164,7 @@ class VectorDQNLearner:
                  eps_decay=8000.0, gamma=0.7, batch_size=128, capacity=1_000_000,
                  updates_per_step=1, target_every=100, hidden_dim=1024, h_channels=32,
                  act_bf16=True, t_max=150, updates_per_epoch=100, allreduce=None, seed=0,
-                 use_graph=True, bit_stem=True):
+                 use_graph=True, bit_stem=True, overlap=False):
         self.device = torch.device(device)
         torch.manual_seed(seed)
         self.variant = variant
@@ -203,6 +205,21 @@ class VectorDQNLearner:
         if self.device.type == "cuda" and act_bf16:
             from .fused import FusedQ
             self.fused = FusedQ(self.source, seed=seed)
+        # env -> learner handoff on a side HIP stream (north_star): the updates of vector step t
+        # run on `side` while the main stream acts and steps the env for t + 1 (see update()).
+        self.overlap = bool(overlap) and self.use_graph and self.fused is not None
+        self._async = False
+        if self.overlap:
+            from .fused import FusedQ
+            self.side = torch.cuda.Stream(self.device)
+            # two actor snapshots of the source net (ping-pong) with their own fused heads and
+            # dropout streams; the source net itself is only touched on `side`
+            self.actors = [copy.deepcopy(self.source) for _ in range(2)]
+            self.actor_fused = [FusedQ(a, seed=seed * 2 + 101 + k) for k, a in enumerate(self.actors)]
+            self._published = collections.deque()  # (slot, event) of issued snapshots, oldest first
+            self._acting = None  # slot greedy() reads
+            self._idx = None     # [2][K, batch] sample indices, written on the main stream
+            self._par = 0
 
     @property
     def supports_bits(self):
@@ -216,6 +233,8 @@ class VectorDQNLearner:
         """argmax_a Q_source(s) for every instance. With packed window bits on the GPU the acting
         forward is the fused HIP stem + bf16 GEMMs (agents/fused.py); otherwise torch."""
         if bits is not None and self.fused is not None:
+            if self._async:
+                return self.actor_fused[self._acting_slot()](obs6, bits).float().argmax(1)
             return self.fused(obs6, bits).float().argmax(1)
         if window is None:
             raise ValueError("greedy() needs the f32 window or window bits on the GPU")
@@ -226,9 +245,14 @@ class VectorDQNLearner:
             q = self.source((obs6, window))
         return q.float().argmax(1)
 
-    def update(self, expand):
+    def update(self, expand, reserve=0):
+        """K updates (graph replays). With overlap, once the graphs exist, they are issued on the
+        side stream and this returns at once; `reserve` = rows the next push will write (the
+        vector step's instance count), kept out of the sampled range meanwhile."""
         if len(self.replay) < self.batch_size:
             return None
+        if self.overlap and self._graph is not None:
+            return self._update_async(reserve)
         for _ in range(self.updates_per_step):
             if self.use_graph:
                 self._graph_update(expand)
@@ -241,12 +265,105 @@ class VectorDQNLearner:
                 self.sched.step()
         return self.last_loss
 
+    # ---- overlapped learner (side stream) --------------------------------------------------
+    # Vector step t on the main stream M: greedy(t) -> env step -> push(t) -> update(): the K
+    # updates u_t go to the side stream S (after push(t)), followed by a snapshot of the source
+    # net into actor slot t % 2 and an event D_t. greedy(t + 1) waits for D_{t-1} only and acts
+    # with slot (t - 1) % 2: the acting weights lag the sequential schedule by one update, and
+    # M never waits for the update it just issued. Races excluded by construction:
+    #   * slot (t+1) % 2 is next written by u_{t+1}, which S starts after push(t+1), i.e. after
+    #     greedy(t+1) finished reading it;
+    #   * u_t samples the newest min(size, C - reserve) replay rows, indices drawn on M into
+    #     buffer t % 2 (M waited D_{t-2}, the last reader of that buffer, in greedy(t)), so the
+    #     rows push(t+1) overwrites concurrently are never read;
+    #   * the source / target nets, the optimizer and the LR tensor are touched on S only.
+    def _acting_slot(self):
+        M = torch.cuda.current_stream(self.device)
+        # keep the newest issued snapshot for the next step (unless nothing else is readable)
+        while len(self._published) > 1 or (self._acting is None and self._published):
+            slot, ev = self._published.popleft()
+            M.wait_event(ev)
+            self._acting = slot
+            self.actor_fused[slot].invalidate()
+        return self._acting
+
+    def _start_async(self):
+        M = torch.cuda.current_stream(self.device)
+        with torch.no_grad():
+            for a, f in zip(self.actors, self.actor_fused):
+                torch._foreach_copy_(list(a.parameters()), list(self.source.parameters()))
+                f.invalidate()
+        K, b = self.updates_per_step, self.batch_size
+        self._idx = [torch.zeros(K, b, dtype=torch.int64, device=self.device) for _ in range(2)]
+        self._idx_ev = [None, None]
+        self._acting, self._par = 0, 1  # the first update writes the slot greedy() does not read
+        self._published.clear()
+        self.side.wait_stream(M)
+        self._async = True
+
+    def _update_async(self, reserve):
+        if not self._async:
+            self._start_async()
+        M, S = torch.cuda.current_stream(self.device), self.side
+        rp, K, slot = self.replay, self.updates_per_step, self._par
+        n_avail = min(rp.size, rp.capacity - int(reserve))
+        if n_avail < self.batch_size:
+            raise ValueError("replay too small to exclude the next push from sampling")
+        if self._idx_ev[slot] is not None:
+            M.wait_event(self._idx_ev[slot])  # the last update that read this index buffer
+        idx = self._idx[slot]
+        u = torch.rand(idx.shape, dtype=torch.float64, device=self.device)
+        torch.sub(rp.ptr - 1, (u * n_avail).to(torch.int64), out=idx)
+        idx.remainder_(rp.capacity)  # the newest n_avail rows, ending at ptr - 1
+        if self._acting == slot:  # greedy() must switch to a newer snapshot before reading again
+            self._acting = None
+        S.wait_stream(M)  # push(t), the indices, and every greedy() that read this slot
+        with torch.cuda.stream(S):
+            for k in range(K):
+                rp.idx_static.copy_(idx[k])
+                self._graph[0].replay()
+                if self.allreduce is not None:
+                    self.allreduce.reduce()
+                    self._graph[1].replay()
+                self.n_updates += 1
+                if self.n_updates % self.target_every == 0:
+                    self.target.load_state_dict(self.source.state_dict())
+                if self.n_updates % self.updates_per_epoch == 0:
+                    self.sched.step()
+            with torch.no_grad():
+                torch._foreach_copy_(list(self.actors[slot].parameters()), list(self.source.parameters()))
+            ev = torch.cuda.Event()
+            ev.record(S)
+        self._idx_ev[slot] = ev
+        self._published.append((slot, ev))
+        self._par ^= 1
+        self.last_loss = self._graph_loss
+        return self.last_loss
+
+    def finish(self):
+        """Join the side stream: the main stream waits for every issued update; greedy() acts with
+        the source net again (evaluation)."""
+        if self._async:
+            torch.cuda.current_stream(self.device).wait_stream(self.side)
+            self._published.clear()
+            self._async = False
+            self.fused.invalidate()
+
     def _one_update(self, expand, static):
+        if self.overlap and not torch.cuda.is_current_stream_capturing():
+            fresh = self.replay.sample_indices(self.batch_size)  # eager (pre-capture) update
+            if self.replay.idx_static is None:
+                self.replay.idx_static = fresh
+            else:
+                self.replay.idx_static.copy_(fresh)
         state, a, r, nxt = self.replay.sample(self.batch_size, None if self.bit_stem else expand,
-                                              static=static)
-        loss = q_loss(self.source, self.target, state, a, r, nxt, self.gamma, self.variant == "ddqn")
+                                              static=static, idx_static=self.overlap)
+        loss = self._loss(state, a, r, nxt)
         learner_update(self.source, self.opt, loss, allreduce=self.allreduce)
         return loss.detach()
+
+    def _loss(self, state, a, r, nxt):
+        return q_loss(self.source, self.target, state, a, r, nxt, self.gamma, self.variant == "ddqn")
 
     def _graph_update(self, expand, warmup=3):
         ar = self.allreduce
@@ -269,9 +386,9 @@ class VectorDQNLearner:
                 ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
                 with torch.cuda.graph(ga):
                     state, a, r, nxt = self.replay.sample(
-                        self.batch_size, None if self.bit_stem else expand, static=True)
-                    loss = q_loss(self.source, self.target, state, a, r, nxt, self.gamma,
-                                  self.variant == "ddqn")
+                        self.batch_size, None if self.bit_stem else expand, static=True,
+                        idx_static=self.overlap)
+                    loss = self._loss(state, a, r, nxt)
                     learner_backward(self.opt, loss)
                     ar.pack(self.source)
                     self._graph_loss = loss.detach()

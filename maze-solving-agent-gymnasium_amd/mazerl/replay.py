@@ -51,6 +51,7 @@ class DeviceReplay:
         self.ptr = 0
         self.size = 0
         self.size_dev = torch.zeros((), dtype=torch.float64, **kw)  # for graph-captured sampling
+        self.idx_static = None  # sample rows read by a captured graph (overlapped learner)
         self._gen = torch.Generator(device=self.device)
         self._gen.manual_seed(0x5EED)
 
@@ -93,10 +94,17 @@ class DeviceReplay:
         u = torch.rand(batch, dtype=torch.float64, device=self.device)
         return (u * self.size_dev).to(torch.int64).clamp_(max=self.capacity - 1)
 
-    def sample(self, batch, expand, static=False):
+    def sample(self, batch, expand, static=False, idx_static=False):
         """Returns ((s6, window), a, r, (s6', window')) with f32 windows from `expand(bits)`, or
-        the packed int32 windows themselves when expand is None (QNet's HIP stem reads them)."""
-        i = self.sample_indices_static(batch) if static else self.sample_indices(batch)
+        the packed int32 windows themselves when expand is None (QNet's HIP stem reads them).
+        idx_static: read the rows from `self.idx_static` (filled by the caller before every graph
+        replay — the overlapped learner draws them on the main stream)."""
+        if idx_static:
+            if self.idx_static is None or self.idx_static.numel() != batch:
+                self.idx_static = self.sample_indices(batch)
+            i = self.idx_static
+        else:
+            i = self.sample_indices_static(batch) if static else self.sample_indices(batch)
         if expand is None:
             return ((self.s6.index_select(0, i), self.sw.index_select(0, i)), self.a.index_select(0, i),
                     self.r.index_select(0, i), (self.s6n.index_select(0, i), self.swn.index_select(0, i)))

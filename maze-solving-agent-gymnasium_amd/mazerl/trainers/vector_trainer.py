@@ -64,7 +64,9 @@ class VectorOffPolicyTrainer:
                                torch.where(self.inst_wins >= 5, ALGOS["prim&kill"], ALGOS["r-prim"]))
             env.set_algorithm(algo.to(torch.uint8))
         env.reset_done(regen_won=self.regen_won)
-        return L.update(self._expand)
+        # with an overlapped learner the updates run on its side stream; the next push (one row
+        # per instance) is kept out of their sample range
+        return L.update(self._expand, reserve=env.num_envs)
 
     def train(self, vector_steps, log_every=0, log=print):
         t0 = time.perf_counter()
@@ -79,6 +81,8 @@ class VectorOffPolicyTrainer:
                 self.history.append(rec)
                 if log:
                     log(rec)
+        if hasattr(self.learner, "finish"):
+            self.learner.finish()
         torch.cuda.synchronize()
         return time.perf_counter() - t0
 

@@ -1,0 +1,91 @@
+"""The overlapped learner (env -> learner handoff on a side HIP stream, agents/dqn.py
+VectorDQNLearner(overlap=True)) against the eager learner (q_loss / learner_update,
+dqn_agent.py:121-157).
+
+Same replay trick as test_learner_graph.py: one transition repeated, so every batch is the same
+whatever rows are drawn, and the side-stream graph replays must track the eager updates update
+for update (tolerance as there: capturable AdamW, rtol 1e-5 + atol 1e-5 on params, rel 1e-4 on
+losses). The acting snapshot greedy() reads must be the source net one update behind (the
+documented lag of the overlapped schedule), and the sampled rows must avoid the `reserve` rows
+the next push overwrites."""
+import pytest
+import torch
+
+from test_learner_graph import _fill
+
+pytestmark = pytest.mark.gpu
+
+
+def _mk(overlap, **kw):
+    from mazerl.agents.dqn import VectorDQNLearner
+    args = dict(variant="dqn", batch_size=32, capacity=64, updates_per_step=1, target_every=4,
+                updates_per_epoch=2, seed=5)
+    args.update(kw)
+    return VectorDQNLearner(4, "cuda", overlap=overlap, use_graph=overlap, **args)
+
+
+def _params(net):
+    return [p.detach().clone() for p in net.parameters()]
+
+
+def test_overlapped_updates_track_eager_and_acting_lags_one_update():
+    from mazerl import VectorMazeEnv
+    env = VectorMazeEnv(4, 21, enrich=True, device="cuda", seed=1)
+    A, B = _mk(True), _mk(False)
+    assert A.overlap and not B.overlap
+    B.source.load_state_dict(A.source.state_dict())
+    B.target.load_state_dict(A.target.state_dict())
+    _fill(A)
+    _fill(B)
+    bits, obs6 = A.replay.sw[:8].contiguous(), A.replay.s6[:8].contiguous()
+    after = [_params(B.source)]  # B's params after j updates
+    for k in range(12):
+        A.greedy(obs6, None, bits)
+        if A._async and k >= 5:
+            slot = A._acting
+            torch.cuda.synchronize()
+            for pa, pb in zip(A.actors[slot].parameters(), after[k - 1]):
+                assert torch.allclose(pa, pb, rtol=1e-5, atol=1e-5), k
+        la = A.update(env.expand_window, reserve=0)
+        lb = B.update(env.expand_window)
+        after.append(_params(B.source))
+        torch.cuda.synchronize()
+        assert float(la) == pytest.approx(float(lb), rel=1e-4, abs=1e-7), k
+    assert A._async  # the graph replays went to the side stream
+    A.finish()
+    torch.cuda.synchronize()
+    assert A.n_updates == B.n_updates == 12
+    assert float(A.opt.param_groups[0]["lr"]) == pytest.approx(B.opt.param_groups[0]["lr"], rel=1e-6)
+    for (na, pa), (nb, pb) in zip(A.source.named_parameters(), B.source.named_parameters()):
+        assert torch.allclose(pa, pb, rtol=1e-5, atol=1e-5), na
+    for pa, pb in zip(A.target.parameters(), B.target.parameters()):
+        assert torch.allclose(pa, pb, rtol=1e-5, atol=1e-5)
+    # after finish() acting reads the source net again
+    assert not A._async
+    q = A.fused(obs6, bits).float()
+    qs = A.greedy(obs6, None, bits)
+    assert torch.equal(qs, q.argmax(1))
+    env.close()
+
+
+def test_overlapped_sampling_avoids_the_next_push():
+    from mazerl import VectorMazeEnv
+    env = VectorMazeEnv(4, 21, enrich=True, device="cuda", seed=1)
+    A = _mk(True, capacity=64)
+    _fill(A, n=64)
+    _fill(A, n=40)  # wrap: ptr = 40, full
+    rp, reserve = A.replay, 16
+    for k in range(10):
+        A.update(env.expand_window, reserve=reserve)
+        if A._async:
+            slot = A._par ^ 1  # the buffer the update just issued reads
+            torch.cuda.synchronize()
+            idx = A._idx[slot].flatten().cpu()
+            ahead = (idx - rp.ptr) % rp.capacity  # 0 .. reserve-1 = rows the next push writes
+            assert int(ahead.min()) >= reserve, k
+            assert len(set(idx.tolist())) > 16  # spread over the allowed rows
+    A.finish()
+    with pytest.raises(ValueError):
+        A.update(env.expand_window, reserve=64 - 8)  # fewer rows left than a batch
+    A.finish()
+    env.close()
