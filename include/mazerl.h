@@ -233,6 +233,23 @@ int mz_stem_backward(const uint32_t* bits_dev, const uint8_t* code_dev, const fl
                      float* db_dev, void* stream);
 int mz_stem_workspace_floats(int32_t n);
 
+/* The learner's parameter update: grad.clamp_(-clamp, clamp) on every parameter, then one
+ * torch.optim.AdamW step (dqn_agent.py:152-157, ddqn_agent.py:148-152: AdamW(lr) with the
+ * defaults betas (0.9, 0.999), eps 1e-8, weight_decay 1e-2 — the eager single-tensor formula)
+ * over a flat f32 parameter buffer param_dev with its moment buffers exp_avg_dev /
+ * exp_avg_sq_dev (same length, 16-byte aligned). Gradients come as nseg (<= 16) device segments:
+ * grads_dev[k] (host array of device pointers, each 16-byte aligned) holds the gradient of flat
+ * elements [sum(seg_len[:k]), sum(seg_len[:k+1])), seg_len[k] a multiple of 4; each is scaled by
+ * grad_scale before the clamp (1/N after an all-reduce sum) and, if write_grad, written back
+ * clamped. lr_dev: f32 learning rate on the device (the cosine schedule writes it); step_dev:
+ * f32 step counter on the device, incremented by this call before the bias corrections (so a
+ * captured HIP graph advances it on every replay). One launch over every parameter. */
+int mz_adamw_flat(float* param_dev, float* exp_avg_dev, float* exp_avg_sq_dev,
+                  const float* const* grads_dev, const int64_t* seg_len, int32_t nseg,
+                  const float* lr_dev, float* step_dev, double beta1, double beta2, double eps,
+                  double weight_decay, float clamp, float grad_scale, int32_t write_grad,
+                  void* stream);
+
 /* Set the per-instance algorithm ids used by regeneration (BaseMazeEnv.ALGORITHM is global in
  * the reference, base_maze_env.py:17,60-64; here it is per instance). algo_dev [B] or NULL. */
 int mz_set_algorithm(mz_handle* h, const uint8_t* algo_dev, int32_t algo_all, void* stream);

@@ -403,6 +403,32 @@ int mz_stem_backward(const uint32_t* bits_dev, const uint8_t* code_dev, const fl
   return MZ_OK;
 }
 
+int mz_adamw_flat(float* param_dev, float* exp_avg_dev, float* exp_avg_sq_dev,
+                  const float* const* grads_dev, const int64_t* seg_len, int32_t nseg,
+                  const float* lr_dev, float* step_dev, double beta1, double beta2, double eps,
+                  double weight_decay, float clamp, float grad_scale, int32_t write_grad,
+                  void* stream) {
+  if (!param_dev || !exp_avg_dev || !exp_avg_sq_dev || !grads_dev || !seg_len || !lr_dev ||
+      !step_dev)
+    return fail(MZ_EINVAL, "bad arguments");
+  if (nseg < 1 || nseg > MZ_OPT_MAX_SEGS) return fail(MZ_EINVAL, "segment count %d", nseg);
+  const uintptr_t al = reinterpret_cast<uintptr_t>(param_dev) | reinterpret_cast<uintptr_t>(exp_avg_dev) |
+                       reinterpret_cast<uintptr_t>(exp_avg_sq_dev);
+  if (al & 15) return fail(MZ_EALIGN, "flat buffers must be 16-byte aligned");
+  for (int k = 0; k < nseg; ++k) {
+    if (!grads_dev[k] || seg_len[k] <= 0 || (seg_len[k] & 3))
+      return fail(MZ_EINVAL, "segment %d: length %lld (multiple of 4 required)", k,
+                  (long long)seg_len[k]);
+    if (reinterpret_cast<uintptr_t>(grads_dev[k]) & 15)
+      return fail(MZ_EALIGN, "gradient %d must be 16-byte aligned", k);
+  }
+  if (!(clamp > 0.0f)) return fail(MZ_EINVAL, "clamp %g", (double)clamp);
+  MZ_HIP(mz_launch_adamw(param_dev, exp_avg_dev, exp_avg_sq_dev, grads_dev, seg_len, nseg, lr_dev,
+                         step_dev, beta1, beta2, eps, weight_decay, clamp, grad_scale, write_grad,
+                         static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
 int mz_stem_workspace_floats(int32_t n) { return n > 0 ? mz_stem_chunks(n) * 32 * 28 : 0; }
 
 int mz_bank_create(mz_handle* h, int32_t slots, int32_t dim, uint32_t algo_mask) {

@@ -37,3 +37,8 @@ hipError_t mz_launch_stem_fwd(const uint32_t* bits, const float* obs6, int n, co
 hipError_t mz_launch_stem_bwd(const uint32_t* bits, const uint8_t* code, const float* g, int ld,
                               int n, float drop_p, float* partial, float* dw, float* db,
                               hipStream_t s);
+#define MZ_OPT_MAX_SEGS 16
+hipError_t mz_launch_adamw(float* p, float* m, float* v, const float* const* grads,
+                           const int64_t* seg_len, int nseg, const float* lr, float* step, double b1,
+                           double b2, double eps, double wd, float clamp, float gscale,
+                           int write_grad, hipStream_t s);

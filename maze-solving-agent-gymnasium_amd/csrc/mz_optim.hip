@@ -1,0 +1,111 @@
+// mz_optim.hip — the learner's parameter update as ONE launch over a flat f32 parameter buffer.
+//
+// The reference's optimize_model ends with (dqn_agent.py:152-157, ddqn_agent.py:148-152)
+//     for param in source_net.parameters(): param.grad.data.clamp_(-1, 1)
+//     optimizer.step()          # torch.optim.AdamW(lr), defaults betas (0.9, 0.999), eps 1e-8,
+//                               # weight_decay 1e-2
+// Through torch's multi-tensor path that is a clamp_min + clamp_max pass and a fused AdamW pass
+// whose grids follow the 8 parameter tensors in 64 Ki-element chunks: ~35 workgroups for the
+// 2,140,548 parameters, i.e. ~15 % of the CUs — 68-95 us per pass at batch 2,048
+// (profiles/r01f_train_kernel_stats.csv). Here the parameters live in one flat buffer (the
+// modules' parameters are views of it, agents/flat.py) and one grid-stride launch over float4s
+// covers every element: read p, g, m, v (16 B each), write p, m, v and the clamped g — 112 B per
+// 4 parameters, ~60 MB per step, HBM-bound.
+//
+// Per element, in torch's order (torch/optim/adamw.py single-tensor path):
+//   g = clamp(g * grad_scale, -c, c)                     (NaN propagates like Tensor.clamp_)
+//   p = p * (1 - lr * wd)
+//   m = lerp(m, g, 1 - b1)                               (m + w * (g - m), w < 0.5)
+//   v = v * b2 + (1 - b2) * g * g
+//   p = p - (lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)
+// with t the step count after this step (incremented on the device by the launcher's first
+// kernel, so a captured HIP graph advances it on every replay) and lr read from the device (the
+// cosine schedule writes it between replays).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "mz_kernels.h"
+
+namespace {
+
+struct Segs {
+  const float* g[MZ_OPT_MAX_SEGS];  // gradient of segment k: flat elements [off[k], off[k] + len[k])
+  int64_t off[MZ_OPT_MAX_SEGS + 1];
+  int n;
+};
+
+__global__ void k_step_inc(float* step) { *step += 1.0f; }
+
+__global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, float* __restrict__ m,
+                                               float* __restrict__ v, Segs segs,
+                                               const float* __restrict__ lr_dev,
+                                               const float* __restrict__ step_dev, double b1,
+                                               double b2, double eps_d, double wd, float clamp,
+                                               float gscale, int write_grad) {
+  // the per-step scalars as torch's eager AdamW forms them (Python doubles, then f32 operands)
+  const double lr = (double)*lr_dev;
+  const double t = (double)*step_dev;
+  const double bc1 = 1.0 - pow(b1, t);
+  const float step_size = (float)(lr / bc1);
+  const float bc2_sqrt = (float)sqrt(1.0 - pow(b2, t));
+  const float decay = (float)(1.0 - lr * wd);
+  const float w1 = (float)(1.0 - b1), b2f = (float)b2, w2 = (float)(1.0 - b2), eps = (float)eps_d;
+  const int64_t n4 = segs.off[segs.n] >> 2;  // every segment length is a multiple of 4
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = q << 2;
+    int k = 0;
+    while (k + 1 < segs.n && e >= segs.off[k + 1]) ++k;
+    float4* gp = reinterpret_cast<float4*>(const_cast<float*>(segs.g[k]) + (e - segs.off[k]));
+    float4 g4 = *gp;
+    float4 p4 = reinterpret_cast<float4*>(p)[q];
+    float4 m4 = reinterpret_cast<float4*>(m)[q];
+    float4 v4 = reinterpret_cast<float4*>(v)[q];
+    float* gs = &g4.x;
+    float* ps = &p4.x;
+    float* ms = &m4.x;
+    float* vs = &v4.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float g = gs[j] * gscale;
+      g = g < -clamp ? -clamp : (g > clamp ? clamp : g);
+      gs[j] = g;
+      float pj = ps[j] * decay;
+      float mj = ms[j] + w1 * (g - ms[j]);
+      float vj = vs[j] * b2f + w2 * (g * g);
+      const float denom = sqrtf(vj) / bc2_sqrt + eps;
+      pj = pj - step_size * (mj / denom);
+      ps[j] = pj;
+      ms[j] = mj;
+      vs[j] = vj;
+    }
+    reinterpret_cast<float4*>(p)[q] = p4;
+    reinterpret_cast<float4*>(m)[q] = m4;
+    reinterpret_cast<float4*>(v)[q] = v4;
+    if (write_grad) *gp = g4;  // the clamped gradient stays visible, as with clamp_ in place
+  }
+}
+
+}  // namespace
+
+hipError_t mz_launch_adamw(float* p, float* m, float* v, const float* const* grads,
+                           const int64_t* seg_len, int nseg, const float* lr, float* step, double b1,
+                           double b2, double eps, double wd, float clamp, float gscale,
+                           int write_grad, hipStream_t s) {
+  Segs sg{};
+  sg.n = nseg;
+  sg.off[0] = 0;
+  for (int k = 0; k < nseg; ++k) {
+    sg.g[k] = grads[k];
+    sg.off[k + 1] = sg.off[k] + seg_len[k];
+  }
+  hipLaunchKernelGGL(k_step_inc, dim3(1), dim3(1), 0, s, step);
+  const int64_t n4 = sg.off[nseg] >> 2;
+  int blocks = (int)((n4 + 255) / 256);
+  if (blocks > 2048) blocks = 2048;  // 8 workgroups per CU, grid-stride beyond
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(k_adamw, dim3(blocks), dim3(256), 0, s, p, m, v, sg, lr, step, b1, b2, eps, wd,
+                     clamp, gscale, write_grad);
+  return hipGetLastError();
+}

@@ -16,7 +16,7 @@ CSRC = os.path.join(ROOT, "csrc")
 LIBDIR = os.path.join(PKG, "_lib")
 LIB = os.path.join(LIBDIR, "libmazerl.so")
 SOURCES = ["mz_env.hip", "mz_api.hip", "mz_difficulty.hip", "mz_qnet.hip", "mz_metrics.hip",
-           "mz_stem.hip"]
+           "mz_stem.hip", "mz_optim.hip"]
 EXTRA_FLAGS = {"mz_qnet.hip": ["-ffinite-math-only"]}
 BASE_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall"]
 DEPS = SOURCES + ["mz_common.h", "mz_kernels.h", "mz_build.inc.h", "mz_pygen.inc.h"]
@@ -52,7 +52,7 @@ def build(force=False, verbose=False):
         subprocess.run(cmd, check=True)
         return obj
 
-    with ThreadPoolExecutor(max_workers=min(4, len(SOURCES))) as ex:
+    with ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
         objs = list(ex.map(compile_one, SOURCES))
     tmp = LIB + ".tmp"
     cmd = [hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp] + objs

@@ -27,6 +27,7 @@ import torch.optim as optim
 from torch.optim import lr_scheduler
 
 from ..replay import ReplayMemory, Transition
+from .flat import copy_flat
 from .nets import QNet
 
 
@@ -50,6 +51,10 @@ def learner_backward(optimizer, loss):
 
 
 def learner_step(net, optimizer, clamp=1.0):
+    if hasattr(optimizer, "exp_avg_sq"):  # FlatAdamW: the clamp runs inside its one launch
+        optimizer.clamp = float(clamp)
+        optimizer.step()
+        return
     grads = [p.grad for p in net.parameters() if p.grad is not None]
     torch._foreach_clamp_min_(grads, -clamp)  # == p.grad.data.clamp_(-1, 1) per parameter
     torch._foreach_clamp_max_(grads, clamp)   # (dqn_agent.py:155-156), two launches in total
@@ -181,9 +186,10 @@ class VectorDQNLearner:
         # (agents/stem.py) instead of expanding them to f32 for MIOpen
         self.bit_stem = bool(bit_stem) and self.device.type == "cuda"
         if self.use_graph:
-            self.opt = optim.AdamW(self.source.parameters(),
-                                   torch.tensor(float(lr), device=self.device), capturable=True,
-                                   fused=True)
+            # one flat buffer per net: clamp + AdamW in one launch, whole-net copies in one
+            from .flat import FlatAdamW, flatten_params
+            flatten_params(self.target)
+            self.opt = FlatAdamW(self.source, lr)
         else:
             self.opt = optim.AdamW(self.source.parameters(), lr)
         self._graph = None
@@ -214,7 +220,10 @@ class VectorDQNLearner:
             self.side = torch.cuda.Stream(self.device)
             # two actor snapshots of the source net (ping-pong) with their own fused heads and
             # dropout streams; the source net itself is only touched on `side`
+            from .flat import flatten_params
             self.actors = [copy.deepcopy(self.source) for _ in range(2)]
+            for a in self.actors:
+                flatten_params(a)
             self.actor_fused = [FusedQ(a, seed=seed * 2 + 101 + k) for k, a in enumerate(self.actors)]
             self._published = collections.deque()  # (slot, event) of issued snapshots, oldest first
             self._acting = None  # slot greedy() reads
@@ -260,10 +269,21 @@ class VectorDQNLearner:
                 self.last_loss = self._one_update(expand, static=False)
             self.n_updates += 1
             if self.n_updates % self.target_every == 0:
-                self.target.load_state_dict(self.source.state_dict())
+                self._sync_target()
             if self.n_updates % self.updates_per_epoch == 0:
                 self.sched.step()
+        if self.fused is not None:
+            self.fused.invalidate()  # FlatAdamW / graph replays leave the params' _version as is
         return self.last_loss
+
+    @torch.no_grad()
+    def _sync_target(self):
+        """update_target (dqn_agent.py): target <- source; one copy between flat buffers."""
+        if getattr(self.source, "_flat_params", None) is not None and \
+                getattr(self.target, "_flat_params", None) is not None:
+            copy_flat(self.target, self.source)
+        else:
+            self.target.load_state_dict(self.source.state_dict())
 
     # ---- overlapped learner (side stream) --------------------------------------------------
     # Vector step t on the main stream M: greedy(t) -> env step -> push(t) -> update(): the K
@@ -291,7 +311,7 @@ class VectorDQNLearner:
         M = torch.cuda.current_stream(self.device)
         with torch.no_grad():
             for a, f in zip(self.actors, self.actor_fused):
-                torch._foreach_copy_(list(a.parameters()), list(self.source.parameters()))
+                copy_flat(a, self.source)
                 f.invalidate()
         K, b = self.updates_per_step, self.batch_size
         self._idx = [torch.zeros(K, b, dtype=torch.int64, device=self.device) for _ in range(2)]
@@ -327,11 +347,11 @@ class VectorDQNLearner:
                     self._graph[1].replay()
                 self.n_updates += 1
                 if self.n_updates % self.target_every == 0:
-                    self.target.load_state_dict(self.source.state_dict())
+                    self._sync_target()
                 if self.n_updates % self.updates_per_epoch == 0:
                     self.sched.step()
             with torch.no_grad():
-                torch._foreach_copy_(list(self.actors[slot].parameters()), list(self.source.parameters()))
+                copy_flat(self.actors[slot], self.source)
             ev = torch.cuda.Event()
             ev.record(S)
         self._idx_ev[slot] = ev

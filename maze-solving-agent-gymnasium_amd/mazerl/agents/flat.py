@@ -1,0 +1,108 @@
+"""Flat parameter buffers and the one-launch clamp + AdamW of the learner update.
+
+`flatten_params(net)` moves every parameter of `net` into ONE contiguous f32 buffer (the
+parameters become views of it; autograd, state_dict and load_state_dict see ordinary leaf
+tensors). Whole-net copies — the target sync `target.load_state_dict(source.state_dict())`
+(dqn_agent.py update_target) and the overlapped learner's actor snapshots — are then one
+device copy (`copy_flat`) instead of one per tensor.
+
+`FlatAdamW` is the reference's optimizer step with its gradient clamp
+(dqn_agent.py:152-157, ddqn_agent.py:148-152: `param.grad.data.clamp_(-1, 1)` for every
+parameter, then `torch.optim.AdamW(lr)` with default betas / eps / weight decay) as one HIP
+launch over the flat buffer (`mz_adamw_flat`, csrc/mz_optim.hip): torch's multi-tensor kernels
+size their grids by tensor chunks and keep ~15 % of the CUs busy on this 8-tensor net. It is a
+torch.optim.Optimizer (one param group over the net's parameters) so the LR schedulers drive
+it; lr and the step counter live on the device, so the step can be captured in a HIP graph.
+"""
+import ctypes as C
+
+import torch
+
+from .. import _native as N
+
+
+def flatten_params(net):
+    """Make `net`'s parameters views of one flat f32 buffer (idempotent); returns the buffer."""
+    flat = getattr(net, "_flat_params", None)
+    params = list(net.parameters())
+    if flat is not None and _aliases(flat, params, net._flat_sizes):
+        return flat  # (a deepcopy clones parameters apart from the buffer: flatten again)
+    if not params:
+        raise ValueError("net has no parameters")
+    dev, dt = params[0].device, params[0].dtype
+    if any(p.device != dev or p.dtype != torch.float32 for p in params):
+        raise ValueError("flatten_params needs f32 parameters on one device")
+    sizes = [(p.numel() + 3) // 4 * 4 for p in params]  # 16-B aligned segments
+    flat = torch.zeros(sum(sizes), dtype=dt, device=dev)
+    off = 0
+    with torch.no_grad():
+        for p, n in zip(params, sizes):
+            view = flat[off:off + p.numel()].view_as(p)
+            view.copy_(p)
+            p.data = view
+            off += n
+    net._flat_params = flat
+    net._flat_sizes = sizes
+    return flat
+
+
+def _aliases(flat, params, sizes):
+    off = 0
+    for p, n in zip(params, sizes):
+        if p.data_ptr() != flat.data_ptr() + 4 * off:
+            return False
+        off += n
+    return len(params) == len(sizes)
+
+
+def copy_flat(dst_net, src_net):
+    """dst <- src for two flattened nets of the same architecture (one device copy)."""
+    dst_net._flat_params.copy_(src_net._flat_params)
+
+
+class FlatAdamW(torch.optim.Optimizer):
+    def __init__(self, net, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, clamp=1.0):
+        flat = flatten_params(net)
+        params = list(net.parameters())
+        dev = flat.device
+        if dev.type != "cuda":
+            raise RuntimeError("FlatAdamW runs on the GPU (HIP)")
+        if len(params) > 16:
+            raise ValueError("mz_adamw_flat takes at most 16 parameter tensors")
+        defaults = dict(lr=torch.tensor(float(lr), dtype=torch.float32, device=dev), betas=betas,
+                        eps=eps, weight_decay=weight_decay)
+        super().__init__(params, defaults)
+        self.flat = flat
+        self.sizes = list(net._flat_sizes)
+        self.exp_avg = torch.zeros_like(flat)
+        self.exp_avg_sq = torch.zeros_like(flat)
+        self.step_t = torch.zeros((), dtype=torch.float32, device=dev)
+        self.clamp = float(clamp)
+        self.grad_scale = 1.0
+        self.lib = N.load()
+        self._seg_len = (C.c_int64 * len(params))(*self.sizes)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        if closure is not None:
+            raise ValueError("closures are not supported")
+        g = self.param_groups[0]
+        ptrs = []
+        for p, n in zip(g["params"], self.sizes):
+            if p.grad is None:
+                raise RuntimeError("every parameter needs a gradient")
+            if p.grad.numel() != n or not p.grad.is_contiguous():
+                # segment lengths are padded to 4: pad the gradient (only tiny bias vectors)
+                pad = torch.zeros(n, dtype=p.grad.dtype, device=p.grad.device)
+                pad[:p.numel()].copy_(p.grad.reshape(-1))
+                p.grad = pad[:p.numel()].view_as(p)
+                # keep the padded storage alive with the gradient
+            ptrs.append(p.grad.data_ptr())
+        arr = (C.c_void_p * len(ptrs))(*ptrs)
+        b1, b2 = g["betas"]
+        st = torch.cuda.current_stream(self.flat.device).cuda_stream
+        N.check(self.lib.mz_adamw_flat(self.flat.data_ptr(), self.exp_avg.data_ptr(),
+                                       self.exp_avg_sq.data_ptr(), arr, self._seg_len, len(ptrs),
+                                       g["lr"].data_ptr(), self.step_t.data_ptr(), float(b1),
+                                       float(b2), float(g["eps"]), float(g["weight_decay"]),
+                                       self.clamp, float(self.grad_scale), 1, st))

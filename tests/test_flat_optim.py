@@ -1,0 +1,72 @@
+"""FlatAdamW (agents/flat.py, csrc/mz_optim.hip: the reference's per-parameter
+grad.clamp_(-1, 1) + torch.optim.AdamW step, dqn_agent.py:152-157, as one launch over a flat
+buffer) against torch.optim.AdamW (single-tensor path) + clamp_ on the same QNet, with a cosine
+schedule stepping the device-side lr. Same formula and operation order; torch's kernels may
+contract multiply-adds, so params agree within rtol 1e-5 / atol 1e-6 after 25 steps and the
+moments within rtol 1e-4 (relative to each tensor's scale)."""
+import copy
+
+import pytest
+import torch
+from torch.optim import lr_scheduler
+
+pytestmark = pytest.mark.gpu
+
+
+def test_flat_adamw_matches_torch_adamw_with_clamp():
+    from mazerl.agents.flat import FlatAdamW
+    from mazerl.agents.nets import QNet
+    torch.manual_seed(0)
+    A = QNet(variant="ddqn").cuda()
+    B = copy.deepcopy(A)
+    oa = FlatAdamW(A, lr=1e-3)
+    ob = torch.optim.AdamW(B.parameters(), lr=1e-3, foreach=False)
+    sa = lr_scheduler.CosineAnnealingLR(oa, T_max=7, eta_min=1e-5)
+    sb = lr_scheduler.CosineAnnealingLR(ob, T_max=7, eta_min=1e-5)
+    assert all(p.data_ptr() >= A._flat_params.data_ptr() for p in A.parameters())
+    g = torch.Generator(device="cuda").manual_seed(1)
+    for k in range(25):
+        for pa, pb in zip(A.parameters(), B.parameters()):
+            gr = torch.randn(pa.shape, device="cuda", generator=g) * (0.5 if k % 3 else 3.0)
+            pa.grad = gr.clone()
+            pb.grad = gr.clone()
+        oa.step()
+        for p in B.parameters():
+            p.grad.data.clamp_(-1, 1)
+        ob.step()
+        if k % 4 == 3:
+            sa.step()
+            sb.step()
+    torch.cuda.synchronize()
+    assert float(oa.param_groups[0]["lr"]) == pytest.approx(ob.param_groups[0]["lr"], rel=1e-6)
+    assert float(oa.step_t) == 25.0
+    for (n, pa), pb in zip(A.named_parameters(), B.parameters()):
+        assert torch.allclose(pa, pb, rtol=1e-5, atol=1e-6), n
+        assert torch.equal(pa.grad, pb.grad), n  # clamped in place, like clamp_
+    off = 0
+    for pb, n in zip(B.parameters(), oa.sizes):
+        st = ob.state[pb]
+        m = oa.exp_avg[off:off + pb.numel()].view_as(pb)
+        v = oa.exp_avg_sq[off:off + pb.numel()].view_as(pb)
+        assert torch.allclose(m, st["exp_avg"], rtol=1e-4, atol=1e-4 * float(st["exp_avg"].abs().max()))
+        assert torch.allclose(v, st["exp_avg_sq"], rtol=1e-4, atol=1e-4 * float(st["exp_avg_sq"].abs().max()))
+        off += n
+
+
+def test_flat_params_survive_state_dict_and_copy():
+    from mazerl.agents.flat import copy_flat, flatten_params
+    from mazerl.agents.nets import QNet
+    torch.manual_seed(0)
+    A, B = QNet(variant="dqn").cuda(), QNet(variant="dqn").cuda()
+    ref = {k: v.clone() for k, v in A.state_dict().items()}
+    fa, fb = flatten_params(A), flatten_params(B)
+    assert flatten_params(A) is fa  # idempotent
+    for k, v in A.state_dict().items():
+        assert torch.equal(v, ref[k]), k
+    copy_flat(B, A)
+    for (k, v), w in zip(B.state_dict().items(), A.state_dict().values()):
+        assert torch.equal(v, w), k
+    C = copy.deepcopy(A)  # deepcopy clones the parameters apart from the buffer
+    fc = flatten_params(C)
+    assert fc.data_ptr() != fa.data_ptr()
+    assert all(torch.equal(x, y) for x, y in zip(C.parameters(), A.parameters()))
