@@ -9,15 +9,15 @@
 // [2048, 32, 15, 15] conv output, and their backward passes: ~0.8 ms of a 1.65 ms update at
 // batch 2,048. Here:
 //
-//   k_stem_fwd     one workgroup per 2 samples: the 22 window words -> padded 17-bit rows in LDS;
-//                  one thread per (sample, channel, pooled position) computes the 4 conv outputs
-//                  of its 2x2 pool window (the window is binary: a sum of the weights under set
-//                  bits, in weight order, + bias), LeakyReLU (x > 0 ? x : x * 0.01f), dropout
-//                  (x * keep * scale, keep from a counter hash), and the max in torch's scan
-//                  order (first strict maximum wins), writing the f32 fc1 input row
-//                  [feature c*49 + q (torch's flatten order) | obs6] and, when the caller needs
-//                  the backward, one code byte per feature: the argmax position (2 bits) and its
-//                  gradient class (0 dropped, 1 kept and a > 0, 2 kept and a <= 0);
+//   k_stem_fwd     one wave per 4 samples: the 22 window words -> padded 17-bit rows -> one
+//                  27-bit patch word per conv position in LDS; the conv as an f32 MFMA GEMM
+//                  (positions x 28 patch bits x 32 channels, exact products — the window is
+//                  binary), + bias, LeakyReLU (x > 0 ? x : x * 0.01f), dropout (x * keep *
+//                  scale, keep from a counter hash) and the max in torch's scan order (first
+//                  strict maximum wins) on the accumulator registers, writing the f32 fc1 input
+//                  row [feature c*49 + q (torch's flatten order) | obs6] and, when the caller
+//                  needs the backward, one code byte per feature: the argmax position (2 bits)
+//                  and its gradient class (0 dropped, 1 kept and a > 0, 2 kept and a <= 0);
 //   k_stem_bwd     grid (sample chunk of 64, channel): the conv-output gradient at the argmax
 //                  position, g * scale (dropout) then * 0.01f when a <= 0 (LeakyReLU backward),
 //                  exactly torch's elementwise chain, accumulated into the 27 weight + 1 bias
@@ -39,7 +39,6 @@ constexpr int NPOOL = 49;
 constexpr int NOBS = 6;
 constexpr int WW = 22;       // window words per sample (675 bits)
 constexpr int PR = 17;       // padded rows per channel (rows 0 and 16 zero)
-constexpr int SPB = 2;       // samples per forward workgroup
 constexpr int CHUNK = 64;    // samples per backward workgroup
 constexpr int NACC = 28;     // 27 weights + bias per channel
 
@@ -75,7 +74,27 @@ __device__ inline void load_rows(const uint32_t* __restrict__ bits, int n, int n
   __syncthreads();
 }
 
-template <bool DROP>
+// LDS written and read by the same wave only: a wave-scope fence orders it, no s_barrier.
+__device__ inline void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+// Forward, one wave per group of FG = 4 samples (4 x 49 pooled outputs = 49 MFMA row tiles of 16),
+// 4 waves per workgroup, persistent over the groups. The conv is an f32 MFMA GEMM
+// (v_mfma_f32_16x16x4_f32, exact f32 products, an fmaf chain per output): rows = conv positions,
+// K = the 27 patch bits in torch's weight order k = ch*9 + ky*3 + kx (padded to 28: 7 MFMAs),
+// columns = the 32 output channels (two 16-column tiles). The window is binary, so A is 0.0/1.0
+// from one patch word per row, built once per group into LDS in A-row order: row i of tile t is
+// pooled output 4t + i/4 of the group at 2x2 position i%4 — the C/D map (row = 4*(lane>>4) + reg)
+// then hands every lane the 4 positions of one pool window for one channel, so LeakyReLU,
+// dropout and the max (first strict maximum in (0,0) (0,1) (1,0) (1,1) order, torch's scan) run
+// on registers. Dropout masks: the counter hash of the scalar kernel this replaced (same keys, so
+// tests/test_stem.py regenerates them).
+template <bool DROP, bool CODE>
 __global__ __launch_bounds__(256) void k_stem_fwd(const uint32_t* __restrict__ bits,
                                                   const float* __restrict__ obs6, int n,
                                                   const float* __restrict__ w,
@@ -83,68 +102,115 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const uint32_t* __restrict__ b
                                                   float scale, const uint64_t* __restrict__ rng,
                                                   uint32_t salt, float* __restrict__ feat, int ld,
                                                   uint8_t* __restrict__ code) {
-  __shared__ float ws[32 * 27];
-  __shared__ float bs[32];
-  __shared__ uint32_t wb[SPB][WW];
-  __shared__ uint32_t rows[SPB][3][PR];
-  const int tid = threadIdx.x;
-  for (int i = tid; i < 32 * 27; i += blockDim.x) ws[i] = w[i];
-  if (tid < 32) bs[tid] = b[tid];
-  const int n0 = blockIdx.x * SPB;
-  load_rows(bits, n, n0, SPB, wb, rows);
+  constexpr int FG = 4, NQ = FG * NPOOL, NT = NQ / 4;  // 196 pooled outputs, 49 tiles
+  __shared__ uint32_t wbs[4][FG * WW];
+  __shared__ uint32_t rws[4][FG * 3 * PR];
+  __shared__ uint32_t pts[4][NQ * 4];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t* wb = wbs[wid];
+  uint32_t* rows = rws[wid];
+  uint32_t* patch = pts[wid];
+  const int col = lane & 15, kq = lane >> 4;
+  // B operands: B[k = 4*kc + kq][c] = w[c][k] (0 for k = 27), c = col (tile 0) / 16 + col (tile 1)
+  float bw0[7], bw1[7];
+#pragma unroll
+  for (int kc = 0; kc < 7; ++kc) {
+    const int k = 4 * kc + kq;
+    bw0[kc] = k < 27 ? w[col * 27 + k] : 0.0f;
+    bw1[kc] = k < 27 ? w[(16 + col) * 27 + k] : 0.0f;
+  }
+  const float bias0 = b[col], bias1 = b[16 + col];
   uint32_t k0 = 0u, k1 = 0u;
   if (DROP) {
     const uint64_t key = *rng;  // device-side counter: a fresh mask per (graph-replayed) call
     k0 = (uint32_t)key ^ (salt * 0x9E3779B9u);
     k1 = (uint32_t)(key >> 32) + hash32(salt);
   }
-  for (int i = tid; i < SPB * FEAT; i += blockDim.x) {
-    const int s = i / FEAT, j = i - s * FEAT, nn = n0 + s;
-    if (nn >= n) break;
-    const int c = j / NPOOL, q = j - c * NPOOL, py = q / 7, px = q - py * 7;
-    uint32_t h0 = 0u, h1 = 0u;
-    if (DROP) {
-      const uint32_t gid = 2u * ((uint32_t)nn * FEAT + j);
-      h0 = hash32(hash32(gid ^ k0) + k1);
-      h1 = hash32(hash32((gid + 1u) ^ k0) + k1);
+  const int ngroups = (n + FG - 1) / FG;
+  for (int grp = blockIdx.x * 4 + wid; grp < ngroups; grp += gridDim.x * 4) {
+    const int n0 = grp * FG;
+    wave_sync();  // the previous group's LDS fully consumed
+    for (int i = lane; i < FG * WW; i += 64) {
+      const int s = i / WW;
+      wb[i] = n0 + s < n ? bits[(size_t)n0 * WW + i] : 0u;
     }
-    const float* wc = ws + c * 27;
-    float m = -__builtin_inff();
-    int idx = 0, cls = 0;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int y = 2 * py + (r >> 1), x = 2 * px + (r & 1);
-      float acc = 0.0f;
+    wave_sync();
+    // padded rows: rows[(s*3 + ch)*PR + pr] = grid row pr - 1, column c at bit c + 1
+    for (int i = lane; i < FG * 3 * PR; i += 64) {
+      const int sc = i / PR, pr = i - sc * PR, s = sc / 3, ch = sc - s * 3;
+      uint32_t v = 0u;
+      if (pr >= 1 && pr <= 15) {
+        const int f0 = ch * 225 + (pr - 1) * 15, j = f0 >> 5;
+        const uint64_t w2 = ((uint64_t)(j + 1 < WW ? wb[s * WW + j + 1] : 0u) << 32) | wb[s * WW + j];
+        v = ((uint32_t)(w2 >> (f0 & 31)) & 0x7FFFu) << 1;
+      }
+      rows[i] = v;
+    }
+    wave_sync();
+    // patch words in A-row order: patch[4*Q + r], Q = group pooled output, r = 2x2 position
+    for (int p = lane; p < NQ * 4; p += 64) {
+      const int Q = p >> 2, r = p & 3, s = Q / NPOOL, q = Q - s * NPOOL;
+      const int y = 2 * (q / 7) + (r >> 1), x = 2 * (q % 7) + (r & 1);
+      uint32_t pw = 0u;
 #pragma unroll
       for (int ch = 0; ch < 3; ++ch)
 #pragma unroll
-        for (int ky = 0; ky < 3; ++ky) {
-          const uint32_t b3 = (rows[s][ch][y + ky] >> x) & 7u;  // columns x-1 .. x+1
+        for (int ky = 0; ky < 3; ++ky)
+          pw |= ((rows[(s * 3 + ch) * PR + y + ky] >> x) & 7u) << (ch * 9 + ky * 3);
+      patch[p] = pw;
+    }
+    wave_sync();
+    for (int t = 0; t < NT; ++t) {
+      const uint32_t pw = patch[16 * t + col] >> kq;
+      f32x4 acc0 = {bias0, bias0, bias0, bias0};
+      f32x4 acc1 = {bias1, bias1, bias1, bias1};
 #pragma unroll
-          for (int kx = 0; kx < 3; ++kx)
-            if ((b3 >> kx) & 1u) acc += wc[ch * 9 + ky * 3 + kx];
-        }
-      const float a = acc + bs[c];
-      const float lk = a > 0.0f ? a : a * 0.01f;  // nn.LeakyReLU(negative_slope=0.01)
-      bool kept = true;
-      float v = lk;
-      if (DROP) {
-        const uint32_t u = ((r < 2 ? h0 : h1) >> (16 * (r & 1))) & 0xFFFFu;
-        kept = u >= thresh;
-        v = (lk * (kept ? 1.0f : 0.0f)) * scale;  // torch: src * mask * scale
+      for (int kc = 0; kc < 7; ++kc) {
+        const float a = (float)((pw >> (4 * kc)) & 1u);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bw0[kc], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bw1[kc], acc1, 0, 0, 0);
       }
-      if (v > m) {  // MaxPool2d: first strict maximum in (0,0) (0,1) (1,0) (1,1) order
-        m = v;
-        idx = r;
-        cls = kept ? (a > 0.0f ? 1 : 2) : 0;
+      // this lane: pooled output Q = 4t + kq, channels col and 16 + col, positions r = 0..3
+      const int Q = 4 * t + kq, s = Q / NPOOL, q = Q - s * NPOOL, nn = n0 + s;
+      if (nn >= n) continue;
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const f32x4& acc = half ? acc1 : acc0;
+        const int j = (half * 16 + col) * NPOOL + q;
+        uint32_t h0 = 0u, h1 = 0u;
+        if (DROP) {
+          const uint32_t gid = 2u * ((uint32_t)nn * FEAT + j);
+          h0 = hash32(hash32(gid ^ k0) + k1);
+          h1 = hash32(hash32((gid + 1u) ^ k0) + k1);
+        }
+        float m = -__builtin_inff();
+        int idx = 0, cls = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float a = acc[r];
+          const float lk = a > 0.0f ? a : a * 0.01f;  // nn.LeakyReLU(negative_slope=0.01)
+          bool kept = true;
+          float v = lk;
+          if (DROP) {
+            const uint32_t u = ((r < 2 ? h0 : h1) >> (16 * (r & 1))) & 0xFFFFu;
+            kept = u >= thresh;
+            v = (lk * (kept ? 1.0f : 0.0f)) * scale;  // torch: src * mask * scale
+          }
+          if (v > m) {  // MaxPool2d: first strict maximum
+            m = v;
+            idx = r;
+            cls = kept ? (a > 0.0f ? 1 : 2) : 0;
+          }
+        }
+        feat[(size_t)nn * ld + j] = m;
+        if (CODE) code[(size_t)nn * FEAT + j] = (uint8_t)(idx | (cls << 2));
       }
     }
-    feat[(size_t)nn * ld + j] = m;
-    if (code) code[(size_t)nn * FEAT + j] = (uint8_t)(idx | (cls << 2));
-  }
-  for (int i = tid; i < SPB * NOBS; i += blockDim.x) {  // || obs6 (torch.cat((fw, s), 1))
-    const int s = i / NOBS, k = i - s * NOBS, nn = n0 + s;
-    if (nn < n) feat[(size_t)nn * ld + FEAT + k] = obs6[(size_t)nn * NOBS + k];
+    for (int i = lane; i < FG * NOBS; i += 64) {  // || obs6 (torch.cat((fw, s), 1))
+      const int s = i / NOBS, k = i - s * NOBS, nn = n0 + s;
+      if (nn < n) feat[(size_t)nn * ld + FEAT + k] = obs6[(size_t)nn * NOBS + k];
+    }
   }
 }
 
@@ -218,13 +284,15 @@ hipError_t mz_launch_stem_fwd(const uint32_t* bits, const float* obs6, int n, co
   // keep iff a 16-bit uniform >= thresh: P(drop) = thresh / 65536 (0.2 -> 13107)
   const uint32_t thresh = drop_p > 0.0f ? (uint32_t)(drop_p * 65536.0f + 0.5f) : 0u;
   const float scale = drop_p > 0.0f ? (float)(1.0 / (1.0 - (double)drop_p)) : 1.0f;
-  const dim3 grid((n + SPB - 1) / SPB);
-  if (thresh)
-    hipLaunchKernelGGL(k_stem_fwd<true>, grid, dim3(256), 0, s, bits, obs6, n, w, b, thresh, scale,
-                       rng, salt, feat, ld, code);
-  else
-    hipLaunchKernelGGL(k_stem_fwd<false>, grid, dim3(256), 0, s, bits, obs6, n, w, b, 0u, 1.0f,
-                       rng, salt, feat, ld, code);
+  const int groups = (n + 3) / 4;
+  int blocks = (groups + 3) / 4;
+  if (blocks > 2048) blocks = 2048;
+#define MZ_SF(D, C)                                                                              \
+  hipLaunchKernelGGL((k_stem_fwd<D, C>), dim3(blocks), dim3(256), 0, s, bits, obs6, n, w, b,      \
+                     thresh, D ? scale : 1.0f, rng, salt, feat, ld, code)
+  if (thresh) { if (code) MZ_SF(true, true); else MZ_SF(true, false); }
+  else { if (code) MZ_SF(false, true); else MZ_SF(false, false); }
+#undef MZ_SF
   return hipGetLastError();
 }
 
