@@ -244,6 +244,14 @@ int mz_stem_workspace_floats(int32_t n);
  * clamped. lr_dev: f32 learning rate on the device (the cosine schedule writes it); step_dev:
  * f32 step counter on the device, incremented by this call before the bias corrections (so a
  * captured HIP graph advances it on every replay). One launch over every parameter. */
+/* The PPO clipped surrogate with the reference's [b, b] broadcast (ppo_agent.py:188-197, clip
+ * 0.3 there): for every column i, part_dev[i] = sum_j min(r a_i, clamp(r, 1-clip, 1+clip) a_i)
+ * and dsum_dev[i] = sum_j r * w with r = exp(lp_new[i] - lp_old[j]) and w torch's gradient
+ * routing through min / clamp (1/2 + 1/2 [inside] on ties, 1 where r a_i is the smaller, [inside]
+ * otherwise). The loss is sum(part) / b^2 and dL/dlp_new[i] = a_i dsum[i] / b^2. All f32 [b]. */
+int mz_pair_surrogate(const float* lp_new_dev, const float* lp_old_dev, const float* adv_dev,
+                      int32_t b, float clip, float* part_dev, float* dsum_dev, void* stream);
+
 int mz_adamw_flat(float* param_dev, float* exp_avg_dev, float* exp_avg_sq_dev,
                   const float* const* grads_dev, const int64_t* seg_len, int32_t nseg,
                   const float* lr_dev, float* step_dev, double beta1, double beta2, double eps,

@@ -429,6 +429,16 @@ int mz_adamw_flat(float* param_dev, float* exp_avg_dev, float* exp_avg_sq_dev,
   return MZ_OK;
 }
 
+int mz_pair_surrogate(const float* lp_new_dev, const float* lp_old_dev, const float* adv_dev,
+                      int32_t b, float clip, float* part_dev, float* dsum_dev, void* stream) {
+  if (!lp_new_dev || !lp_old_dev || !adv_dev || !part_dev || !dsum_dev || b < 0)
+    return fail(MZ_EINVAL, "bad arguments");
+  if (!(clip >= 0.0f && clip < 1.0f)) return fail(MZ_EINVAL, "clip %g", (double)clip);
+  MZ_HIP(mz_launch_pair_surrogate(lp_new_dev, lp_old_dev, adv_dev, b, clip, part_dev, dsum_dev,
+                                  static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
 int mz_stem_workspace_floats(int32_t n) { return n > 0 ? mz_stem_chunks(n) * 32 * 28 : 0; }
 
 int mz_bank_create(mz_handle* h, int32_t slots, int32_t dim, uint32_t algo_mask) {

@@ -42,3 +42,5 @@ hipError_t mz_launch_adamw(float* p, float* m, float* v, const float* const* gra
                            const int64_t* seg_len, int nseg, const float* lr, float* step, double b1,
                            double b2, double eps, double wd, float clamp, float gscale,
                            int write_grad, hipStream_t s);
+hipError_t mz_launch_pair_surrogate(const float* lp_new, const float* lp_old, const float* adv,
+                                    int b, float clip, float* part, float* dsum, hipStream_t s);

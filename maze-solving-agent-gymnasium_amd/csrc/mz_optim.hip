@@ -109,3 +109,56 @@ hipError_t mz_launch_adamw(float* p, float* m, float* v, const float* const* gra
                      clamp, gscale, write_grad);
   return hipGetLastError();
 }
+
+// ------------------------------------------------------------------------------------------
+// The PPO clipped surrogate with the reference's [b, b] broadcast (ppo_agent.py:188-197: new
+// log-probs [b] against old ones [b, 1], advantages [b] along the last dim):
+//   L = mean_{j,i} min(r_ji a_i, clamp(r_ji, 1-c, 1+c) a_i),   r_ji = exp(lp_new[i] - lp_old[j])
+// One workgroup per column i sums over j, without materialising the 4 M-element pair matrix:
+//   part[i]  = sum_j min(r_ji a_i, clamp(r_ji) a_i)
+//   dsum[i]  = sum_j r_ji * w_ji,  w = torch's gradient routing through min / clamp: 1/2 + 1/2 *
+//              [1-c <= r <= 1+c] on a tie, 1 where r a < clamp(r) a, [1-c <= r <= 1+c] otherwise
+// so dL/dlp_new[i] = a_i * dsum[i] / b^2 (the caller scales by the upstream gradient).
+static __global__ __launch_bounds__(256) void k_pair_surrogate(const float* __restrict__ lp_new,
+                                                               const float* __restrict__ lp_old,
+                                                               const float* __restrict__ adv,
+                                                               int b, float clip,
+                                                               float* __restrict__ part,
+                                                               float* __restrict__ dsum) {
+  __shared__ float red[2][4];
+  const int i = blockIdx.x, tid = threadIdx.x;
+  const float li = lp_new[i], a = adv[i];
+  const float lo = 1.0f - clip, hi = 1.0f + clip;
+  float s = 0.0f, d = 0.0f;
+  for (int j = tid; j < b; j += blockDim.x) {
+    const float r = expf(li - lp_old[j]);
+    const float s1 = r * a;
+    const float rc = r < lo ? lo : (r > hi ? hi : r);
+    const float s2 = rc * a;
+    const float inside = (r >= lo && r <= hi) ? 1.0f : 0.0f;
+    const float w = s1 == s2 ? 0.5f + 0.5f * inside : (s1 < s2 ? 1.0f : inside);
+    s += s1 < s2 ? s1 : s2;
+    d += r * w;
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    s += __shfl_xor(s, o);
+    d += __shfl_xor(d, o);
+  }
+  if ((tid & 63) == 0) {
+    red[0][tid >> 6] = s;
+    red[1][tid >> 6] = d;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    part[i] = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+    dsum[i] = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+  }
+}
+
+hipError_t mz_launch_pair_surrogate(const float* lp_new, const float* lp_old, const float* adv,
+                                    int b, float clip, float* part, float* dsum, hipStream_t s) {
+  if (b <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pair_surrogate, dim3(b), dim3(256), 0, s, lp_new, lp_old, adv, b, clip,
+                     part, dsum);
+  return hipGetLastError();
+}

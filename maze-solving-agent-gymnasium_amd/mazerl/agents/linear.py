@@ -1,0 +1,40 @@
+"""nn.Linear whose backward is safe to capture in a HIP graph on PyTorch-ROCm.
+
+Replaying a captured forward + backward of torch's own Linear at batch >= 512 gives a wrong bias
+gradient for a Linear whose input needs no gradient (the first layer of every head here) from the
+second replay on — the weight and input gradients and every other layer are right, and eager
+execution is right (profiles/dbg_graph_linear.py reproduces it: 5 of 6 replays wrong at batch
+2,048, 0 of 6 at 256; torch 2.10.0+rocm7.0, hipBLASLt or rocBLAS alike). The learners' updates
+are captured graphs (agents/dqn.py, agents/ppo.py), so on the GPU their Linear layers compute the
+same three products explicitly: dX = dY W, dW = dY^T X (GEMMs) and db = dY^T 1 (a GEMV) — the
+same arithmetic class as torch's, and correct under replay (tests/test_graph_linear.py).
+Module and parameter names are nn.Linear's, so state_dicts interchange with the reference's.
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_bias = b is not None
+        return F.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gx = gy @ w if ctx.needs_input_grad[0] else None
+        gw = gy.t() @ x if ctx.needs_input_grad[1] else None
+        gb = None
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = torch.mv(gy.t(), torch.ones(gy.shape[0], dtype=gy.dtype, device=gy.device))
+        return gx, gw, gb
+
+
+class GraphSafeLinear(nn.Linear):
+    def forward(self, x):
+        if x.is_cuda and x.dim() == 2 and torch.is_grad_enabled() and self.weight.requires_grad:
+            return _LinearFn.apply(x, self.weight, self.bias)
+        return F.linear(x, self.weight, self.bias)

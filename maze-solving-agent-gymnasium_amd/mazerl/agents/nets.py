@@ -18,6 +18,8 @@ acting). The conv front-end is MIOpen.
 import torch
 import torch.nn as nn
 
+from .linear import GraphSafeLinear
+
 WINDOW = (15, 15)
 
 
@@ -40,11 +42,11 @@ class QNet(nn.Module):
         conv_out = h_channels * (WINDOW[0] // 2) * (WINDOW[1] // 2)
         act2 = nn.ReLU() if variant == "ddqn" else nn.LeakyReLU()
         self.fc = nn.Sequential(
-            nn.Linear(conv_out + n_observations, hidden_dim),
+            GraphSafeLinear(conv_out + n_observations, hidden_dim),
             nn.LeakyReLU(),
-            nn.Linear(hidden_dim, hidden_dim // 2),
+            GraphSafeLinear(hidden_dim, hidden_dim // 2),
             act2,
-            nn.Linear(hidden_dim // 2, n_actions),
+            GraphSafeLinear(hidden_dim // 2, n_actions),
         )
         if variant == "dqn":
             for layer in self.conv:

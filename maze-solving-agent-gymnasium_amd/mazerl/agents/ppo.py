@@ -20,6 +20,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 import torch.optim as optim
 
+from .linear import GraphSafeLinear
+
 WINDOW = (15, 15)
 
 
@@ -32,16 +34,20 @@ class ActorCriticNet(nn.Module):
         d0 = h_channels * (WINDOW[0] // 2) * (WINDOW[1] // 2) + n_observations
 
         def head(out):
-            return nn.Sequential(nn.Linear(d0, hidden_dim), nn.LeakyReLU(),
-                                 nn.Linear(hidden_dim, hidden_dim // 2), nn.LeakyReLU(),
-                                 nn.Linear(hidden_dim // 2, out))
+            return nn.Sequential(GraphSafeLinear(d0, hidden_dim), nn.LeakyReLU(),
+                                 GraphSafeLinear(hidden_dim, hidden_dim // 2), nn.LeakyReLU(),
+                                 GraphSafeLinear(hidden_dim // 2, out))
         self.actor_head = head(n_actions)
         self.critic_head = head(1)
 
     def forward(self, x):
         s, w = x
-        fw = self.conv(w)
-        y = torch.cat((fw.view(fw.shape[0], -1), s), dim=1)
+        if w.dtype == torch.int32 and w.dim() == 2:  # packed windows: the HIP f32 stem
+            from .stem import stem_features  # (Conv -> LeakyReLU -> MaxPool, no dropout)
+            y = stem_features(w, s, self.conv[0], 0.0, None, 0)
+        else:
+            fw = self.conv(w)
+            y = torch.cat((fw.view(fw.shape[0], -1), s), dim=1)
         return self.actor_head(y), self.critic_head(y)
 
     def act(self, state):
@@ -58,12 +64,15 @@ class ActorCriticNet(nn.Module):
         return logp, value, entropy
 
 
-def make_optimizer(net, actor_lr, critic_lr):
+def make_optimizer(net, actor_lr, critic_lr, capturable=False):
+    """ppo_agent.py's 3-group AdamW; capturable (device step counters, fused kernel) for the
+    graph-captured minibatch step."""
+    kw = dict(capturable=True, fused=True) if capturable else {}
     return optim.AdamW([
         {"params": net.actor_head.parameters(), "lr": actor_lr},
         {"params": net.critic_head.parameters(), "lr": critic_lr},
         {"params": net.conv.parameters(), "lr": (actor_lr + critic_lr) / 2},
-    ])
+    ], **kw)
 
 
 def calculate_returns(rewards, gamma):
@@ -80,20 +89,78 @@ def calculate_advantages(returns, values):
     return (adv - adv.mean()) / (adv.std() + 1e-8)
 
 
+class _PairSurrogate(torch.autograd.Function):
+    """The reference's clipped surrogate with its [b, b] broadcast (ppo_agent.py:188-197: new
+    log-probs [b] against old ones [b, 1]): mean over (j, i) of min(r a_i, clamp(r, 1-c, 1+c) a_i)
+    with r = exp(lp_new[i] - lp_old[j]), as one HIP kernel (mz_pair_surrogate) that sums over j
+    per column without materialising the 4 M-element pair matrix, and returns the gradient's
+    column sums with it (torch.minimum splits a tie's gradient in halves, clamp passes it inside
+    [1-c, 1+c] inclusive). Besides saving ~10 passes over 16.8 MB tensors per minibatch, this
+    keeps the captured PPO step free of large temporaries: replayed from a HIP graph with eager
+    work in between, the torch expression's gradient came out wrong at batch 2,048 on
+    PyTorch-ROCm (profiles/dbg_ppo_graph.py; tests/test_ppo_gpu.py)."""
+
+    @staticmethod
+    def forward(ctx, lp_new, lp_old, adv, clip):
+        from .. import _native as N
+        b = lp_new.shape[0]
+        lp_new, lp_old, adv = (t.contiguous().float() for t in (lp_new, lp_old, adv))
+        part = torch.empty(b, dtype=torch.float32, device=lp_new.device)
+        dsum = torch.empty_like(part)
+        st = torch.cuda.current_stream(lp_new.device).cuda_stream
+        N.check(N.load().mz_pair_surrogate(lp_new.data_ptr(), lp_old.data_ptr(), adv.data_ptr(), b,
+                                           float(clip), part.data_ptr(), dsum.data_ptr(), st))
+        ctx.save_for_backward(adv, dsum)
+        ctx.n = b * lp_old.shape[0]
+        return part.sum() / ctx.n
+
+    @staticmethod
+    def backward(ctx, g):
+        adv, dsum = ctx.saved_tensors
+        return adv * dsum * (g / ctx.n), None, None, None
+
+
 def ppo_losses(logp_old, logp_new, advantages, entropy, returns, value_pred, entropy_coef,
                clip=0.3):
     advantages = advantages.detach()
-    ratio = (logp_new - logp_old).exp()
-    s1 = ratio * advantages
-    s2 = torch.clamp(ratio, min=1 - clip, max=1 + clip) * advantages
-    surrogate = torch.min(s1, s2).mean()
+    if logp_new.is_cuda and logp_new.dim() == 1 and logp_old.dim() == 2 and logp_old.shape[1] == 1 \
+            and advantages.dim() == 1:
+        surrogate = _PairSurrogate.apply(logp_new, logp_old.detach(), advantages, clip)
+    else:
+        ratio = (logp_new - logp_old).exp()
+        s1 = ratio * advantages
+        s2 = torch.clamp(ratio, min=1 - clip, max=1 + clip) * advantages
+        surrogate = torch.min(s1, s2).mean()
     policy_loss = -(surrogate + entropy * entropy_coef).mean()
     value_loss = F.mse_loss(returns.unsqueeze(1), value_pred)
     return policy_loss, value_loss
 
 
+def ppo_minibatch(net, optimizer, pos, win, act, lp_old, adv, ret, entropy_coef, allreduce=None,
+                  phase=None):
+    """One minibatch step of optimize_model (ppo_agent.py:217-236). phase "a" / "b" split it
+    around the gradient all-reduce (backward + pack / unpack + clip + step) for graph capture."""
+    if phase != "b":
+        lp_new, value, ent = net.evaluate((pos, win), act)
+        pl, vl = ppo_losses(lp_old, lp_new, adv, ent, ret, value, entropy_coef)
+        total = pl + 0.5 * vl
+        optimizer.zero_grad()
+        total.backward()
+        if phase == "a":
+            allreduce.pack(net)
+            return total.detach()
+        if allreduce is not None:
+            allreduce(net)
+    else:
+        allreduce.unpack(net)
+        total = None
+    torch.nn.utils.clip_grad_norm_(net.parameters(), max_norm=0.5)
+    optimizer.step()
+    return total.detach() if total is not None else None
+
+
 def optimize_model(net, optimizer, states, actions, logp, advantages, returns, entropy_coef,
-                   batch_size, ppo_steps, allreduce=None):
+                   batch_size, ppo_steps, allreduce=None, graph=None):
     """The reference iterates DataLoader(TensorDataset(...), batch_size, shuffle=False)
     (ppo_agent.py:214-216): consecutive, unshuffled minibatches with a short last one. The
     same minibatches are taken here as slices (a DataLoader over device tensors would gather
@@ -103,18 +170,71 @@ def optimize_model(net, optimizer, states, actions, logp, advantages, returns, e
     last = None
     for _ in range(ppo_steps):
         for i in range(0, n, batch_size):
-            pos, win, act, lp_old, adv, ret = (c[i:i + batch_size] for c in cols)
-            lp_new, value, ent = net.evaluate((pos, win), act)
-            pl, vl = ppo_losses(lp_old, lp_new, adv, ent, ret, value, entropy_coef)
-            total = pl + 0.5 * vl
-            optimizer.zero_grad()
-            total.backward()
-            if allreduce is not None:
-                allreduce(net)
-            torch.nn.utils.clip_grad_norm_(net.parameters(), max_norm=0.5)
-            optimizer.step()
-            last = total.detach()
+            mb = [c[i:i + batch_size] for c in cols]
+            if graph is not None and mb[0].shape[0] == graph.batch:
+                last = graph.step(mb, entropy_coef)  # full minibatch: HIP graph replay
+            else:
+                last = ppo_minibatch(net, optimizer, *mb, entropy_coef, allreduce=allreduce)
     return last
+
+
+class PPOMinibatchGraph:
+    """optimize_model's full-size minibatch step (forward of both heads from packed windows,
+    the clipped-surrogate / entropy / value losses, backward, clip_grad_norm_(0.5), AdamW) captured
+    once into a HIP graph and replayed: ~250 small kernels per minibatch are launch-bound when
+    issued eagerly. Inputs are copied into static buffers before each replay; the entropy
+    coefficient lives on the device. With a gradient all-reduce it is two graphs with the one
+    RCCL all-reduce between the replays (as the DQN learner, agents/dqn.py). The optimizer must
+    be capturable (make_optimizer(..., capturable=True))."""
+
+    def __init__(self, net, optimizer, batch, allreduce=None, warmup=3):
+        self.net, self.opt, self.batch, self.allreduce = net, optimizer, batch, allreduce
+        self.warmup, self.done_eager = warmup, 0
+        self.graphs = None
+        self.static = None
+        self.coef = None
+        self.loss = None
+
+    def _alloc(self, mb):
+        self.static = [torch.empty_like(x) for x in mb]
+        self.coef = torch.zeros((), dtype=torch.float32, device=mb[0].device)
+
+    def step(self, mb, entropy_coef):
+        if self.static is None:
+            self._alloc(mb)
+        for d, x in zip(self.static, mb):
+            d.copy_(x)
+        self.coef.fill_(float(entropy_coef))
+        ar, dev = self.allreduce, mb[0].device
+        if self.graphs is None:
+            if self.done_eager < self.warmup:  # real steps on a side stream before capture
+                s = torch.cuda.Stream(dev)
+                s.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(s):
+                    out = ppo_minibatch(self.net, self.opt, *self.static, self.coef, allreduce=ar)
+                torch.cuda.current_stream(dev).wait_stream(s)
+                self.done_eager += 1
+                return out
+            self.opt.zero_grad(set_to_none=True)
+            if ar is None:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self.loss = ppo_minibatch(self.net, self.opt, *self.static, self.coef)
+                self.graphs = (g,)
+            else:
+                ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(ga):
+                    self.loss = ppo_minibatch(self.net, self.opt, *self.static, self.coef,
+                                              allreduce=ar, phase="a")
+                with torch.cuda.graph(gb, pool=ga.pool()):
+                    ppo_minibatch(self.net, self.opt, *self.static, self.coef, allreduce=ar,
+                                  phase="b")
+                self.graphs = (ga, gb)
+        self.graphs[0].replay()
+        if ar is not None:
+            ar.reduce()
+            self.graphs[1].replay()
+        return self.loss
 
 
 class PPOAgent:

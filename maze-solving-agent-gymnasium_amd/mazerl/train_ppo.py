@@ -28,6 +28,9 @@ def main(argv=None):
     ap.add_argument("--gamma", type=float, default=0.9)
     ap.add_argument("--eval-mazes", type=int, default=1000)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--eager-update", action="store_true", help="no captured minibatch step")
+    ap.add_argument("--f32-window-update", action="store_true",
+                    help="update through the f32 window + torch conv instead of the HIP bit stem")
     a = ap.parse_args(argv)
     if "-" in a.dims:
         lo, hi = (int(x) for x in a.dims.split("-"))
@@ -40,7 +43,8 @@ def main(argv=None):
     env = make_env(a.envs, dims, toroidal=True, algorithm=a.algo, seed=0x5EED0000 + rank * a.envs,
                    device=dev, done_list=False, reward64=True, window=False, window_bits=True)
     tr = VectorPPOTrainer(env, dev, gamma=a.gamma, batch_size=a.batch, ppo_steps=a.ppo_steps,
-                          pool_size=a.pool, seed=a.seed,
+                          pool_size=a.pool, seed=a.seed, use_graph=not a.eager_update,
+                          bit_stem=not a.f32_window_update,
                           allreduce=GradAllReduce() if world > 1 else None)
     if world > 1:
         broadcast_params(tr.net)

@@ -19,18 +19,24 @@ import torch
 import torch.nn.functional as F
 
 from .. import _native as N
-from ..agents.ppo import ActorCriticNet, make_optimizer, optimize_model
+from ..agents.ppo import ActorCriticNet, PPOMinibatchGraph, make_optimizer, optimize_model
 
 
 class VectorPPOTrainer:
     def __init__(self, env, device, actor_lr=3e-4, critic_lr=1e-4, gamma=0.9, batch_size=2048,
                  ppo_steps=4, pool_size=65536, hidden_dim=1024, h_channels=32, seed=0,
-                 allreduce=None, act_bf16=True):
+                 allreduce=None, act_bf16=True, use_graph=True, bit_stem=True):
         self.env = env
         self.device = torch.device(device)
         torch.manual_seed(seed)
         self.net = ActorCriticNet(3, 6, 4, h_channels, hidden_dim).to(self.device)
-        self.opt = make_optimizer(self.net, actor_lr, critic_lr)
+        # on the GPU the update reads the pool's packed windows through the HIP stem and replays
+        # a captured minibatch step (PPOMinibatchGraph)
+        self.on_gpu = self.device.type == "cuda"
+        self.bit_stem = self.on_gpu and bit_stem
+        self.opt = make_optimizer(self.net, actor_lr, critic_lr, capturable=self.on_gpu and use_graph)
+        self.graph = (PPOMinibatchGraph(self.net, self.opt, batch_size, allreduce)
+                      if self.on_gpu and use_graph else None)
         self.gamma, self.batch_size, self.ppo_steps = gamma, batch_size, ppo_steps
         self.pool_size = pool_size
         self.allreduce = allreduce
@@ -124,13 +130,15 @@ class VectorPPOTrainer:
         self.pool = [tuple(rest)] if rest[0].shape[0] else []
         self.pool_n = int(rest[0].shape[0])
         s6, w, a, lp, adv, ret = (x[:P] for x in cat)
-        win = self.env.expand_window(w)
+        win = w if self.bit_stem else self.env.expand_window(w)  # packed bits -> HIP stem
         coef = 1e-2 - (1e-2 - 5e-4) * frac  # ppo_trainer.py:73
         keep = (adv == adv) & (ret == ret)  # a 1-step episode has an undefined std (NaN): drop
         if not bool(keep.all()):
             s6, win, a, lp, adv, ret = (x[keep] for x in (s6, win, a, lp, adv, ret))
         optimize_model(self.net, self.opt, (s6, win), a[:, None], lp[:, None], adv, ret, coef,
-                       self.batch_size, self.ppo_steps, allreduce=self.allreduce)
+                       self.batch_size, self.ppo_steps, allreduce=self.allreduce, graph=self.graph)
+        if self.fused is not None:
+            self.fused.invalidate()  # graph replays leave the params' _version as is
         self.updates += 1
 
     def vector_step(self, frac=0.0):

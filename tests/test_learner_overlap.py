@@ -89,3 +89,44 @@ def test_overlapped_sampling_avoids_the_next_push():
         A.update(env.expand_window, reserve=64 - 8)  # fewer rows left than a batch
     A.finish()
     env.close()
+
+
+def test_overlapped_updates_on_distinct_rows_match_a_reference_update():
+    """Distinct transitions in the replay: each side-stream graph replay must equal q_loss +
+    learner_update (the reference's optimize_model, dqn_agent.py:121-157) computed eagerly on the
+    rows the update drew: loss and clamped gradients, one update at a time (a repeated transition
+    would hide a gradient that goes stale between replays)."""
+    from mazerl import VectorMazeEnv
+    from mazerl.agents.dqn import q_loss
+    env = VectorMazeEnv(4, 21, enrich=True, device="cuda", seed=1)
+    A, B = _mk(True, batch_size=1024, capacity=4096), _mk(False, batch_size=1024, capacity=4096)
+    B.source.load_state_dict(A.source.state_dict())
+    B.target.load_state_dict(A.target.state_dict())
+    g = torch.Generator(device="cuda").manual_seed(3)
+    n = 4096
+    s6, s6n = (torch.randn(n, 6, device="cuda", generator=g) for _ in range(2))
+    sw, swn = (torch.randint(0, 2**31 - 1, (n, 22), device="cuda", generator=g, dtype=torch.int32)
+               for _ in range(2))
+    a = torch.randint(0, 4, (n,), device="cuda", generator=g)
+    r = torch.randn(n, device="cuda", generator=g)
+    for L in (A, B):
+        L.replay.push(s6, sw, a, r, s6n, swn)
+    for k in range(8):
+        B.source.load_state_dict(A.source.state_dict())  # A's nets before this update
+        B.target.load_state_dict(A.target.state_dict())
+        A.update(env.expand_window, reserve=0)
+        torch.cuda.synchronize()
+        if not A._async:  # eager warm-up and capture updates draw their own rows
+            continue
+        idx = A._idx[A._par ^ 1][0]  # the rows this side-stream update read
+        rp = B.replay
+        loss = q_loss(B.source, B.target, (rp.s6[idx], rp.sw[idx]), rp.a[idx], rp.r[idx],
+                      (rp.s6n[idx], rp.swn[idx]), B.gamma, False)
+        B.opt.zero_grad()
+        loss.backward()
+        for (name, pa), pb in zip(A.source.named_parameters(), B.source.parameters()):
+            ref = pb.grad.clamp(-1, 1)  # A's FlatAdamW leaves the clamped gradient in place
+            assert torch.allclose(pa.grad, ref, rtol=1e-3, atol=1e-4 * float(ref.abs().max())), (k, name)
+        assert float(A.last_loss) == pytest.approx(float(loss), rel=1e-4), k
+    A.finish()
+    env.close()
