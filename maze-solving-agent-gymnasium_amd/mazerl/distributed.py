@@ -20,9 +20,11 @@ def init_from_env(backend=None):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and not dist.is_initialized():
-        if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend is None:  # MZ_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs
+            backend = os.environ.get("MZ_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         dist.init_process_group(backend, init_method="env://")
+    if torch.cuda.is_available() and torch.cuda.device_count() > 0:
+        local %= torch.cuda.device_count()  # rehearsal: several ranks share a GPU
     return rank, world, local
 
 

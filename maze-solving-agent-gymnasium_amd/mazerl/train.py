@@ -37,6 +37,8 @@ def parse(argv=None):
     ap.add_argument("--eval-mazes", type=int, default=1000)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--log-every", type=int, default=50)
+    ap.add_argument("--overlap", type=int, default=1,
+                    help="1: updates on a side HIP stream (acting one update behind); 0: sequential")
     return ap.parse_args(argv)
 
 
@@ -59,7 +61,8 @@ def main(argv=None):
                                eps_final=a.eps_final, eps_decay=decay, gamma=a.gamma,
                                batch_size=a.batch, capacity=a.capacity,
                                updates_per_step=a.updates_per_step, target_every=a.target_every,
-                               allreduce=GradAllReduce() if world > 1 else None, seed=a.seed)
+                               allreduce=GradAllReduce() if world > 1 else None, seed=a.seed,
+                               overlap=bool(a.overlap))
     if world > 1:
         broadcast_params(learner.source)
         learner.target.load_state_dict(learner.source.state_dict())
