@@ -1,6 +1,6 @@
 // mz_env.hip — the per-step hot path of the batched maze env on gfx950 (+ build/reset kernels).
 //
-//   k_step        BaseMazeEnv.step (base_maze_env.py:163-210) for 32 instances per 64-lane wave:
+//   k_step        BaseMazeEnv.step (base_maze_env.py:163-210) for IPW (16) instances per 64-lane wave:
 //                 phase 1, one lane per instance: (optional fused epsilon-greedy act,
 //                   dqn_agent.py:104-116) move rule of maze_view.move_agent (maze_view.py:167-197),
 //                   reward, counters, "best dir" from the precomputed cell word, done-list
@@ -8,7 +8,7 @@
 //                 phase 2, one lane per (instance, window row): the Enrich window
 //                   (maze_handler.py:4-99) from the open/visited bit planes, 15 consecutive lanes
 //                   reading 15 consecutive 32-B rows of one instance (few cache lines per load);
-//                 phase 3, the wave's 32 windows (21,600 bits back to back in LDS) leave as f32
+//                 phase 3, the wave's IPW windows (675 bits each, back to back in LDS) leave as f32
 //                   with 16-B stores, 1 KiB contiguous per wave instruction.
 //   k_reset_list  one wave per listed instance: BaseMazeEnv.reset (:136-161); consumes the
 //                 device done count it was given (zeroes it when the grid has read it).
@@ -24,8 +24,14 @@
 #include "../../include/mazerl.h"
 
 #define WAVE 64
-#define IPW 32                          // instances per wave in k_step
-#define CAT_WORDS (IPW * 675 / 32 + 2)  // 21,600 window bits + funnel-shift slack
+// Instances per wave in k_step. 16 (4,096 waves at 65,536 instances: twice the gathers in flight,
+// finer-grained window stores) measured best: k_step at 65,536 x 81 = 38.8 / 34.4 / 36.1 / 40.4 us
+// at 8 / 16 / 32 / 64 (bench, 500 launches).
+#ifndef MZ_IPW
+#define MZ_IPW 16
+#endif
+#define IPW MZ_IPW
+#define CAT_WORDS (IPW * 675 / 32 + 2)  // IPW x 675 window bits + funnel-shift slack
 
 namespace {
 
@@ -287,7 +293,7 @@ __device__ inline void win_band(int r, int c, int tr, int tc, int N, int& geo, i
 #define WIN_IT (IPW * 16 / WAVE)  // band rows per lane: lane l of pass it = instance 4*it + l/16, row l%16
 
 // ------------------------------------------------------------------------------------------
-// One vector step, 32 instances per 64-lane wave, with two dependent global round trips:
+// One vector step, IPW instances per 64-lane wave, with two dependent global round trips:
 //   level 1  per-instance state (5 coalesced u32 + eps/greedy or the given action), and the
 //            reward tables into LDS;
 //   level 2  target-cell word and its visit count (one lane per instance), and the 16-row
@@ -297,7 +303,7 @@ __device__ inline void win_band(int r, int c, int tr, int tc, int N, int& geo, i
 //   then     reward / counters (BaseMazeEnv.step, base_maze_env.py:163-210), the Enrich window
 //            assembled bit by bit in LDS from band rows picked with a lane shuffle (row i of
 //            the chosen window = band row off + i), and only then every global store: state,
-//            outputs, and the 32 windows as f32 with 16-B stores (1 KiB per wave instruction).
+//            outputs, and the IPW windows as f32 with 16-B stores (1 KiB per wave instruction).
 //            No wait in the kernel ever covers a store.
 // AR (autoreset): an instance whose previous step ended terminated|truncated is reset by this
 // launch instead of stepping (BaseMazeEnv.reset, :136-161: same maze, agent at start, visits

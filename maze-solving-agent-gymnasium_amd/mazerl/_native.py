@@ -54,7 +54,7 @@ def load(build_if_missing=True):
     global _lib
     if _lib is not None:
         return _lib
-    path = _build.LIB
+    path = os.environ.get("MZ_LIB_OVERRIDE") or _build.LIB  # an alternative build (experiments)
     if not os.path.exists(path):
         if not build_if_missing:
             raise RuntimeError(f"libmazerl.so not built ({path}); run mazerl._build.build()")
