@@ -157,6 +157,7 @@ def cpu_baseline(env, seconds):
     for every find_path) timed on this host's cores on one of the benchmark's own mazes."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as O
+    from mazerl import VectorMazeEnv
     q = env.query(0)
     grid = env.grid(0)
     start, goal = (q["start_r"], q["start_c"]), (q["goal_r"], q["goal_c"])
@@ -168,8 +169,22 @@ def cpu_baseline(env, seconds):
     t, n = O.bench(grid, start, goal, False, True, True, threads, per_env, threads, seed=2)
     tf, nf = O.bench(grid, start, goal, False, True, False, threads, per_env * 20, threads, seed=3)
     t1, n1 = O.bench(grid, start, goal, False, True, True, 1, max(20, per_env // 4), 1, seed=4)
+    per_config = {}
+    for name, dim, tor in (("cfg2 15x15 euclidean Enrich", 15, False),
+                           ("cfg5 29x29 toroidal Enrich", 29, True)):
+        # the other configs' grids, one maze each (generated on the GPU), reference-cost mode
+        e2 = VectorMazeEnv(1, dim, toroidal=tor, enrich=True, device=env.device, seed=0x5EED0000)
+        q2 = e2.query(0)
+        g2 = e2.grid(0)
+        e2.close()
+        s2, g2p = (q2["start_r"], q2["start_c"]), (q2["goal_r"], q2["goal_c"])
+        tc, nc = O.bench(g2, s2, g2p, tor, True, True, threads, 2000, threads)
+        per = max(2000, int(nc / max(tc, 1e-9) * 1.5 / threads))  # ~1.5 s sample
+        tc, nc = O.bench(g2, s2, g2p, tor, True, True, threads, per, threads, seed=5)
+        per_config[name] = {"value": nc / tc, "steps": nc, "seconds": round(tc, 2)}
     return {"value": n / t, "unit": "env steps/s", "cores": threads, "kind": "port",
             "single_core": {"value": n1 / t1, "steps": n1, "seconds": round(t1, 2)},
+            "per_config": per_config,
             "sample": f"{threads} envs x {per_env} steps (81x81 r-prim Enrich, masked-exploration "
                       f"actions, auto-reset), oracle in reference-cost mode (heap A* per find_path); "
                       f"{t:.1f} s",
