@@ -244,6 +244,11 @@ int mz_stem_workspace_floats(int32_t n);
  * clamped. lr_dev: f32 learning rate on the device (the cosine schedule writes it); step_dev:
  * f32 step counter on the device, incremented by this call before the bias corrections (so a
  * captured HIP graph advances it on every replay). One launch over every parameter. */
+/* nn.LeakyReLU(slope) in place on n bf16 values (the acting head's hidden layers, dqn_agent.py
+ * :52-57): x > 0 ? x : x * slope in f32, rounded to nearest even — torch's leaky_relu_ on bf16
+ * element for element. n a multiple of 8, x_dev 16-byte aligned. */
+int mz_leaky_relu_bf16(uint16_t* x_dev, int64_t n, float slope, void* stream);
+
 /* The PPO clipped surrogate with the reference's [b, b] broadcast (ppo_agent.py:188-197, clip
  * 0.3 there): for every column i, part_dev[i] = sum_j min(r a_i, clamp(r, 1-clip, 1+clip) a_i)
  * and dsum_dev[i] = sum_j r * w with r = exp(lp_new[i] - lp_old[j]) and w torch's gradient

@@ -429,6 +429,14 @@ int mz_adamw_flat(float* param_dev, float* exp_avg_dev, float* exp_avg_sq_dev,
   return MZ_OK;
 }
 
+int mz_leaky_relu_bf16(uint16_t* x_dev, int64_t n, float slope, void* stream) {
+  if (!x_dev || n < 0) return fail(MZ_EINVAL, "bad arguments");
+  if ((n & 7) || (reinterpret_cast<uintptr_t>(x_dev) & 15))
+    return fail(MZ_EALIGN, "leaky_relu_bf16 needs a 16-byte aligned multiple of 8 elements");
+  MZ_HIP(mz_launch_leaky_bf16(x_dev, n, slope, static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
 int mz_pair_surrogate(const float* lp_new_dev, const float* lp_old_dev, const float* adv_dev,
                       int32_t b, float clip, float* part_dev, float* dsum_dev, void* stream) {
   if (!lp_new_dev || !lp_old_dev || !adv_dev || !part_dev || !dsum_dev || b < 0)

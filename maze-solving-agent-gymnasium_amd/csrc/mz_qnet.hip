@@ -262,3 +262,32 @@ hipError_t mz_launch_qfront(const uint32_t* bits, const float* obs6, int n, cons
                        1.0f, 0u, 0u, o, ld);
   return hipGetLastError();
 }
+
+// LeakyReLU in place on the bf16 output of the acting head's first Linear (65,536 x 1,024 per
+// vector step; dqn_agent.py:52-57 nn.LeakyReLU): x > 0 ? x : x * slope in f32, rounded to bf16
+// (round to nearest even) — torch's leaky_relu_ on bf16 element for element. 8 elements per
+// 16-B load / store, grid-stride; torch's elementwise kernel moves these 268 MB at ~3.8 TB/s.
+static __global__ __launch_bounds__(256) void k_leaky_bf16(uint4* __restrict__ x, int64_t n8,
+                                                           float slope) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    uint4 v = x[i];
+    uint32_t* w = &v.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float lo = __uint_as_float(w[k] << 16), hi = __uint_as_float(w[k] & 0xFFFF0000u);
+      w[k] = bf16x2(lo > 0.0f ? lo : lo * slope, hi > 0.0f ? hi : hi * slope);
+    }
+    x[i] = v;
+  }
+}
+
+hipError_t mz_launch_leaky_bf16(uint16_t* x, int64_t n, float slope, hipStream_t s) {
+  const int64_t n8 = n >> 3;
+  if (n8 == 0) return hipSuccess;
+  int64_t blocks = (n8 + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(k_leaky_bf16, dim3((unsigned)blocks), dim3(256), 0, s,
+                     reinterpret_cast<uint4*>(x), n8, slope);
+  return hipGetLastError();
+}

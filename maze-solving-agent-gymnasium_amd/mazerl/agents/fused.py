@@ -30,9 +30,20 @@ def feature_perm(device=None):
     return torch.arange(CONV_OUT, device=device).view(32, 49).t().reshape(-1)
 
 
+def _leaky_(h, slope):
+    """In-place LeakyReLU; bf16 on the GPU through mz_leaky_relu_bf16 (torch's elementwise kernel
+    moves the 65,536 x 1,024 hidden layer at ~3.8 TB/s), same rounding as F.leaky_relu_."""
+    if h.is_cuda and h.dtype == torch.bfloat16 and h.is_contiguous() and h.numel() % 8 == 0 \
+            and h.data_ptr() % 16 == 0:
+        N.check(N.load().mz_leaky_relu_bf16(h.data_ptr(), h.numel(), float(slope),
+                                            torch.cuda.current_stream(h.device).cuda_stream))
+        return h
+    return F.leaky_relu_(h, slope)
+
+
 def _act_fn(m):
     if isinstance(m, nn.LeakyReLU):
-        return lambda h: F.leaky_relu_(h, m.negative_slope)
+        return lambda h: _leaky_(h, m.negative_slope)
     if isinstance(m, nn.ReLU):
         return F.relu_
     raise TypeError(f"unsupported activation {type(m).__name__}")
@@ -46,8 +57,10 @@ class _Head:
     def __init__(self, seq):
         self.seq = seq
         self.lin = [m for m in seq if isinstance(m, nn.Linear)]
-        self.acts = [_act_fn(m) for m in seq if not isinstance(m, nn.Linear)]
+        acts = [m for m in seq if not isinstance(m, nn.Linear)]
+        self.acts = [_act_fn(m) for m in acts]
         assert len(self.lin) == 3 and len(self.acts) == 2
+        self.relu2 = isinstance(acts[1], nn.ReLU)
         l0 = self.lin[0]
         if l0.in_features > LD:
             raise ValueError(f"first Linear has {l0.in_features} inputs > {LD}")
@@ -76,7 +89,10 @@ class _Head:
         self._refresh()
         (w0, b0), (w1, b1), (w2, b2) = self._w
         h = self.acts[0](F.linear(feat, w0, b0))
-        h = self.acts[1](F.linear(h, w1, b1))
+        if self.relu2:  # bias + ReLU as the GEMM's epilogue (hipBLASLt), bit-identical
+            h = torch._addmm_activation(b1, h, w1.t())
+        else:
+            h = self.acts[1](F.linear(h, w1, b1))
         return F.linear(h, w2, b2)
 
 
