@@ -2,7 +2,9 @@
 the same code over RCCL) with different replay data. The HIP-graph-captured update (backward +
 pack graph, the all-reduce of the flat gradient bucket, unpack + clamp + AdamW graph) must track
 the eager all-reduce update (learner_update, dqn_agent.py:121-157 with the gradient average of
-SURVEY §8e) update for update, and both ranks must hold bit-identical weights afterwards.
+SURVEY §8e) update for update, and both ranks must hold bit-identical weights afterwards — also
+with the overlapped schedule (bench.py's default: graph replays and the all-reduce issued on the
+side stream, agents/dqn.py VectorDQNLearner(overlap=True)).
 Tolerances as in test_learner_graph.py (capturable vs eager AdamW arithmetic)."""
 import os
 import socket
@@ -23,7 +25,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, overlap):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK="0")
     import torch.distributed as dist
@@ -34,10 +36,11 @@ def _worker(rank, world, port, outdir):
     init_from_env("gloo")
     torch.cuda.set_device(0)
     env = VectorMazeEnv(4, 21, enrich=True, device="cuda", seed=1)
-    mk = lambda g: VectorDQNLearner(4, "cuda", variant="ddqn", batch_size=32, capacity=64,  # noqa: E731
-                                    updates_per_step=1, target_every=4, updates_per_epoch=2,
-                                    seed=5 + rank, use_graph=g, allreduce=GradAllReduce())
-    A, B = mk(True), mk(False)
+    mk = lambda g, ov: VectorDQNLearner(4, "cuda", variant="ddqn", batch_size=32, capacity=64,  # noqa: E731
+                                        updates_per_step=1, target_every=4, updates_per_epoch=2,
+                                        seed=5 + rank, use_graph=g, overlap=ov,
+                                        allreduce=GradAllReduce())
+    A, B = mk(True, overlap), mk(False, False)
     assert A.use_graph and not B.use_graph
     broadcast_params(A.source)  # rank 1 started from other weights (seed 5 + rank)
     A.target.load_state_dict(A.source.state_dict())
@@ -47,12 +50,17 @@ def _worker(rank, world, port, outdir):
     _fill(B, seed=10 + rank)
     # Dropout(0.2) in train mode (Q13) would draw different masks in the two paths
     A.source.eval(); A.target.eval(); B.source.eval(); B.target.eval()
-    losses = []
+    losses, went_async = [], False
     for _ in range(9):
-        la = A.update(env.expand_window)
+        la = A.update(env.expand_window, reserve=0)
+        went_async |= bool(getattr(A, "_async", False))
         lb = B.update(env.expand_window)
         torch.cuda.synchronize()
         losses.append((float(la), float(lb)))
+    if overlap:
+        A.finish()
+        torch.cuda.synchronize()
+    assert went_async == overlap
     assert A._graph is not None and len(A._graph) == 2
     torch.save({"losses": losses,
                 "A": [p.detach().cpu() for p in A.source.parameters()],
@@ -62,9 +70,10 @@ def _worker(rank, world, port, outdir):
     dist.destroy_process_group()
 
 
-def test_graph_allreduce_update_tracks_eager_two_ranks():
+@pytest.mark.parametrize("overlap", [False, True], ids=["sequential", "overlapped"])
+def test_graph_allreduce_update_tracks_eager_two_ranks(overlap):
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        mp.spawn(_worker, args=(2, _free_port(), d, overlap), nprocs=2, join=True)
         r = [torch.load(os.path.join(d, f"r{k}.pt"), weights_only=True) for k in range(2)]
     for k in range(2):
         for la, lb in r[k]["losses"]:
