@@ -31,6 +31,12 @@
 #define MZ_IPW 16
 #endif
 #define IPW MZ_IPW
+#ifndef MZ_SPW
+// k_step waves per workgroup (they share the staged 4 KB reward tables). Measured at 65,536
+// instances: 1 -> 34.3 us, 2 -> 36.2 us, 4 -> 36.4 us per launch — the saved L2 reads are worth
+// less than the workgroup barrier that the shared table needs.
+#define MZ_SPW 1
+#endif
 #define CAT_WORDS (IPW * 675 / 32 + 2)  // IPW x 675 window bits + funnel-shift slack
 
 namespace {
@@ -315,15 +321,15 @@ __device__ inline void win_band(int r, int c, int tr, int tc, int N, int& geo, i
 // per pass, and the slowest wave sets the launch time).
 __device__ inline void clear_counts(const MzDev& d, size_t e, int N) {
   uint32_t* c = d.cells + e * d.P * d.P;
-  for (int k = threadIdx.x; k < N * d.P; k += WAVE)
+  for (int k = threadIdx.x & (WAVE - 1); k < N * d.P; k += WAVE)
     (void)__hip_atomic_fetch_and(&c[k], MZ_CELL_STATIC, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <bool TOR, bool ENRICH, bool ACT, bool AR>
 __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ act, const MzAct& ap,
                                   const MzOut& o, int e0, uint32_t* cat, double* pen, bool load_pen) {
-  const int lane = threadIdx.x;
-  const int nb = min(IPW, d.B - e0);
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int nb = max(0, min(IPW, d.B - e0));  // 0: a trailing wave of the last workgroup
   const int e = e0 + lane;
   const size_t es = (size_t)e;
   const bool live = lane < nb;
@@ -342,11 +348,17 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
     }
   }
   if (load_pen) {
-    const uint4* pv = reinterpret_cast<const uint4*>(d.pen_visit);
-    const uint4* pi = reinterpret_cast<const uint4*>(d.pen_inv);
-    const uint4 t0 = pv[lane], t1 = pv[lane + WAVE], t2 = pi[lane], t3 = pi[lane + WAVE];
     uint4* pl = reinterpret_cast<uint4*>(pen);
-    pl[lane] = t0; pl[lane + WAVE] = t1; pl[2 * WAVE + lane] = t2; pl[3 * WAVE + lane] = t3;
+    if (MZ_SPW == 1) {
+      const uint4* pv = reinterpret_cast<const uint4*>(d.pen_visit);
+      const uint4* pi = reinterpret_cast<const uint4*>(d.pen_inv);
+      const uint4 t0 = pv[lane], t1 = pv[lane + WAVE], t2 = pi[lane], t3 = pi[lane + WAVE];
+      pl[lane] = t0; pl[lane + WAVE] = t1; pl[2 * WAVE + lane] = t2; pl[3 * WAVE + lane] = t3;
+    } else {  // each wave stages its share of the 4 KB (pen_inv follows pen_visit in one buffer)
+      const uint4* pt = reinterpret_cast<const uint4*>(d.pen_visit);
+      for (int i = (int)(threadIdx.x / WAVE) * WAVE + lane; i < 4 * WAVE; i += MZ_SPW * WAVE)
+        pl[i] = pt[i];
+    }
   }
   if (ENRICH)
     for (int i = lane; i < CAT_WORDS; i += WAVE) cat[i] = 0u;
@@ -526,11 +538,13 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
 // groups-per-wave setting: 46 / 60 / 104 us at 2 / 4 / 8 groups per wave vs 40 us at 1, because
 // the gather phase is latency-bound per wave and needs every group's wave in flight at once.)
 template <bool TOR, bool ENRICH, bool ACT, bool AR>
-__global__ __launch_bounds__(WAVE) void k_step(MzDev d, const int32_t* __restrict__ act, MzAct ap,
-                                               MzOut o) {
-  __shared__ uint32_t cat[CAT_WORDS];
+__global__ __launch_bounds__(WAVE * MZ_SPW) void k_step(MzDev d, const int32_t* __restrict__ act,
+                                                        MzAct ap, MzOut o) {
+  __shared__ uint32_t cat[MZ_SPW][(CAT_WORDS + 3) & ~3];
   __shared__ __align__(16) double pen[512];  // pen_visit[256] | pen_inv[256]
-  step_group<TOR, ENRICH, ACT, AR>(d, act, ap, o, blockIdx.x * IPW, cat, pen, true);
+  const int w = MZ_SPW > 1 ? (int)(threadIdx.x / WAVE) : 0;
+  step_group<TOR, ENRICH, ACT, AR>(d, act, ap, o, (blockIdx.x * MZ_SPW + w) * IPW, cat[w], pen,
+                                   true);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -801,7 +815,7 @@ hipError_t mz_launch_regen(const MzDev& d, const int32_t* idx, const int32_t* co
 template <bool T, bool E>
 void launch_step_te(const MzDev& d, const int32_t* act, const MzAct& a, bool has_act, bool ar,
                     const MzOut& o, hipStream_t s) {
-  dim3 grid((d.B + IPW - 1) / IPW), block(WAVE);
+  dim3 grid((d.B + IPW * MZ_SPW - 1) / (IPW * MZ_SPW)), block(WAVE * MZ_SPW);
   if (has_act) {
     if (ar) hipLaunchKernelGGL((k_step<T, E, true, true>), grid, block, 0, s, d, act, a, o);
     else hipLaunchKernelGGL((k_step<T, E, true, false>), grid, block, 0, s, d, act, a, o);
