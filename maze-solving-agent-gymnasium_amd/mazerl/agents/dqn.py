@@ -31,13 +31,30 @@ from .flat import copy_flat
 from .nets import QNet
 
 
+STACK_ROWS = True  # DDQN on packed windows (GPU): source(s) and source(s') as one pass
+
+
 def q_loss(source, target, state, action, reward, next_state, gamma, double):
     """Loss of optimize_model for a batch: state = (obs6 [B,6], window [B,3,15,15] f32 or packed
-    int32 [B,22] on the GPU — QNet then runs the HIP stem)."""
-    q_sa = source(state).gather(1, action.view(-1, 1))
+    int32 [B,22] on the GPU — QNet then runs the HIP stem). DDQN on the GPU evaluates source(s)
+    and source(s') as ONE pass over the 2B stacked rows (QNet.forward_rows: the stem and GEMMs
+    at twice the rows; the backward reads the first B rows only — the s' rows feed an argmax,
+    which the reference computes under no_grad)."""
+    q_next = None
+    if double and STACK_ROWS and hasattr(source, "forward_rows") and state[1].is_cuda \
+            and state[1].dtype == torch.int32:
+        b = action.shape[0]
+        q = source.forward_rows((torch.cat((state[0], next_state[0])),
+                                 torch.cat((state[1], next_state[1]))), b)
+        q_sa = q[:b].gather(1, action.view(-1, 1))
+        q_next = q[b:].detach()
+    else:
+        q_sa = source(state).gather(1, action.view(-1, 1))
     with torch.no_grad():  # the reference detaches V(s'); no graph is built for it here
         if double:
-            best = source(next_state).max(1)[1].unsqueeze(1)
+            if q_next is None:
+                q_next = source(next_state)
+            best = q_next.max(1)[1].unsqueeze(1)
             v_next = target(next_state).gather(1, best).squeeze(1).detach()
         else:
             v_next = target(next_state).max(1)[0].detach()

@@ -9,6 +9,10 @@ are captured graphs (agents/dqn.py, agents/ppo.py), so on the GPU their Linear l
 same three products explicitly: dX = dY W, dW = dY^T X (GEMMs) and db = dY^T 1 (a GEMV) — the
 same arithmetic class as torch's, and correct under replay (tests/test_graph_linear.py).
 Module and parameter names are nn.Linear's, so state_dicts interchange with the reference's.
+
+`n_grad` (QNet.forward_rows): only the first n_grad rows of the input carry a gradient — the
+rest are rows stacked under them for the forward only (DDQN's source(s') beside source(s)). The
+backward then reads those rows only: dW and db over n_grad rows, dX zero below them.
 """
 import torch
 import torch.nn as nn
@@ -17,24 +21,35 @@ import torch.nn.functional as F
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, n_grad=None):
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
+        ctx.n_grad = n_grad
         return F.linear(x, w, b)
 
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
-        gx = gy @ w if ctx.needs_input_grad[0] else None
-        gw = gy.t() @ x if ctx.needs_input_grad[1] else None
+        n = ctx.n_grad
+        part = n is not None and n < gy.shape[0]
+        gy_n, x_n = (gy[:n], x[:n]) if part else (gy, x)
+        gx = None
+        if ctx.needs_input_grad[0]:
+            if part:
+                gx = torch.empty(x.shape, dtype=gy.dtype, device=gy.device)
+                torch.mm(gy_n, w, out=gx[:n])
+                gx[n:].zero_()
+            else:
+                gx = gy @ w
+        gw = gy_n.t() @ x_n if ctx.needs_input_grad[1] else None
         gb = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            gb = torch.mv(gy.t(), torch.ones(gy.shape[0], dtype=gy.dtype, device=gy.device))
-        return gx, gw, gb
+            gb = torch.mv(gy_n.t(), torch.ones(gy_n.shape[0], dtype=gy.dtype, device=gy.device))
+        return gx, gw, gb, None
 
 
 class GraphSafeLinear(nn.Linear):
-    def forward(self, x):
+    def forward(self, x, n_grad=None):
         if x.is_cuda and x.dim() == 2 and torch.is_grad_enabled() and self.weight.requires_grad:
-            return _LinearFn.apply(x, self.weight, self.bias)
+            return _LinearFn.apply(x, self.weight, self.bias, n_grad)
         return F.linear(x, self.weight, self.bias)

@@ -62,7 +62,19 @@ class QNet(nn.Module):
         return self.fc(torch.cat((fw, s), dim=1))
 
 
-    def _bit_stem(self, s, bits):
+    def forward_rows(self, x, n_grad):
+        """forward() over stacked rows of which only the first n_grad carry a gradient (DDQN's
+        source(s) and source(s') as one pass, agents/dqn.py q_loss): the stem's and the Linear
+        layers' backward read those rows only. Packed windows on the GPU; else forward()."""
+        s, w = x
+        if not (w.dtype == torch.int32 and w.dim() == 2 and w.is_cuda):
+            return self.forward(x)
+        h = self._bit_stem(s, w, n_grad)
+        for m in self.fc:
+            h = m(h, n_grad) if isinstance(m, GraphSafeLinear) else m(h)
+        return h
+
+    def _bit_stem(self, s, bits, n_grad=None):
         from .stem import stem_features
         p = 0.0
         if self.training:
@@ -71,7 +83,7 @@ class QNet(nn.Module):
                     p = float(m.p)
         if p > 0 and (self._stem_rng is None or self._stem_rng.device != bits.device):
             self._stem_rng = torch.zeros(1, dtype=torch.int64, device=bits.device)
-        return stem_features(bits, s, self.conv[0], p, self._stem_rng, self._salt)
+        return stem_features(bits, s, self.conv[0], p, self._stem_rng, self._salt, n_grad)
 
 
 def count_params(net):

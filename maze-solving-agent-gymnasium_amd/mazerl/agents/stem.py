@@ -8,7 +8,8 @@ replay's storage, DeviceReplay.sw) on the GPU runs this instead of Conv2d -> Lea
             flatten order, plus one code byte per feature (pool argmax + gradient class) when
             autograd needs the backward;
   backward  mz_stem_backward: the conv weight / bias gradients (the window is data: no input
-            gradient); the obs6 columns' gradient is not needed either.
+            gradient); the obs6 columns' gradient is not needed either. With `n_grad` only the
+            first n_grad rows carry a gradient (QNet.forward_rows) and only they are read.
 
 Dropout (DDQN, train mode: SURVEY Q13) draws its masks from a counter hash keyed by a device-side
 u64 that is advanced after every call (an in-graph add), so a captured HIP graph replays fresh
@@ -25,7 +26,7 @@ IN_DIM = FEAT + 6
 
 class _StemFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, bits, obs6, weight, bias, p, rng, salt):
+    def forward(ctx, bits, obs6, weight, bias, p, rng, salt, n_grad=None):
         n = bits.shape[0]
         L = N.load()
         feat = torch.empty(n, IN_DIM, dtype=torch.float32, device=bits.device)
@@ -39,14 +40,16 @@ class _StemFn(torch.autograd.Function):
         if need:
             ctx.save_for_backward(bits, code)
         ctx.p = float(p)
+        ctx.n_grad = n if n_grad is None else max(0, min(int(n_grad), n))
         return feat
 
     @staticmethod
     def backward(ctx, gfeat):
         bits, code = ctx.saved_tensors
-        n = bits.shape[0]
+        n = ctx.n_grad  # rows >= n_grad carry no gradient
+        bits, code = bits[:n], code[:n]
         L = N.load()
-        gfeat = gfeat.contiguous()
+        gfeat = gfeat[:n].contiguous()
         dev = gfeat.device
         ws = torch.empty(max(1, L.mz_stem_workspace_floats(n)), dtype=torch.float32, device=dev)
         dw = torch.empty(32, 3, 3, 3, dtype=torch.float32, device=dev)
@@ -54,10 +57,10 @@ class _StemFn(torch.autograd.Function):
         st = torch.cuda.current_stream(dev).cuda_stream
         N.check(L.mz_stem_backward(bits.data_ptr(), code.data_ptr(), gfeat.data_ptr(), IN_DIM, n,
                                    ctx.p, ws.data_ptr(), dw.data_ptr(), db.data_ptr(), st))
-        return None, None, dw, db, None, None, None
+        return None, None, dw, db, None, None, None, None
 
 
-def stem_features(bits, obs6, conv, p, rng, salt):
+def stem_features(bits, obs6, conv, p, rng, salt, n_grad=None):
     """fc.0 input [n, 1574] f32 from packed windows; `conv` is the stem's nn.Conv2d(3, 32, 3)."""
     if conv.weight.shape != (32, 3, 3, 3) or conv.bias is None:
         raise ValueError("the bit stem implements Conv2d(3, 32, 3, padding=1) with bias")
@@ -66,7 +69,7 @@ def stem_features(bits, obs6, conv, p, rng, salt):
     bits = bits.contiguous()
     obs6 = obs6.contiguous().float()
     w = conv.weight.contiguous()
-    feat = _StemFn.apply(bits, obs6, w, conv.bias, p, rng, salt)
+    feat = _StemFn.apply(bits, obs6, w, conv.bias, p, rng, salt, n_grad)
     if p > 0:
         rng.add_(1)  # next call (or graph replay) draws new masks
     return feat
