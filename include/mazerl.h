@@ -249,6 +249,13 @@ int mz_stem_workspace_floats(int32_t n);
  * element for element. n a multiple of 8, x_dev 16-byte aligned. */
 int mz_leaky_relu_bf16(uint16_t* x_dev, int64_t n, float slope, void* stream);
 
+/* Column sums out_dev[c] = sum_{r < n} g_dev[r * ld + c], c < m, f32: the Linear bias gradient
+ * db = dY^T 1 of the learner updates (the bias term of optimize_model's backward,
+ * dqn_agent.py:150 / ppo_agent.py:235). m and ld multiples of 4, buffers 16-byte aligned;
+ * fixed summation order (deterministic). */
+int mz_colsum_f32(const float* g_dev, int32_t n, int32_t m, int32_t ld, float* out_dev,
+                  void* stream);
+
 /* The PPO clipped surrogate with the reference's [b, b] broadcast (ppo_agent.py:188-197, clip
  * 0.3 there): for every column i, part_dev[i] = sum_j min(r a_i, clamp(r, 1-clip, 1+clip) a_i)
  * and dsum_dev[i] = sum_j r * w with r = exp(lp_new[i] - lp_old[j]) and w torch's gradient

@@ -437,6 +437,16 @@ int mz_leaky_relu_bf16(uint16_t* x_dev, int64_t n, float slope, void* stream) {
   return MZ_OK;
 }
 
+int mz_colsum_f32(const float* g_dev, int32_t n, int32_t m, int32_t ld, float* out_dev,
+                  void* stream) {
+  if (!g_dev || !out_dev || n < 0 || m < 0 || ld < m) return fail(MZ_EINVAL, "bad arguments");
+  if ((m & 3) || (ld & 3) || (reinterpret_cast<uintptr_t>(g_dev) & 15) ||
+      (reinterpret_cast<uintptr_t>(out_dev) & 15))
+    return fail(MZ_EALIGN, "colsum_f32 needs m, ld multiples of 4 and 16-byte aligned buffers");
+  MZ_HIP(mz_launch_colsum(g_dev, n, m, ld, out_dev, static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
 int mz_pair_surrogate(const float* lp_new_dev, const float* lp_old_dev, const float* adv_dev,
                       int32_t b, float clip, float* part_dev, float* dsum_dev, void* stream) {
   if (!lp_new_dev || !lp_old_dev || !adv_dev || !part_dev || !dsum_dev || b < 0)

@@ -45,3 +45,4 @@ hipError_t mz_launch_adamw(float* p, float* m, float* v, const float* const* gra
 hipError_t mz_launch_pair_surrogate(const float* lp_new, const float* lp_old, const float* adv,
                                     int b, float clip, float* part, float* dsum, hipStream_t s);
 hipError_t mz_launch_leaky_bf16(uint16_t* x, int64_t n, float slope, hipStream_t s);
+hipError_t mz_launch_colsum(const float* g, int n, int m, int ld, float* out, hipStream_t s);

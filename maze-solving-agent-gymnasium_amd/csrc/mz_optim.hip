@@ -162,3 +162,39 @@ hipError_t mz_launch_pair_surrogate(const float* lp_new, const float* lp_old, co
                      part, dsum);
   return hipGetLastError();
 }
+
+// ------------------------------------------------------------------------------------------
+// Column sums of a row-major f32 matrix g[n][ld] over its first m columns: the Linear bias
+// gradient db = dY^T 1 of the learners' captured updates (agents/linear.py). rocBLAS's GEMV
+// against a ones vector took ~20 us for [2,048 x 1,024] (plus the ones fill); here 64 columns
+// per workgroup, 16-B loads (4 columns per lane), 64 row groups summed in LDS in a fixed order
+// (deterministic).
+static __global__ __launch_bounds__(1024) void k_colsum(const float* __restrict__ g, int n, int m,
+                                                        int ld, float* __restrict__ out) {
+  __shared__ float4 part[64][16];
+  const int cq = threadIdx.x & 15, rg = threadIdx.x >> 4;
+  const int c = blockIdx.x * 64 + cq * 4;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c < m) {
+    for (int r = rg; r < n; r += 64) {
+      const float4 v = *reinterpret_cast<const float4*>(g + (size_t)r * ld + c);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  }
+  part[rg][cq] = s;
+  __syncthreads();
+  if (rg == 0 && c < m) {
+    float4 t = part[0][cq];
+    for (int k = 1; k < 64; ++k) {
+      const float4 u = part[k][cq];
+      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+    }
+    *reinterpret_cast<float4*>(out + c) = t;
+  }
+}
+
+hipError_t mz_launch_colsum(const float* g, int n, int m, int ld, float* out, hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_colsum, dim3((m + 63) / 64), dim3(1024), 0, s, g, n, m, ld, out);
+  return hipGetLastError();
+}

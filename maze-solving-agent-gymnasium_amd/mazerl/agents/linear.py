@@ -12,7 +12,8 @@ Module and parameter names are nn.Linear's, so state_dicts interchange with the 
 
 `n_grad` (QNet.forward_rows): only the first n_grad rows of the input carry a gradient — the
 rest are rows stacked under them for the forward only (DDQN's source(s') beside source(s)). The
-backward then reads those rows only: dW and db over n_grad rows, dX zero below them.
+backward then reads those rows only: dW and db over n_grad rows, dX for them alone. db is one
+HIP column-sum launch (mz_colsum_f32) instead of rocBLAS's GEMV against a ones vector.
 """
 import torch
 import torch.nn as nn
@@ -36,16 +37,31 @@ class _LinearFn(torch.autograd.Function):
         gx = None
         if ctx.needs_input_grad[0]:
             if part:
+                # rows >= n are left unwritten: every consumer below a forward_rows pass (the
+                # activation, this class and the stem with the same n_grad) reads rows < n only
                 gx = torch.empty(x.shape, dtype=gy.dtype, device=gy.device)
                 torch.mm(gy_n, w, out=gx[:n])
-                gx[n:].zero_()
             else:
                 gx = gy @ w
         gw = gy_n.t() @ x_n if ctx.needs_input_grad[1] else None
         gb = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            gb = torch.mv(gy_n.t(), torch.ones(gy_n.shape[0], dtype=gy.dtype, device=gy.device))
+            gb = _bias_grad(gy_n)
         return gx, gw, gb, None
+
+
+def _bias_grad(gy):
+    """db = dY^T 1: one HIP column-sum launch (mz_colsum_f32) for f32 rows whose width is a
+    multiple of 4; else a GEMV against ones."""
+    m = gy.shape[1]
+    if gy.dtype == torch.float32 and m % 4 == 0:
+        from .. import _native as N
+        g = gy if gy.is_contiguous() and gy.data_ptr() % 16 == 0 else gy.contiguous()
+        out = torch.empty(m, dtype=torch.float32, device=gy.device)
+        N.check(N.load().mz_colsum_f32(g.data_ptr(), g.shape[0], m, m, out.data_ptr(),
+                                       torch.cuda.current_stream(gy.device).cuda_stream))
+        return out
+    return torch.mv(gy.t(), torch.ones(gy.shape[0], dtype=gy.dtype, device=gy.device))
 
 
 class GraphSafeLinear(nn.Linear):

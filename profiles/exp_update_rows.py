@@ -51,7 +51,7 @@ def update_us(stack, env):
 def main():
     env = VectorMazeEnv(4, 21, enrich=True, device="cuda", seed=1)
     res = {"update_us_two_passes": [], "update_us_stacked": []}
-    for stack in (False, True, False, True):
+    for stack in ((True,) if "--stacked-only" in sys.argv else (False, True, False, True)):
         res["update_us_stacked" if stack else "update_us_two_passes"].append(update_us(stack, env))
     torch.manual_seed(0)
     net = D.QNet(variant="ddqn").cuda()

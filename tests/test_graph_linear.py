@@ -52,3 +52,22 @@ def test_graph_safe_linear_is_a_linear():
     assert isinstance(b, nn.Linear)
     assert all(torch.equal(x, y) for x, y in zip(a.parameters(), b.parameters()))
     assert list(a.state_dict()) == list(b.state_dict())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,m,ld", [(2048, 1024, 1024), (4096, 512, 512), (37, 4, 4), (1, 64, 68),
+                                    (0, 8, 8), (3000, 1028, 1100)])
+def test_colsum_matches_torch_sum(n, m, ld):
+    """mz_colsum_f32 (the bias gradient of GraphSafeLinear's backward) against torch's f32
+    column sum, including a row pitch wider than the columns summed and an empty matrix."""
+    from mazerl import _native as N
+    g = torch.Generator(device="cuda").manual_seed(n + m)
+    full = torch.randn(max(n, 1), ld, device="cuda", generator=g)
+    out = torch.full((m,), float("nan"), device="cuda")
+    N.check(N.load().mz_colsum_f32(full.data_ptr(), n, m, ld, out.data_ptr(),
+                                   torch.cuda.current_stream().cuda_stream))
+    ref = full[:n, :m].double().sum(0).float()
+    assert torch.allclose(out, ref, rtol=1e-5, atol=1e-4 * max(1.0, n ** 0.5))
+    bad = N.load().mz_colsum_f32(full.data_ptr(), n, 6, ld, out.data_ptr(),
+                                 torch.cuda.current_stream().cuda_stream)
+    assert bad != 0  # m not a multiple of 4
