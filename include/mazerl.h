@@ -256,6 +256,17 @@ int mz_leaky_relu_bf16(uint16_t* x_dev, int64_t n, float slope, void* stream);
 int mz_colsum_f32(const float* g_dev, int32_t n, int32_t m, int32_t ld, float* out_dev,
                   void* stream);
 
+/* One learner update's replay sample (ReplayMemory.sample, replay_memory.py:17-18, drawn as
+ * indices on the device): rows idx_dev[i] (i < b, int64, clamped into [0, capacity)) of the state
+ * arrays obs6 f32 [capacity][6] / window bits int32 [capacity][22] and of the next-state arrays
+ * go to rows i and b + i of out_s6_dev f32 [2b][6] / out_sw_dev int32 [2b][22] (state rows, then
+ * next-state rows), actions int64 and rewards f32 to out_a_dev / out_r_dev [b]. */
+int mz_replay_gather(const int64_t* idx_dev, int32_t b, int64_t capacity,
+                     const float* s6_dev, const int32_t* sw_dev, const int64_t* a_dev,
+                     const float* r_dev, const float* s6n_dev, const int32_t* swn_dev,
+                     float* out_s6_dev,
+                     int32_t* out_sw_dev, int64_t* out_a_dev, float* out_r_dev, void* stream);
+
 /* The PPO clipped surrogate with the reference's [b, b] broadcast (ppo_agent.py:188-197, clip
  * 0.3 there): for every column i, part_dev[i] = sum_j min(r a_i, clamp(r, 1-clip, 1+clip) a_i)
  * and dsum_dev[i] = sum_j r * w with r = exp(lp_new[i] - lp_old[j]) and w torch's gradient

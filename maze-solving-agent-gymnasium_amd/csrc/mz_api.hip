@@ -447,6 +447,22 @@ int mz_colsum_f32(const float* g_dev, int32_t n, int32_t m, int32_t ld, float* o
   return MZ_OK;
 }
 
+int mz_replay_gather(const int64_t* idx_dev, int32_t b, int64_t capacity,
+                     const float* s6_dev, const int32_t* sw_dev, const int64_t* a_dev,
+                     const float* r_dev, const float* s6n_dev, const int32_t* swn_dev,
+                     float* out_s6_dev,
+                     int32_t* out_sw_dev, int64_t* out_a_dev, float* out_r_dev, void* stream) {
+  if (b < 0 || (b > 0 && (!idx_dev || !s6_dev || !sw_dev || !a_dev || !r_dev || !s6n_dev ||
+                          !swn_dev || !out_s6_dev || !out_sw_dev || !out_a_dev || !out_r_dev)))
+    return fail(MZ_EINVAL, "bad arguments");
+  if (b > 0 && capacity < 1) return fail(MZ_EINVAL, "replay capacity %lld", (long long)capacity);
+  MZ_HIP(mz_launch_replay_gather(idx_dev, b, capacity, s6_dev, reinterpret_cast<const uint32_t*>(sw_dev),
+                                 a_dev, r_dev, s6n_dev, reinterpret_cast<const uint32_t*>(swn_dev),
+                                 out_s6_dev, reinterpret_cast<uint32_t*>(out_sw_dev), out_a_dev,
+                                 out_r_dev, static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
 int mz_pair_surrogate(const float* lp_new_dev, const float* lp_old_dev, const float* adv_dev,
                       int32_t b, float clip, float* part_dev, float* dsum_dev, void* stream) {
   if (!lp_new_dev || !lp_old_dev || !adv_dev || !part_dev || !dsum_dev || b < 0)

@@ -46,3 +46,7 @@ hipError_t mz_launch_pair_surrogate(const float* lp_new, const float* lp_old, co
                                     int b, float clip, float* part, float* dsum, hipStream_t s);
 hipError_t mz_launch_leaky_bf16(uint16_t* x, int64_t n, float slope, hipStream_t s);
 hipError_t mz_launch_colsum(const float* g, int n, int m, int ld, float* out, hipStream_t s);
+hipError_t mz_launch_replay_gather(const int64_t* idx, int b, int64_t cap, const float* s6,
+                                   const uint32_t* sw, const int64_t* a, const float* r,
+                                   const float* s6n, const uint32_t* swn, float* o6, uint32_t* ow,
+                                   int64_t* oa, float* orw, hipStream_t s);

@@ -198,3 +198,41 @@ hipError_t mz_launch_colsum(const float* g, int n, int m, int ld, float* out, hi
   hipLaunchKernelGGL(k_colsum, dim3((m + 63) / 64), dim3(1024), 0, s, g, n, m, ld, out);
   return hipGetLastError();
 }
+
+// ------------------------------------------------------------------------------------------
+// The replay sample of one learner update in one launch (DeviceReplay.sample, replay_memory.py
+// :17-18 random.sample): rows idx[i] of the state / next-state arrays gathered into stacked
+// [2b] buffers (state rows 0..b-1, next-state rows b..2b-1: the layout QNet.forward_rows
+// takes), plus the actions and rewards. One 32-bit word per thread, rows in order.
+static __global__ __launch_bounds__(256) void k_replay_gather(
+    const int64_t* __restrict__ idx, int b, int64_t cap, const float* __restrict__ s6,
+    const uint32_t* __restrict__ sw, const int64_t* __restrict__ a, const float* __restrict__ r,
+    const float* __restrict__ s6n, const uint32_t* __restrict__ swn, float* __restrict__ o6,
+    uint32_t* __restrict__ ow, int64_t* __restrict__ oa, float* __restrict__ orw) {
+  constexpr int W = 6 + 22;  // words of one state row (obs6 | window bits)
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)b * (2 * W + 1)) return;
+  const int i = (int)(t / (2 * W + 1)), k = (int)(t - (long)i * (2 * W + 1));
+  const int64_t j = min(max(idx[i], (int64_t)0), cap - 1);  // never outside the ring
+  if (k < 2 * W) {
+    const bool nx = k >= W;
+    const int q = nx ? k - W : k;
+    const int row = nx ? b + i : i;
+    if (q < 6) o6[(size_t)row * 6 + q] = (nx ? s6n : s6)[(size_t)j * 6 + q];
+    else ow[(size_t)row * 22 + (q - 6)] = (nx ? swn : sw)[(size_t)j * 22 + (q - 6)];
+  } else {
+    oa[i] = a[j];
+    orw[i] = r[j];
+  }
+}
+
+hipError_t mz_launch_replay_gather(const int64_t* idx, int b, int64_t cap, const float* s6,
+                                   const uint32_t* sw, const int64_t* a, const float* r,
+                                   const float* s6n, const uint32_t* swn, float* o6, uint32_t* ow,
+                                   int64_t* oa, float* orw, hipStream_t s) {
+  if (b <= 0) return hipSuccess;
+  const long total = (long)b * (2 * (6 + 22) + 1);
+  hipLaunchKernelGGL(k_replay_gather, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, idx,
+                     b, cap, s6, sw, a, r, s6n, swn, o6, ow, oa, orw);
+  return hipGetLastError();
+}

@@ -40,7 +40,8 @@ EXPORTS = ["mz_last_error", "mz_device_count", "mz_create", "mz_destroy", "mz_lo
            "mz_difficulty", "mz_maze_complexity", "mz_maze_metrics", "mz_get_meta", "mz_discounted_returns", "mz_q_front",
            "mz_bank_create", "mz_bank_fill", "mz_bank_use", "mz_bank_consumed",
            "mz_stem_forward", "mz_stem_backward", "mz_stem_workspace_floats", "mz_adamw_flat",
-           "mz_pair_surrogate", "mz_leaky_relu_bf16", "mz_colsum_f32"]
+           "mz_pair_surrogate", "mz_leaky_relu_bf16", "mz_colsum_f32",
+           "mz_replay_gather"]
 
 _lib = None
 
@@ -102,6 +103,7 @@ def load(build_if_missing=True):
     L.mz_stem_workspace_floats.argtypes = [C.c_int32]
     L.mz_leaky_relu_bf16.argtypes = [vp, C.c_int64, C.c_float, vp]
     L.mz_colsum_f32.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, vp, vp]
+    L.mz_replay_gather.argtypes = [vp, C.c_int32, C.c_int64] + [vp] * 11
     L.mz_pair_surrogate.argtypes = [vp, vp, vp, C.c_int32, C.c_float, vp, vp, vp]
     L.mz_adamw_flat.argtypes = [vp, vp, vp, vp, vp, C.c_int32, vp, vp, C.c_double, C.c_double,
                                 C.c_double, C.c_double, C.c_float, C.c_float, C.c_int32, vp]

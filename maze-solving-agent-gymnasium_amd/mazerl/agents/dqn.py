@@ -34,6 +34,17 @@ from .nets import QNet
 STACK_ROWS = True  # DDQN on packed windows (GPU): source(s) and source(s') as one pass
 
 
+def _stacked(x, y):
+    """[x; y] — without a copy when x and y are the two halves of one buffer (the layout
+    DeviceReplay.sample gathers into)."""
+    base = x._base
+    if base is not None and y._base is base and base.is_contiguous() and \
+            base.shape[0] == x.shape[0] + y.shape[0] and x.data_ptr() == base.data_ptr() and \
+            y.data_ptr() == base.data_ptr() + x.numel() * x.element_size():
+        return base
+    return torch.cat((x, y))
+
+
 def q_loss(source, target, state, action, reward, next_state, gamma, double):
     """Loss of optimize_model for a batch: state = (obs6 [B,6], window [B,3,15,15] f32 or packed
     int32 [B,22] on the GPU — QNet then runs the HIP stem). DDQN on the GPU evaluates source(s)
@@ -44,8 +55,8 @@ def q_loss(source, target, state, action, reward, next_state, gamma, double):
     if double and STACK_ROWS and hasattr(source, "forward_rows") and state[1].is_cuda \
             and state[1].dtype == torch.int32:
         b = action.shape[0]
-        q = source.forward_rows((torch.cat((state[0], next_state[0])),
-                                 torch.cat((state[1], next_state[1]))), b)
+        q = source.forward_rows((_stacked(state[0], next_state[0]),
+                                 _stacked(state[1], next_state[1])), b)
         q_sa = q[:b].gather(1, action.view(-1, 1))
         q_next = q[b:].detach()
     else:

@@ -7,8 +7,8 @@ DeviceReplay   — the vectorised learner's ring buffer, resident in HBM as stru
                  obs6 f32[C,6], window bits i32[C,22] (675-bit 3x15x15 window, 88 B instead of
                  the 2,700 B f32 tensor), action i64[C], reward f32[C], and the next-state pair.
                  push() takes a whole vector step at once (index_copy into the ring); sample()
-                 draws uniform indices on the device and expands the windows with the HIP
-                 kernel of libmazerl (mz_expand_window). Sampling is with replacement (the
+                 draws uniform indices on the device and gathers every row in one HIP launch
+                 (mz_replay_gather; or expands f32 windows with mz_expand_window). Sampling is with replacement (the
                  reference's random.sample is without; at C >> batch the difference is a few
                  duplicate rows per batch — documented deviation).
 """
@@ -106,9 +106,28 @@ class DeviceReplay:
         else:
             i = self.sample_indices_static(batch) if static else self.sample_indices(batch)
         if expand is None:
+            if self.device.type == "cuda" and self.s6.shape[1] == 6 and self.sw.shape[1] == 22:
+                return self._gather_stacked(i, batch)
             return ((self.s6.index_select(0, i), self.sw.index_select(0, i)), self.a.index_select(0, i),
                     self.r.index_select(0, i), (self.s6n.index_select(0, i), self.swn.index_select(0, i)))
         bits = torch.cat((self.sw.index_select(0, i), self.swn.index_select(0, i)), 0)
         w = expand(bits)
         return ((self.s6.index_select(0, i), w[:batch]), self.a.index_select(0, i),
                 self.r.index_select(0, i), (self.s6n.index_select(0, i), w[batch:]))
+
+    def _gather_stacked(self, i, batch):
+        """All rows of a sample in one HIP launch (mz_replay_gather): state and next state come
+        back as the two halves of stacked [2 * batch] buffers (views), the layout
+        QNet.forward_rows reads without a copy (agents/dqn.py q_loss)."""
+        from . import _native as N
+        dev = self.device
+        i = i.contiguous()
+        s6 = torch.empty(2 * batch, self.s6.shape[1], dtype=torch.float32, device=dev)
+        sw = torch.empty(2 * batch, self.sw.shape[1], dtype=torch.int32, device=dev)
+        a = torch.empty(batch, dtype=torch.int64, device=dev)
+        r = torch.empty(batch, dtype=torch.float32, device=dev)
+        N.check(N.load().mz_replay_gather(
+            i.data_ptr(), batch, self.capacity, self.s6.data_ptr(), self.sw.data_ptr(),
+            self.a.data_ptr(), self.r.data_ptr(), self.s6n.data_ptr(), self.swn.data_ptr(), s6.data_ptr(),
+            sw.data_ptr(), a.data_ptr(), r.data_ptr(), torch.cuda.current_stream(dev).cuda_stream))
+        return (s6[:batch], sw[:batch]), a, r, (s6[batch:], sw[batch:])

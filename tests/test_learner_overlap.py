@@ -130,3 +130,30 @@ def test_overlapped_updates_on_distinct_rows_match_a_reference_update():
         assert float(A.last_loss) == pytest.approx(float(loss), rel=1e-4), k
     A.finish()
     env.close()
+
+
+def test_replay_gather_matches_index_select():
+    """DeviceReplay.sample on the GPU (one mz_replay_gather launch into stacked [2b] buffers)
+    returns exactly the rows index_select gives, and q_loss reads the stacked buffer in place."""
+    from mazerl.agents.dqn import _stacked
+    from mazerl.replay import DeviceReplay
+    rp = DeviceReplay(1000, "cuda")
+    g = torch.Generator(device="cuda").manual_seed(7)
+    n = 700
+    s6, s6n = (torch.randn(n, 6, device="cuda", generator=g) for _ in range(2))
+    sw, swn = (torch.randint(-2**31, 2**31 - 1, (n, 22), device="cuda", generator=g,
+                             dtype=torch.int32) for _ in range(2))
+    a = torch.randint(0, 4, (n,), device="cuda", generator=g)
+    r = torch.randn(n, device="cuda", generator=g)
+    rp.push(s6, sw, a, r, s6n, swn)
+    rp.push(s6[:500], sw[:500], a[:500], r[:500], s6n[:500], swn[:500])  # wraps the ring
+    for b in (1, 37, 512):
+        rp.idx_static = torch.randint(0, rp.size, (b,), device="cuda", generator=g)
+        (x6, xw), xa, xr, (y6, yw) = rp.sample(b, None, idx_static=True)
+        i = rp.idx_static
+        assert torch.equal(x6, rp.s6[i]) and torch.equal(xw, rp.sw[i])
+        assert torch.equal(y6, rp.s6n[i]) and torch.equal(yw, rp.swn[i])
+        assert torch.equal(xa, rp.a[i]) and torch.equal(xr, rp.r[i])
+        st = _stacked(x6, y6)
+        assert st.data_ptr() == x6.data_ptr() and st.shape == (2 * b, 6)
+        assert torch.equal(_stacked(xw, yw), torch.cat((rp.sw[i], rp.swn[i])))
