@@ -6,7 +6,7 @@ ReplayMemory   — the reference's deque + random.sample memory (lib/replay_memo
 DeviceReplay   — the vectorised learner's ring buffer, resident in HBM as structure-of-arrays:
                  obs6 f32[C,6], window bits i32[C,22] (675-bit 3x15x15 window, 88 B instead of
                  the 2,700 B f32 tensor), action i64[C], reward f32[C], and the next-state pair.
-                 push() takes a whole vector step at once (index_copy into the ring); sample()
+                 push() takes a whole vector step at once (slice copies into the ring); sample()
                  draws uniform indices on the device and gathers every row in one HIP launch
                  (mz_replay_gather; or expands f32 windows with mz_expand_window). Sampling is with replacement (the
                  reference's random.sample is without; at C >> batch the difference is a few
@@ -66,24 +66,28 @@ class DeviceReplay:
         if mask is not None:
             keep = torch.nonzero(mask, as_tuple=False).flatten()
             s6, sw, a, r, s6n, swn = (t.index_select(0, keep) for t in (s6, sw, a, r, s6n, swn))
-        n = s6.shape[0]
+        n = a.shape[0]
         if n == 0:
             return
         if n > self.capacity:
             s6, sw, a, r, s6n, swn = (t[-self.capacity:] for t in (s6, sw, a, r, s6n, swn))
             n = self.capacity
-        idx = (torch.arange(n, device=self.device) + self.ptr) % self.capacity
-        self.s6.index_copy_(0, idx, s6)
-        self.sw.index_copy_(0, idx, sw)
-        self.a.index_copy_(0, idx, a.to(torch.int64))
-        self.r.index_copy_(0, idx, r.to(torch.float32))
-        self.s6n.index_copy_(0, idx, s6n)
-        self.swn.index_copy_(0, idx, swn)
+        self._write(((self.s6, s6), (self.sw, sw), (self.a, a), (self.r, r), (self.s6n, s6n),
+                     (self.swn, swn)), n)
         self.ptr = (self.ptr + n) % self.capacity
         size = min(self.size + n, self.capacity)
         if size != self.size:
             self.size_dev.fill_(float(size))
         self.size = size
+
+    def _write(self, pairs, n):
+        """Ring rows ptr .. ptr + n - 1 (one or two contiguous slices) <- the n source rows, one
+        copy kernel per array and slice (dtype conversion included)."""
+        k = min(n, self.capacity - self.ptr)
+        for dst, src in pairs:
+            dst[self.ptr:self.ptr + k].copy_(src[:k])
+            if k < n:
+                dst[:n - k].copy_(src[k:n])
 
     def sample_indices(self, batch):
         return torch.randint(0, self.size, (batch,), device=self.device, generator=self._gen)

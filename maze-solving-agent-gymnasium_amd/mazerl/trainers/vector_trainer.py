@@ -47,8 +47,7 @@ class VectorOffPolicyTrainer:
     def vector_step(self):
         env, L = self.env, self.learner
         greedy = L.greedy(env.obs6, env.window, env.window_bits)
-        s6 = env.obs6.clone()
-        sw = env.window_bits.clone()
+        s6, sw = env.obs6.clone(), env.window_bits.clone()
         env.step_act(eps=L.epsilon(), greedy=greedy, seed=self.seed, counter=self.counter)
         self.counter += 1
         L.replay.push(s6, sw, env.actions, env.reward, env.obs6, env.window_bits)
