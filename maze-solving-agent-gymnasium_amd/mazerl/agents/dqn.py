@@ -446,6 +446,10 @@ class VectorDQNLearner:
                     ar.unpack(self.source)
                     learner_step(self.source, self.opt)
                 self._graph = (ga, gb)
+            if self.overlap:
+                # the capture drew no indices (it does not run): the first replay must not reuse
+                # the last eager warm-up's rows, which that update already applied
+                self.replay.idx_static.copy_(self.replay.sample_indices(self.batch_size))
         self._graph[0].replay()
         if ar is not None:
             ar.reduce()

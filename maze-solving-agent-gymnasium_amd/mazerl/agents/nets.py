@@ -65,10 +65,21 @@ class QNet(nn.Module):
     def forward_rows(self, x, n_grad):
         """forward() over stacked rows of which only the first n_grad carry a gradient (DDQN's
         source(s) and source(s') as one pass, agents/dqn.py q_loss): the stem's and the Linear
-        layers' backward read those rows only. Packed windows on the GPU; else forward()."""
+        layers' backward read those rows only. Packed windows on the GPU; else forward().
+
+        Contract: the input gradients of this pass hold rows < n_grad only (rows >= n_grad are
+        left unwritten, agents/linear.py), so every module between the stem and the output must
+        be a row-limited GraphSafeLinear or a row-wise activation; nothing may read the whole
+        gradient tensor (hooks, anomaly mode, gradcheck)."""
         s, w = x
         if not (w.dtype == torch.int32 and w.dim() == 2 and w.is_cuda):
             return self.forward(x)
+        for m in self.fc:
+            if not isinstance(m, (GraphSafeLinear, nn.LeakyReLU, nn.ReLU)):
+                raise TypeError(f"forward_rows: {type(m).__name__} would read gradient rows >= n_grad")
+        if torch.is_anomaly_enabled():
+            raise RuntimeError("forward_rows leaves gradient rows >= n_grad unwritten; "
+                               "anomaly mode would read them")
         h = self._bit_stem(s, w, n_grad)
         for m in self.fc:
             h = m(h, n_grad) if isinstance(m, GraphSafeLinear) else m(h)

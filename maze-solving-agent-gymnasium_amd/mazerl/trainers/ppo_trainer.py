@@ -133,8 +133,17 @@ class VectorPPOTrainer:
         win = w if self.bit_stem else self.env.expand_window(w)  # packed bits -> HIP stem
         coef = 1e-2 - (1e-2 - 5e-4) * frac  # ppo_trainer.py:73
         keep = (adv == adv) & (ret == ret)  # a 1-step episode has an undefined std (NaN): drop
-        if not bool(keep.all()):
-            s6, win, a, lp, adv, ret = (x[keep] for x in (s6, win, a, lp, adv, ret))
+        rows = torch.nonzero(keep).flatten()
+        n_keep = torch.tensor([rows.numel()], dtype=torch.int64, device=self.device)
+        if self.allreduce is not None:
+            # every rank must run the same minibatch schedule (same collective count and the
+            # same graph-replay / eager split): all keep the smallest kept count
+            import torch.distributed as dist
+            dist.all_reduce(n_keep, op=dist.ReduceOp.MIN)
+        n_keep = int(n_keep.item())
+        if n_keep < P:
+            rows = rows[:n_keep]
+            s6, win, a, lp, adv, ret = (x.index_select(0, rows) for x in (s6, win, a, lp, adv, ret))
         optimize_model(self.net, self.opt, (s6, win), a[:, None], lp[:, None], adv, ret, coef,
                        self.batch_size, self.ppo_steps, allreduce=self.allreduce, graph=self.graph)
         if self.fused is not None:

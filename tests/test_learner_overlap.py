@@ -10,6 +10,7 @@ documented lag of the overlapped schedule), and the sampled rows must avoid the 
 the next push overwrites."""
 import pytest
 import torch
+import torch.nn.functional as F
 
 from test_learner_graph import _fill
 
@@ -191,3 +192,50 @@ def test_stacked_ddqn_pass_matches_two_passes():
     assert out[True][0] == pytest.approx(out[False][0], rel=1e-5)
     for g1, g0 in zip(out[True][1], out[False][1]):
         assert torch.allclose(g1, g0, rtol=1e-4, atol=1e-5 * float(g0.abs().max()) + 1e-12)
+
+
+def test_stacked_ddqn_pass_train_mode_matches_torch_with_same_masks():
+    """The stacked pass in TRAIN mode (Dropout(0.2) on, as DDQN always runs: SURVEY Q13): the
+    forward over [s; s'] and the row-limited backward against the torch pipeline (Conv2d ->
+    LeakyReLU -> dropout with the kernel's masks regenerated in numpy -> MaxPool2d -> fc) over
+    the same 2b rows, the gradient taken through the first b rows only. f32 tolerances as in
+    test_stem.py."""
+    import copy
+
+    from test_stem import _bits, _close, _masks, _torch_stem, _window
+
+    from mazerl.agents.nets import QNet
+    torch.manual_seed(6)
+    net = QNet(variant="ddqn").cuda().train()
+    ref = copy.deepcopy(net)
+    b = 384
+    bits = _bits(2 * b, 21)
+    win = _window(bits).cuda()
+    bits = bits.cuda()
+    s6 = torch.randn(2 * b, 6).cuda()
+    key = 0x5151_0000_2222
+    net._stem_rng = torch.tensor([key], dtype=torch.int64, device="cuda")
+    q = net.forward_rows((s6, bits), b)
+    assert int(net._stem_rng.item()) == key + 1
+    keep = torch.from_numpy(_masks(2 * b, key, net._salt, 0.2)).cuda()
+    q_ref = ref.fc(_torch_stem(ref, s6, win, keep, 0.2))
+    assert _close(q, q_ref.detach(), 1e-5, 1e-6)
+    R = torch.randn(b, 4).cuda()
+    # Rows holding a pool window whose two largest (kept, non-zero) activations lie within f32
+    # reassociation noise of each other get zero weight: there the argmax — and so which conv
+    # position receives the gradient — depends on the conv's summation order (MFMA chain here,
+    # MIOpen there), not on the row limiting under test.
+    with torch.no_grad():
+        cw = ref.conv[0]
+        a64 = F.conv2d(win.double(), cw.weight.double(), cw.bias.double(), padding=1)
+        v = F.leaky_relu(a64, 0.01) * keep.double() * 1.25
+        v = v[:, :, :14, :14].reshape(2 * b, 32, 7, 2, 7, 2).permute(0, 1, 2, 4, 3, 5)
+        top = v.reshape(2 * b, 32, 7, 7, 4).topk(2, dim=-1).values
+        near = (top[..., 0] != 0) & ((top[..., 0] - top[..., 1]) <= 1e-5 * top[..., 0].abs())
+        bad = near.flatten(1).any(1)[:b]
+    assert int(bad.sum()) < b // 8
+    R[bad] = 0
+    g = torch.autograd.grad((q[:b] * R).sum(), list(net.parameters()))
+    g_ref = torch.autograd.grad((q_ref[:b] * R).sum(), list(ref.parameters()))
+    for (name, _), a, c in zip(net.named_parameters(), g, g_ref):
+        assert _close(a, c, 1e-4, 1e-5), name
