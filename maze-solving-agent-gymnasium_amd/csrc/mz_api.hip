@@ -21,7 +21,7 @@ struct MzBankStore {  // two banks x the enabled algorithms x K slots (mz_bank_*
   int K = 0, dim = 0, nA = 0;
   uint32_t amask = 0;
   uint32_t* cells = nullptr;   // [2][nA][K][P*P]
-  uint32_t* planes = nullptr;  // [2][nA][K][P*PW]
+  uint32_t* planes = nullptr;  // [2][nA][K][PW]
   uint32_t* meta0 = nullptr;   // [2][nA][K]
   uint32_t* meta1 = nullptr;
   int* heads = nullptr;        // [2][3] consumed slots per algorithm id
@@ -142,11 +142,11 @@ int mz_create(const mz_config* cfg, mz_handle** out) {
   d.P = cfg->max_dim;
   d.toroidal = cfg->toroidal != 0;
   d.enrich = cfg->enrich != 0;
-  d.NW = (d.P + 31) / 32;
-  d.PW = 2 * d.NW;
+  d.NS = mz_nstrips(d.P);
+  d.PW = 2 * d.NS * d.P;
   const size_t B = (size_t)d.B, P = (size_t)d.P;
   int rc;
-  if ((rc = alloc(h, &d.cells, B * P * P)) || (rc = alloc(h, &d.planes, B * P * (size_t)d.PW + 16)) ||
+  if ((rc = alloc(h, &d.cells, B * P * P)) || (rc = alloc(h, &d.planes, B * (size_t)d.PW + 16)) ||
       (rc = alloc(h, &d.meta0, B)) ||
       (rc = alloc(h, &d.meta1, B)) || (rc = alloc(h, &d.posw, B)) || (rc = alloc(h, &d.stw, B)) ||
       (rc = alloc(h, &d.curw, B)) || (rc = alloc(h, &d.algo, B)) || (rc = alloc(h, &d.last_term, B)) ||
@@ -487,7 +487,7 @@ int mz_bank_create(mz_handle* h, int32_t slots, int32_t dim, uint32_t algo_mask)
   const MzDev& d = h->d;
   const int nA = __builtin_popcount(algo_mask);
   const size_t S = 2 * (size_t)nA * slots, K = (size_t)slots;
-  if ((rc = alloc(h, &b.cells, S * d.P * d.P)) || (rc = alloc(h, &b.planes, S * d.P * d.PW)) ||
+  if ((rc = alloc(h, &b.cells, S * d.P * d.P)) || (rc = alloc(h, &b.planes, S * d.PW)) ||
       (rc = alloc(h, &b.meta0, S)) || (rc = alloc(h, &b.meta1, S)) || (rc = alloc(h, &b.heads, 6)) ||
       (rc = alloc(h, &b.s_posw, K)) ||
       (rc = alloc(h, &b.s_stw, K)) || (rc = alloc(h, &b.s_curw, K)) || (rc = alloc(h, &b.s_last, K)) ||
@@ -516,7 +516,7 @@ int mz_bank_fill(mz_handle* h, int32_t bank, uint64_t seed, void* stream) {
     MzDev bd = h->d;  // same pitch / flags; instance arrays = this block's slots + scratch
     bd.B = b.K;
     bd.cells = b.cells + blk * P * P;
-    bd.planes = b.planes + blk * P * h->d.PW;
+    bd.planes = b.planes + blk * h->d.PW;
     bd.meta0 = b.meta0 + blk;
     bd.meta1 = b.meta1 + blk;
     bd.posw = b.s_posw;
@@ -549,7 +549,7 @@ int mz_bank_use(mz_handle* h, int32_t bank) {
   d.bk_dim = b.dim;
   d.bk_amask = b.amask;
   d.bk_cells = b.cells + blk * P * P;
-  d.bk_planes = b.planes + blk * P * d.PW;
+  d.bk_planes = b.planes + blk * d.PW;
   d.bk_meta0 = b.meta0 + blk;
   d.bk_meta1 = b.meta1 + blk;
   d.bk_head = b.heads + 3 * bank;

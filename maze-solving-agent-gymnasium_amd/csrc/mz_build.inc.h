@@ -388,17 +388,20 @@ __device__ void mz_build_one(const MzDev& d, int e, bool tor, bool generate, int
     const bool open = r < N && c < N && L.g[r * N + c] != 0;
     d.cells[es * P * P + p] = open ? mz_cell_word(L, N, tor, r, c, gr, gc) : 0u;
   }
-  // open / visited bit-plane rows, interleaved word pairs; visited = {start} (reset)
-  for (int R = lane; R < P; R += 64) {
-    uint2* row = reinterpret_cast<uint2*>(d.planes + (es * P + R) * d.PW);
-    for (int k = 0; k < d.NW; ++k) {
-      uint32_t o = 0u, v = 0u;
-      if (R < N)
-        for (int c = 32 * k; c < N && c < 32 * k + 32; ++c)
-          if (L.g[R * N + c] != 0) o |= 1u << (c & 31);
-      if (R == sr && (sc >> 5) == k) v = 1u << (sc & 31);
-      row[k] = make_uint2(o, v);
+  // open / visited plane strips (mz_common.h); visited = {start} (reset)
+  for (int k = lane; k < d.NS * P; k += 64) {
+    const int st = k / P, R = k - st * P;
+    uint32_t o = 0u, v = 0u;
+    if (R < N) {
+      for (int j = 0; j < 32; ++j) {
+        int c = MZ_STRIP_STRIDE * st + j;
+        if (tor) c = mz_wrap(c, N);
+        else if (c >= N) break;
+        if (L.g[R * N + c] != 0) o |= 1u << j;
+      }
+      if (R == sr) v = mz_strip_colmask(st, sc, N, tor);
     }
+    *mz_strip_row(d, es, st, R) = make_uint2(o, v);
   }
   if (lane == 0) {
     // set_max_steps: ceil((((H-1)*(W-1)) - 1) * (len / CE)), CE = (H-1)*((W-1)//2) - 1

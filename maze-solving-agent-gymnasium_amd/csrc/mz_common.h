@@ -13,10 +13,16 @@
 //                        rides in the same word, so one gather serves both; it counts only when
 //                        its tag equals the instance's episode tag (stw bits 24-26), so a reset
 //                        bumps the tag instead of clearing the maze (a full clear every 8th reset).
-//   planes u32 [B][P][PW] per row, interleaved (open, visited) word pairs for columns 32k..32k+31,
-//                        PW = 2 * ceil(P / 32) (24 B rows at P = 81): [o0 v0 o1 v1 o2 v2];
+//   planes u32 [B][NS][P][2]  open / visited bit planes in column STRIPS: strip s holds the 32
+//                        columns 18s .. 18s + 31 (torus: (18s + j) mod N; euclidean columns >= N
+//                        are 0), one (open, visited) u32 pair per row, NS = ceil(P / 18). Any
+//                        15-column window [c0, c0 + 14] lies in strip c0 / 18 at bit offset
+//                        c0 mod 18, so a window is 15 consecutive 8-B rows of one strip (120 B,
+//                        about two 128-B lines; the row-major pair layout this replaced read a
+//                        16-row x 24-B band, about four). A cell sits in up to two strips
+//                        (euclidean), so its visited bit is set in each.
 //                        visited = the reference's non_visited plane inverted
-//                        (base_maze_env.py:40-41,184). A window row needs 2 x 8 B loads.
+//                        (base_maze_env.py:40-41,184).
 //   SoA per instance (coalesced u32 each):
 //     meta0 = N | N<<8 (H,W) | sr<<16 | sc<<24     meta1 = gr | gc<<8 | max_steps<<16
 //     posw  = r | c<<8 | nm<<16 (min(len(visited_cell),2)) | last_action<<18 | done<<20
@@ -43,7 +49,7 @@ __host__ __device__ inline int mz_cell_count(uint32_t w, uint32_t tag) {
 
 struct MzDev {
   int B, P, toroidal, enrich;
-  int NW, PW;               // plane words per row per plane (ceil(P/32)) and row pitch (2*NW)
+  int NS, PW;               // plane strips (ceil(P/18)) and plane words per instance (NS*P*2)
   uint32_t* cells;
   uint32_t* planes;
   uint32_t* meta0;
@@ -64,7 +70,7 @@ struct MzDev {
   int bk_dim;               // maze size of the bank's mazes
   uint32_t bk_amask;        // algorithms the bank holds (bit a)
   const uint32_t* bk_cells; // [slots][P*P]
-  const uint32_t* bk_planes;// [slots][P*PW]
+  const uint32_t* bk_planes;// [slots][PW]
   const uint32_t* bk_meta0; // [slots]
   const uint32_t* bk_meta1; // [slots]
   int* bk_head;             // [3]
@@ -145,6 +151,25 @@ __device__ inline int mz_win_start(int p, int N) {
   if (p - 7 >= 0 && p + 7 < N) return p - 7;
   if (p - 7 < 0) return 0;
   return N - 15;
+}
+
+// ---- plane strips (see the layout above)
+#define MZ_STRIP_STRIDE 18
+__host__ __device__ inline int mz_nstrips(int P) { return (P + MZ_STRIP_STRIDE - 1) / MZ_STRIP_STRIDE; }
+
+// the (open, visited) pair of row R of strip s of instance e
+__device__ inline uint2* mz_strip_row(const MzDev& d, size_t e, int s, int R) {
+  return reinterpret_cast<uint2*>(d.planes) + ((e * d.NS + s) * d.P + R);
+}
+
+// bits j of strip s that hold column col (euclidean: at most one; torus: j = col - 18s mod N,
+// + N, + 2N, ... < 32 — a column repeats inside a strip when N < 32)
+__device__ inline uint32_t mz_strip_colmask(int s, int col, int N, bool tor) {
+  const int j0 = col - MZ_STRIP_STRIDE * s;
+  if (!tor) return (j0 >= 0 && j0 < 32) ? (1u << j0) : 0u;
+  uint32_t m = 0u;
+  for (int j = mz_wrap(j0, N); j < 32; j += N) m |= 1u << j;
+  return m;
 }
 
 #define MZ_ALGO_RPRIM_DEV 0

@@ -41,26 +41,6 @@
 
 namespace {
 
-__device__ inline uint32_t ext15(uint32_t lo, uint32_t hi, int sh) {
-  uint64_t v = ((uint64_t)hi << 32) | lo;
-  return (uint32_t)(v >> sh) & 0x7FFFu;
-}
-
-// 15 bits starting at column s of a 128-bit row, wrapping at N (toroidal rows).
-__device__ inline uint32_t row15_wrap(const uint32_t w[4], int s, int N) {
-  if (N >= 15) {
-    uint32_t a = ext15(w[s >> 5], (s >> 5) < 3 ? w[(s >> 5) + 1] : 0u, s & 31);
-    if (s + 15 <= N) return a;
-    int k = N - s;  // bits taken before the wrap
-    uint32_t b = ext15(w[0], w[1], 0);
-    return (a & ((1u << k) - 1u)) | ((b << k) & 0x7FFFu);
-  }
-  uint32_t v = 0;
-  for (int j = 0, col = s; j < 15; ++j, col = (col + 1 == N) ? 0 : col + 1)
-    v |= ((w[col >> 5] >> (col & 31)) & 1u) << j;
-  return v;
-}
-
 // bits j in [0,15) with (C0 + j) mod N == col
 __device__ inline uint32_t wrap_colmask(int col, int C0, int N) {
   uint32_t m = 0;
@@ -68,47 +48,72 @@ __device__ inline uint32_t wrap_colmask(int col, int C0, int N) {
   return m;
 }
 
-// Window row i (0..14) of instance e at (r,c): the three 15-bit channel rows of get_mask_tensor
-// (maze_handler.py:82-99): [maze==0, maze==1, non_visited]; the goal (2) is 0 in channels 0 and
-// 1; non_visited = open & ~visited. (vr,vc): cell to count as visited although its plane bit may
-// not be stored yet (just entered, base_maze_env.py:184 precedes _get_obs); vr < 0 = none.
-// vso: at reset the visited plane is {start} (:148-149) — used without reading it back.
-__device__ inline void win_row(const MzDev& d, size_t e, bool tor, int N, int r, int c, int gr,
-                               int gc, int vr, int vc, bool vso, int i, uint32_t& ch0,
-                               uint32_t& ch1, uint32_t& ch2) {
-  uint32_t open15, vis15, gmask = 0;
-  if (!tor) {
-    const int r0 = mz_win_start(r, N), c0 = mz_win_start(c, N);  // len(maze) for both axes
-    const int R = r0 + i;
-    const uint32_t* row = d.planes + (e * d.P + R) * d.PW;
-    const int w0 = c0 >> 5, sh = c0 & 31;
-    const uint2 a = *reinterpret_cast<const uint2*>(row + 2 * w0);      // (open, visited) w0
-    const uint2 b = *reinterpret_cast<const uint2*>(row + 2 * w0 + 2);  // (open, visited) w0+1
-    open15 = ext15(a.x, b.x, sh);
-    vis15 = vso ? ((R == vr) ? (1u << (vc - c0)) : 0u) : ext15(a.y, b.y, sh);
-    if (!vso && R == vr) vis15 |= 1u << (vc - c0);
-    if (R == gr && gc >= c0 && gc < c0 + 15) gmask = 1u << (gc - c0);
+// Window of an agent at (r, c) (extract_submaze / extract_submaze_toroid, maze_handler.py:4-80):
+// first row R0 and first column C0 = 18 st + off, packed with N as
+//   geo = R0 | st << 7 | off << 10 | N << 15
+// — the window is rows R0 .. R0 + 14 (torus: mod N) of plane strip st, bits off .. off + 14.
+template <bool TOR>
+__device__ inline int win_geo(int r, int c, int N) {
+  int R0, C0;
+  if (!TOR) { R0 = mz_win_start(r, N); C0 = mz_win_start(c, N); }
+  else { R0 = mz_wrapn(r - 7, N); C0 = mz_wrapn(c - 7, N); }
+  const int st = C0 / MZ_STRIP_STRIDE;
+  return R0 | (st << 7) | ((C0 - MZ_STRIP_STRIDE * st) << 10) | (N << 15);
+}
+__device__ inline int geo_st(int g) { return (g >> 7) & 7; }
+__device__ inline int geo_n(int g) { return (g >> 15) & 0x7F; }
+// grid row of window row i
+template <bool TOR>
+__device__ inline int geo_row(int g, int i) {
+  return TOR ? mz_wrapn((g & 0x7F) + i, geo_n(g)) : (g & 0x7F) + i;
+}
+
+// Window row i (grid row R) from its strip pair pr = (open, visited): the three 15-bit channel
+// rows of get_mask_tensor (maze_handler.py:82-99): [maze==0, maze==1, non_visited]; the goal (2)
+// is 0 in channels 0 and 1; non_visited = open & ~visited. (vr, vc): a cell counted as visited
+// although its plane bit is not stored yet (just entered — base_maze_env.py:184 precedes
+// _get_obs — or the reset start); vr < 0 = none. vso: the visited plane is {start} only (reset,
+// :148-149) and the stored bits are not read. The agent's own cell always lies in its window.
+template <bool TOR>
+__device__ inline void win_row_bits(uint2 pr, int g, int R, int gr, int gc, int vr, int vc,
+                                    bool vso, uint32_t& ch0, uint32_t& ch1, uint32_t& ch2) {
+  const int off = (g >> 10) & 31, N = geo_n(g);
+  const int C0 = MZ_STRIP_STRIDE * geo_st(g) + off;
+  const uint32_t open15 = (pr.x >> off) & 0x7FFFu;
+  uint32_t vis15 = vso ? 0u : (pr.y >> off) & 0x7FFFu, gmask = 0u;
+  if (!TOR) {
+    if (R == vr) vis15 |= 1u << (vc - C0);
+    if (R == gr && gc >= C0 && gc < C0 + 15) gmask = 1u << (gc - C0);
   } else {
-    const int R = mz_wrapn(r + i - 7, N), C0 = mz_wrapn(c - 7, N);
-    const uint2* row2 = reinterpret_cast<const uint2*>(d.planes + (e * d.P + R) * d.PW);
-    uint32_t ow[4] = {0u, 0u, 0u, 0u}, vw[4] = {0u, 0u, 0u, 0u};
-    for (int k = 0; k < d.NW; ++k) {
-      const uint2 pr = row2[k];
-      ow[k] = pr.x;
-      vw[k] = pr.y;
-    }
-    open15 = row15_wrap(ow, C0, N);
-    if (vso) {
-      vis15 = (R == vr) ? wrap_colmask(vc, C0, N) : 0u;
-    } else {
-      vis15 = row15_wrap(vw, C0, N);
-      if (R == vr) vis15 |= wrap_colmask(vc, C0, N);
-    }
+    if (R == vr) vis15 |= wrap_colmask(vc, C0, N);
     if (R == gr) gmask = wrap_colmask(gc, C0, N);
   }
   ch0 = ~open15 & 0x7FFFu;
   ch1 = open15 & ~gmask;
   ch2 = open15 & ~vis15;
+}
+
+// visited_cell.append (base_maze_env.py:196) in the planes: the cell's bit in every strip that
+// holds its column (euclidean: one or two; torus: any strip, repeated when N < 32). No-return
+// atomics: several lanes may touch one word of an instance only through this, one at a time.
+template <bool TOR>
+__device__ inline void mark_visited(const MzDev& d, size_t e, int R, int col, int N) {
+  const int lo = TOR ? 0 : max(0, (col - 31 + MZ_STRIP_STRIDE - 1) / MZ_STRIP_STRIDE);
+  const int hi = TOR ? d.NS - 1 : min(d.NS - 1, col / MZ_STRIP_STRIDE);
+  for (int st = lo; st <= hi; ++st) {
+    const uint32_t m = mz_strip_colmask(st, col, N, TOR);
+    if (m) atomicOr(reinterpret_cast<uint32_t*>(mz_strip_row(d, e, st, R)) + 1, m);
+  }
+}
+
+// visited plane of instance e = {(sr, sc)} (reset; rows >= N hold no open cell): one wave
+__device__ inline void reset_visited(const MzDev& d, size_t e, int N, int sr, int sc, bool tor,
+                                     int lane) {
+  for (int k = lane; k < N * d.NS; k += WAVE) {
+    const int st = k / N, R = k - st * N;
+    reinterpret_cast<uint32_t*>(mz_strip_row(d, e, st, R))[1] =
+        R == sr ? mz_strip_colmask(st, sc, N, tor) : 0u;
+  }
 }
 
 __device__ inline void cat_put(uint32_t* cat, int o, uint32_t v) {
@@ -220,97 +225,22 @@ __device__ inline int act_sample(const MzAct& ap, int e, uint32_t pw, uint32_t c
                   cw, tor);
 }
 
-// Plane words of one row: euclidean = the (open, visited) pairs of words W0 and W0 + 1
-// (columns 32*W0 .. 32*W0 + 63); toroidal = the whole row (NW <= 4 pairs).
-template <bool TOR>
-__device__ inline void load_row(const MzDev& d, size_t e, int R, int W0, uint32_t* w) {
-  const uint2* row = reinterpret_cast<const uint2*>(d.planes + (e * d.P + R) * d.PW);
-  if (!TOR) {
-    const uint2 a = row[W0], b = row[W0 + 1];
-    w[0] = a.x; w[1] = a.y; w[2] = b.x; w[3] = b.y;
-  } else {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      uint2 a = make_uint2(0u, 0u);
-      if (k < d.NW) a = row[k];
-      w[2 * k] = a.x;
-      w[2 * k + 1] = a.y;
-    }
-  }
-}
-
-// Window row R (first column C0) from its plane words: the three 15-bit channel rows of
-// get_mask_tensor (maze_handler.py:82-99) as in win_row above. Euclidean words start at column
-// 32*W0 <= C0 (C0 - 32*W0 <= 48).
-template <bool TOR>
-__device__ inline void win_bits(const uint32_t* w, int N, int R, int C0, int W0, int gr, int gc,
-                                int vr, int vc, bool vso, uint32_t& ch0, uint32_t& ch1,
-                                uint32_t& ch2) {
-  uint32_t open15, vis15, gmask = 0;
-  if (!TOR) {
-    const int sh = C0 - 32 * W0;
-    open15 = ext15(w[0], w[2], sh);
-    vis15 = vso ? 0u : ext15(w[1], w[3], sh);
-    if (R == vr) vis15 |= 1u << (vc - C0);
-    if (R == gr && gc >= C0 && gc < C0 + 15) gmask = 1u << (gc - C0);
-  } else {
-    const uint32_t ow[4] = {w[0], w[2], w[4], w[6]}, vw[4] = {w[1], w[3], w[5], w[7]};
-    open15 = row15_wrap(ow, C0, N);
-    vis15 = vso ? 0u : row15_wrap(vw, C0, N);
-    if (R == vr) vis15 |= wrap_colmask(vc, C0, N);
-    if (R == gr) gmask = wrap_colmask(gc, C0, N);
-  }
-  ch0 = ~open15 & 0x7FFFu;
-  ch1 = open15 & ~gmask;
-  ch2 = open15 & ~vis15;
-}
-
-// Rows and columns of the two windows a step can end in — around (r, c) if the agent stays,
-// around (tr, tc) if it moves (tr, tc one step away, or equal) — as one 16-row band:
-//   geo = R0 | W0 << 8 | offA << 12 | offB << 13 | vert << 14 | N << 16   (window X's row i is
-//         band row offX + i; band row k is grid row R0 + k, wrapped on the torus; vert = the
-//         band needs its 16th row)
-//   col = C0A | C0B << 8                                                   (first columns)
-template <bool TOR>
-__device__ inline void win_band(int r, int c, int tr, int tc, int N, int& geo, int& col) {
-  int R0, offA = 0, offB = 0, C0A, C0B, W0 = 0;
-  if (!TOR) {
-    const int sA = mz_win_start(r, N), sB = mz_win_start(tr, N);
-    R0 = min(sA, sB);
-    offA = sA - R0;
-    offB = sB - R0;
-    C0A = mz_win_start(c, N);
-    C0B = mz_win_start(tc, N);
-    W0 = min(C0A, C0B) >> 5;
-  } else {
-    const int rA = mz_wrapn(r - 7, N);
-    R0 = rA;
-    if (tr != r) {
-      if (tr == mz_wrapn(r + 1, N)) offB = 1;
-      else { R0 = mz_wrapn(rA - 1, N); offA = 1; }
-    }
-    C0A = mz_wrapn(c - 7, N);
-    C0B = mz_wrapn(tc - 7, N);
-  }
-  geo = R0 | (W0 << 8) | (offA << 12) | (offB << 13) | ((offA | offB) << 14) | (N << 16);
-  col = C0A | (C0B << 8);
-}
-
-#define WIN_IT (IPW * 16 / WAVE)  // band rows per lane: lane l of pass it = instance 4*it + l/16, row l%16
+#define WIN_IT (IPW * 16 / WAVE)  // window rows per lane: lane l of pass it = instance 4*it + l/16, row l%16
 
 // ------------------------------------------------------------------------------------------
 // One vector step, IPW instances per 64-lane wave, with two dependent global round trips:
 //   level 1  per-instance state (5 coalesced u32 + eps/greedy or the given action), and the
-//            reward tables into LDS;
-//   level 2  target-cell word and its visit count (one lane per instance), and the 16-row
-//            plane band that holds BOTH windows the step can end in (agent stays / agent
-//            moves; one lane per band row, 16-B loads) — the move itself is decided by the
-//            target cell word that arrives in the same round trip;
+//            reward tables into LDS; the action, and whether the agent moves: the target is open
+//            iff the current cell word's open-neighbour bit for the action is set (the same
+//            predicate maze[(r+dr) mod N][(c+dc) mod N] != 0, mz_cell_word) — so the window the
+//            step ends in is known before any gather;
+//   level 2  the target cell word and its visit count (one lane per moving / resetting
+//            instance), and that window's 15 rows from its plane strip (one lane per row, 8-B
+//            loads, 120 contiguous bytes per instance);
 //   then     reward / counters (BaseMazeEnv.step, base_maze_env.py:163-210), the Enrich window
-//            assembled bit by bit in LDS from band rows picked with a lane shuffle (row i of
-//            the chosen window = band row off + i), and only then every global store: state,
-//            outputs, and the IPW windows as f32 with 16-B stores (1 KiB per wave instruction).
-//            No wait in the kernel ever covers a store.
+//            assembled bit by bit in LDS, and only then every global store: state, outputs, and
+//            the IPW windows as f32 with 16-B stores (1 KiB per wave instruction). No wait in the
+//            kernel ever covers a store.
 // AR (autoreset): an instance whose previous step ended terminated|truncated is reset by this
 // launch instead of stepping (BaseMazeEnv.reset, :136-161: same maze, agent at start, visits
 // cleared; the trainer's env.reset() after a finished episode) — its action is ignored
@@ -371,53 +301,52 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
   if (ACT && live && !rst) araw = act_draw(ap, e, ep, greedy, pw, cw, TOR);
   const int a = araw & 3;
   const bool trans = live && !rst && araw >= 0;  // araw < 0: observe only (obs of current state)
-  // the cell the agent ends in if its move is legal (reset: the start cell)
+  // the cell the agent would enter (reset: the start cell) and whether it does: the move rule
+  // of maze_view.move_agent (maze_view.py:167-197) — in bounds (Q3) and open
   int tr = r, tc = c;
-  bool inb = rst;
+  bool mv = false;
   if (rst) { tr = sr; tc = sc; }
   else if (trans) {
     tr = r + mz_dr(a); tc = c + mz_dc(a);
-    if (TOR) { tr = mz_wrapn(tr, N); tc = mz_wrapn(tc, N); inb = true; }
+    bool inb = true;
+    if (TOR) { tr = mz_wrapn(tr, N); tc = mz_wrapn(tc, N); }
     else inb = 0 < tr && tr < N - 1 && 0 < tc && tc < N - 1;  // maze_view.py:169 (Q3)
-    if (!inb) { tr = r; tc = c; }
+    mv = inb && ((cw >> (MZ_CELL_NB_SHIFT + a)) & 1u);  // == target cell word & MZ_CELL_OPEN
+    if (!mv) { tr = r; tc = c; }
   }
 
   // ---- level 2
   const uint32_t tag = (sw >> MZ_STW_TAG_SHIFT) & 7u;  // the episode's visit-count tag
   uint32_t ncw = 0u;
-  if (inb) ncw = d.cells[es * d.P * d.P + (size_t)tr * d.P + tc];  // cell word + visit count
+  if (mv || rst) ncw = d.cells[es * d.P * d.P + (size_t)tr * d.P + tc];  // cell word + visit count
   const int cnt = rst ? 0 : mz_cell_count(ncw, tag);
-  constexpr int RW = TOR ? 8 : 4;
-  uint32_t wv[WIN_IT][RW];  // band row words
-  int geo = 0, col = 0;
+  uint2 wr[WIN_IT];  // strip pairs of the final window's rows
+  int geo = 0;
   if (ENRICH) {
-    if (live) win_band<TOR>(rst ? tr : r, rst ? tc : c, tr, tc, N, geo, col);  // reset: start only
+    if (live) geo = win_geo<TOR>(tr, tc, N);  // tr, tc = where the agent is after this launch
 #pragma unroll
     for (int it = 0; it < WIN_IT; ++it) {
-      const int j = it * (WAVE / 16) + (lane >> 4), k = lane & 15;
+      const int j = it * (WAVE / 16) + (lane >> 4), i = lane & 15;
       const int g = __shfl(geo, j);
-      if (j < nb && (k < 15 || ((g >> 14) & 1))) {
-        const int n_ = (g >> 16) & 0xFF, R0 = g & 0xFF;
-        load_row<TOR>(d, (size_t)(e0 + j), TOR ? mz_wrapn(R0 + k, n_) : R0 + k, (g >> 8) & 0xF,
-                      wv[it]);
-      }
+      wr[it] = make_uint2(0u, 0u);
+      if (j < nb && i < 15) wr[it] = *mz_strip_row(d, (size_t)(e0 + j), geo_st(g), geo_row<TOR>(g, i));
     }
   }
   __syncthreads();  // pen[] (single-wave workgroup: an LDS wait, no s_barrier)
 
   // ---- transition (BaseMazeEnv.step) or reset
   double rew = 0.0;
-  bool term = false, trunc = false, done = false, sel = false;
+  bool term = false, trunc = false, done = false;
   int vr = -1, vc = -1;
   uint32_t ntag = tag;
   if (rst) {
     r = sr; c = sc; cw = ncw; nm = 0; la = 0; steps = 0; inv = 0;
     ntag = (tag + 1u) & 7u;  // visited_cell = [] (base_maze_env.py:159): a new count tag
-    sel = true; vr = sr; vc = sc;  // visited = {start} (base_maze_env.py:148-149)
+    vr = sr; vc = sc;  // visited = {start} (base_maze_env.py:148-149)
   } else if (trans) {
-    if (ncw & MZ_CELL_OPEN) {  // moved (ncw = 0 when out of bounds)
+    if (mv) {
       if (cnt == 0) {
-        // first entry: non_visited[cell] = 0 (base_maze_env.py:184); plane bit set below
+        // first entry: non_visited[cell] = 0 (base_maze_env.py:184); plane bits set below
         vr = tr; vc = tc;
         if (tr == gr && tc == gc) { rew = 1.0; term = true; }  // :185-187
         else {  // (old_dist - new_dist) * 0.5 - 0.05 with len = D + 1 (:189-192)
@@ -431,7 +360,6 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
       nm = min(nm + 1, 2);
       la = a;
       r = tr; c = tc; cw = ncw;
-      sel = true;
     } else {
       inv = min(inv + 1, 255);
       rew = pen[256 + inv];  // :199-200
@@ -445,24 +373,16 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
   // ---- window bits in LDS (compute only: every global store of the step comes after, so no
   // wait in this kernel ever covers a store)
   if (ENRICH) {
-    const int ps = (int)sel | ((int)rst << 1) | ((vr + 1) << 8) | ((vc + 1) << 16);
+    const int ps = (int)rst | ((vr + 1) << 8) | ((vc + 1) << 16);
     const int pg = gr | (gc << 8);
 #pragma unroll
     for (int it = 0; it < WIN_IT; ++it) {
       const int j = it * (WAVE / 16) + (lane >> 4), i = lane & 15;
-      const int s_ = __shfl(ps, j), g = __shfl(geo, j), cc = __shfl(col, j), gg = __shfl(pg, j);
-      const bool useb = s_ & 1;
-      const int off = useb ? ((g >> 13) & 1) : ((g >> 12) & 1);
-      uint32_t w[RW];
-#pragma unroll
-      for (int k = 0; k < RW; ++k) w[k] = (uint32_t)__shfl((int)wv[it][k], (lane + off) & (WAVE - 1));
+      const int s_ = __shfl(ps, j), g = __shfl(geo, j), gg = __shfl(pg, j);
       if (j < nb && i < 15) {
-        const int n_ = (g >> 16) & 0xFF, R0 = g & 0xFF;
-        const int R = TOR ? mz_wrapn(R0 + i + off, n_) : R0 + i + off;
-        const int C0 = useb ? ((cc >> 8) & 0xFF) : (cc & 0xFF);
         uint32_t c0, c1, c2;
-        win_bits<TOR>(w, n_, R, C0, (g >> 8) & 0xF, gg & 0xFF, (gg >> 8) & 0xFF,
-                      ((s_ >> 8) & 0xFF) - 1, ((s_ >> 16) & 0xFF) - 1, (s_ >> 1) & 1, c0, c1, c2);
+        win_row_bits<TOR>(wr[it], g, geo_row<TOR>(g, i), gg & 0xFF, (gg >> 8) & 0xFF,
+                          ((s_ >> 8) & 0xFF) - 1, ((s_ >> 16) & 0xFF) - 1, s_ & 1, c0, c1, c2);
         const int base = j * 675 + i * 15;
         cat_put(cat, base, c0);
         cat_put(cat, base + 225, c1);
@@ -478,8 +398,8 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
     d.stw[e] = (uint32_t)steps | ((uint32_t)inv << 16) | (ntag << MZ_STW_TAG_SHIFT);
     d.curw[e] = cw;
     d.last_term[e] = term;
-    if (sel && !rst) {
-      if (vr >= 0) atomicOr(&d.planes[(es * d.P + tr) * d.PW + 2 * (tc >> 5) + 1], 1u << (tc & 31));
+    if (mv) {
+      if (ENRICH && vr >= 0) mark_visited<TOR>(d, es, tr, tc, N);
       d.cells[es * d.P * d.P + (size_t)tr * d.P + tc] =  // visited_cell.append (:196)
           (ncw & MZ_CELL_STATIC) | ((uint32_t)min(cnt + 1, 255) << MZ_CELL_CNT_SHIFT) |
           (tag << MZ_CELL_TAG_SHIFT);
@@ -509,15 +429,11 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
     while (bal) {
       const int j = __ffsll((long long)bal) - 1;
       bal &= bal - 1;
-      const int q = __shfl(sp, j), srj = q & 0xFF, scj = (q >> 8) & 0xFF;
+      const int q = __shfl(sp, j);
       const size_t ej = (size_t)(e0 + j);
       const int Nj = (q >> 19) & 0xFF;
-      for (int k = lane; k < Nj * d.NW; k += WAVE) {  // rows >= N hold no open cell
-        const int R = k / d.NW, w = k - R * d.NW;
-        d.planes[(ej * d.P + R) * d.PW + 2 * w + 1] =
-            (R == srj && w == (scj >> 5)) ? (1u << (scj & 31)) : 0u;
-      }
-      if (((q >> 16) & 7) == 0) clear_counts(d, ej, (q >> 19) & 0xFF);
+      reset_visited(d, ej, Nj, q & 0xFF, (q >> 8) & 0xFF, TOR, lane);
+      if (((q >> 16) & 7) == 0) clear_counts(d, ej, Nj);
     }
   }
 
@@ -560,12 +476,8 @@ __device__ void reset_one(const MzDev& d, int e, const MzOut& o, uint32_t* wsh) 
   // visited_cell = [] (base_maze_env.py:159): a new visit-count tag (all counts cleared on wrap)
   const uint32_t ntag = ((d.stw[e] >> MZ_STW_TAG_SHIFT) + 1u) & 7u;
   if (ntag == 0u) clear_counts(d, es, N);
-  // visited plane = {start} (non_visited = open & ~start, :148-149): odd words of each row
-  for (int k = lane; k < N * d.NW; k += WAVE) {  // rows >= N hold no open cell
-    const int R = k / d.NW, w = k - R * d.NW;
-    const uint32_t v = (R == sr && w == (sc >> 5)) ? (1u << (sc & 31)) : 0u;
-    d.planes[(es * d.P + R) * d.PW + 2 * w + 1] = v;
-  }
+  // visited plane = {start} (non_visited = open & ~start, :148-149)
+  reset_visited(d, es, N, sr, sc, TOR, lane);
   if (lane == 0) {
     int br, bc;
     best_dir(sr, sc, cw, N, TOR, br, bc);
@@ -586,7 +498,8 @@ __device__ void reset_one(const MzDev& d, int e, const MzOut& o, uint32_t* wsh) 
     __syncthreads();
     if (lane < 15) {  // open words are static; the visited plane is {start} (not read back)
       uint32_t c0, c1, c2;
-      win_row(d, es, TOR, N, sr, sc, gr, gc, sr, sc, true, lane, c0, c1, c2);
+      const int g = win_geo<TOR>(sr, sc, N), R = geo_row<TOR>(g, lane);
+      win_row_bits<TOR>(*mz_strip_row(d, es, geo_st(g), R), g, R, gr, gc, sr, sc, true, c0, c1, c2);
       cat_put(wsh, lane * 15, c0);
       cat_put(wsh, 225 + lane * 15, c1);
       cat_put(wsh, 450 + lane * 15, c2);
@@ -635,7 +548,7 @@ __device__ bool bank_take(const MzDev& d, int e, int a, int N) {
   const uint32_t* cs = d.bk_cells + src * pp;
   uint32_t* cd = d.cells + es * pp;
   for (size_t i = threadIdx.x; i < pp; i += WAVE) cd[i] = cs[i];
-  const size_t pw = (size_t)d.P * d.PW;
+  const size_t pw = (size_t)d.PW;
   const uint32_t* ps = d.bk_planes + src * pw;
   uint32_t* pd = d.planes + es * pw;
   for (size_t i = threadIdx.x; i < pw; i += WAVE) pd[i] = ps[i];
