@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""A/B of the headline vector step in its steady state (bench.py's loop: fused act + step with
+autoreset, 65,536 x 81x81 r-prim Enrich, f32 window): time per launch and resets per launch.
+
+  python profiles/exp_autoreset.py [--lib alt.so] [--warmup 300] [--iters 1000]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "maze-solving-agent-gymnasium_amd"))
+
+import torch  # noqa: E402
+
+import mazerl  # noqa: E402
+from mazerl import _build  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=65536)
+    ap.add_argument("--dim", type=int, default=81)
+    ap.add_argument("--warmup", type=int, default=300)
+    ap.add_argument("--iters", type=int, default=1000)
+    ap.add_argument("--lib", default=None)
+    a = ap.parse_args()
+    if a.lib:
+        _build.LIB = os.path.abspath(a.lib)
+    env = mazerl.VectorMazeEnv(a.envs, a.dim, enrich=True, device="cuda:0", seed=0x5EED0000,
+                               window=True, window_bits=False, pos=False, done_list=False)
+    st = torch.cuda.current_stream()
+    for k in range(a.warmup):
+        env.step_act(eps=1.0, seed=0xBE7C4, counter=k, autoreset=True)
+    resets = torch.zeros((), dtype=torch.int64, device="cuda")
+    for k in range(50):  # resets per launch in the steady state
+        env.step_act(eps=1.0, seed=0xBE7C4, counter=a.warmup + k, autoreset=True)
+        resets += (env.actions < 0).sum()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for k in range(a.iters):
+        env.step_act(eps=1.0, seed=0xBE7C4, counter=a.warmup + 50 + k, autoreset=True)
+    e1.record(st)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / a.iters * 1e3
+    print(json.dumps({"lib": a.lib or "in-tree", "us_per_launch": round(us, 2),
+                      "resets_per_launch": float(resets) / 50.0}), flush=True)
+    env.close()
+
+
+if __name__ == "__main__":
+    main()

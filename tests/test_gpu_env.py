@@ -322,11 +322,13 @@ def test_generate_from_random_advances_python_stream(mazerl):
     env.close()
 
 
-@pytest.mark.parametrize("tor,dim", [(False, 15), (True, 17)])
-def test_many_episodes_reset_done_vs_oracle(mazerl, tor, dim):
-    """Visit counts live in the cell words under an episode tag that wraps every 8 resets (then
-    the counts are cleared): replay 25+ episodes per instance through step + k_reset_done
-    (flag-scan auto-reset) against the oracle, rewards compared as float64 ==."""
+@pytest.mark.parametrize("tor,dim,ar", [(False, 15, False), (True, 17, False), (False, 15, True),
+                                        (True, 17, True)])
+def test_many_episodes_reset_done_vs_oracle(mazerl, tor, dim, ar):
+    """Visit counts live in the cell words under a 3-bit episode tag that wraps every 8 resets
+    (then the counts are cleared). Replay 25+ episodes per instance — through step + k_reset_done (flag-scan
+    auto-reset) or through k_step's fused autoreset — against the oracle, rewards compared as
+    float64 ==."""
     import pyoracle as O
     B = 96
     env = mazerl.VectorMazeEnv(B, dim, toroidal=tor, enrich=True, reward64=True, seed=777)
@@ -337,21 +339,29 @@ def test_many_episodes_reset_done_vs_oracle(mazerl, tor, dim):
         o.reset()
         ors.append(o)
     episodes = np.zeros(B, np.int64)
+    was_done = np.zeros(B, bool)
     for k in range(1500):
-        env.step_act(eps=1.0, seed=5, counter=k)
+        env.step_act(eps=1.0, seed=5, counter=k, autoreset=ar)
         a = env.actions.cpu().numpy()
         r64 = env.reward64.cpu().numpy()
         win = env.window.cpu().numpy()
         done = (env.terminated | env.truncated).cpu().numpy().astype(bool)
         for i in range(B):
-            o = ors[i].step(int(a[i]))
+            if ar and was_done[i]:
+                assert a[i] == -1, (k, i)
+                o = ors[i].reset()
+            else:
+                o = ors[i].step(int(a[i]))
             assert r64[i] == o["reward"], (k, i)
             assert bool(done[i]) == (o["terminated"] or o["truncated"]), (k, i)
             np.testing.assert_array_equal(win[i], o["window"].astype(np.float32))
             if done[i]:
-                ors[i].reset()
+                if not ar:
+                    ors[i].reset()
                 episodes[i] += 1
-        env.reset_done()
+            was_done[i] = done[i]
+        if not ar:
+            env.reset_done()
     assert episodes.min() >= 9, episodes.min()  # every instance wrapped its tag at least once
     env.close()
 
