@@ -168,7 +168,7 @@ __device__ inline uint32_t mz_strip_colmask(int s, int col, int N, bool tor) {
   const int j0 = col - MZ_STRIP_STRIDE * s;
   if (!tor) return (j0 >= 0 && j0 < 32) ? (1u << j0) : 0u;
   uint32_t m = 0u;
-  for (int j = mz_wrap(j0, N); j < 32; j += N) m |= 1u << j;
+  for (int j = mz_wrapn(j0, N); j < 32; j += N) m |= 1u << j;
   return m;
 }
 

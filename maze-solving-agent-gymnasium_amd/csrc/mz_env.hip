@@ -37,7 +37,8 @@
 // less than the workgroup barrier that the shared table needs.
 #define MZ_SPW 1
 #endif
-#define CAT_WORDS (IPW * 675 / 32 + 2)  // IPW x 675 window bits + funnel-shift slack
+// LDS words of a wave's window bits: ipw x 675 bits + funnel-shift slack
+__host__ __device__ constexpr int cat_words(int ipw) { return ipw * 675 / 32 + 2; }
 
 namespace {
 
@@ -93,13 +94,20 @@ __device__ inline void win_row_bits(uint2 pr, int g, int R, int gr, int gc, int 
   ch2 = open15 & ~vis15;
 }
 
+// strips a window of an N-grid can start in (euclidean c0 <= N - 15, torus c0 <= N - 1); the
+// others are never read, so neither marked nor reset (a small maze under a large pitch)
+__device__ inline int used_strips(int N, bool tor) {
+  return tor ? mz_nstrips(N) : (N - 15) / MZ_STRIP_STRIDE + 1;
+}
+
 // visited_cell.append (base_maze_env.py:196) in the planes: the cell's bit in every strip that
 // holds its column (euclidean: one or two; torus: any strip, repeated when N < 32). No-return
-// atomics: several lanes may touch one word of an instance only through this, one at a time.
+// atomics (a plain store of the window strip's word, which the step has just read, measured
+// slower: 32.26 vs 31.96 us per launch at 65,536 x 81, 25.11 vs 24.67 on config 5's shape).
 template <bool TOR>
 __device__ inline void mark_visited(const MzDev& d, size_t e, int R, int col, int N) {
   const int lo = TOR ? 0 : max(0, (col - 31 + MZ_STRIP_STRIDE - 1) / MZ_STRIP_STRIDE);
-  const int hi = TOR ? d.NS - 1 : min(d.NS - 1, col / MZ_STRIP_STRIDE);
+  const int hi = min(used_strips(N, TOR), TOR ? d.NS : col / MZ_STRIP_STRIDE + 1) - 1;
   for (int st = lo; st <= hi; ++st) {
     const uint32_t m = mz_strip_colmask(st, col, N, TOR);
     if (m) atomicOr(reinterpret_cast<uint32_t*>(mz_strip_row(d, e, st, R)) + 1, m);
@@ -109,11 +117,11 @@ __device__ inline void mark_visited(const MzDev& d, size_t e, int R, int col, in
 // visited plane of instance e = {(sr, sc)} (reset; rows >= N hold no open cell): one wave
 __device__ inline void reset_visited(const MzDev& d, size_t e, int N, int sr, int sc, bool tor,
                                      int lane) {
-  for (int k = lane; k < N * d.NS; k += WAVE) {
-    const int st = k / N, R = k - st * N;
-    reinterpret_cast<uint32_t*>(mz_strip_row(d, e, st, R))[1] =
-        R == sr ? mz_strip_colmask(st, sc, N, tor) : 0u;
-  }
+  const int ns = min(d.NS, used_strips(N, tor));
+  for (int R = lane; R < N; R += WAVE)  // one row per lane, every used strip (no index division)
+    for (int st = 0; st < ns; ++st)
+      reinterpret_cast<uint32_t*>(mz_strip_row(d, e, st, R))[1] =
+          R == sr ? mz_strip_colmask(st, sc, N, tor) : 0u;
 }
 
 __device__ inline void cat_put(uint32_t* cat, int o, uint32_t v) {
@@ -236,7 +244,8 @@ __device__ inline int act_sample(const MzAct& ap, int e, uint32_t pw, uint32_t c
                   cw, tor);
 }
 
-#define WIN_IT (IPW * 16 / WAVE)  // window rows per lane: lane l of pass it = instance 4*it + l/16, row l%16
+// window-row passes: lane l of pass it = instance 4*it + l/16, row l%16
+__host__ __device__ constexpr int win_it(int ipw) { return ipw * 16 / WAVE; }
 
 // ------------------------------------------------------------------------------------------
 // One vector step, IPW instances per 64-lane wave, with two dependent global round trips:
@@ -262,15 +271,24 @@ __device__ inline int act_sample(const MzAct& ap, int e, uint32_t pw, uint32_t c
 // per pass, and the slowest wave sets the launch time).
 __device__ inline void clear_counts(const MzDev& d, size_t e, int N) {
   uint32_t* c = d.cells + e * d.P * d.P;
-  for (int k = threadIdx.x & (WAVE - 1); k < N * d.P; k += WAVE)
-    (void)__hip_atomic_fetch_and(&c[k], MZ_CELL_STATIC, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int lane = threadIdx.x & (WAVE - 1), n = N * d.P;
+  // 8-B atomics (512 B per wave instruction, half the instructions of 4-B ones) from the first
+  // 8-B boundary; the odd head / tail word with 4-B ones
+  const int h = (int)((reinterpret_cast<uintptr_t>(c) >> 2) & 1u);
+  if (lane == 0 && h) (void)__hip_atomic_fetch_and(&c[0], MZ_CELL_STATIC, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 1 && ((n - h) & 1))
+    (void)__hip_atomic_fetch_and(&c[n - 1], MZ_CELL_STATIC, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned long long* c2 = reinterpret_cast<unsigned long long*>(c + h);
+  const unsigned long long m2 = ((unsigned long long)MZ_CELL_STATIC << 32) | MZ_CELL_STATIC;
+  for (int k = lane; k < (n - h) >> 1; k += WAVE)
+    (void)__hip_atomic_fetch_and(&c2[k], m2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <bool TOR, bool ENRICH, bool ACT, bool AR>
+template <int IPWT, bool TOR, bool ENRICH, bool ACT, bool AR>
 __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ act, const MzAct& ap,
                                   const MzOut& o, int e0, uint32_t* cat, double* pen, bool load_pen) {
   const int lane = threadIdx.x & (WAVE - 1);
-  const int nb = max(0, min(IPW, d.B - e0));  // 0: a trailing wave of the last workgroup
+  const int nb = max(0, min(IPWT, d.B - e0));  // 0: a trailing wave of the last workgroup
   const int e = e0 + lane;
   const size_t es = (size_t)e;
   const bool live = lane < nb;
@@ -302,7 +320,7 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
     }
   }
   if (ENRICH)
-    for (int i = lane; i < CAT_WORDS; i += WAVE) cat[i] = 0u;
+    for (int i = lane; i < cat_words(IPWT); i += WAVE) cat[i] = 0u;
 
   const int N = m0 & 0xFF, sr = (m0 >> 16) & 0xFF, sc = m0 >> 24;
   const int gr = m1 & 0xFF, gc = (m1 >> 8) & 0xFF, maxs = m1 >> 16;
@@ -331,12 +349,12 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
   uint32_t ncw = 0u;
   if (mv || rst) ncw = d.cells[es * d.P * d.P + (size_t)tr * d.P + tc];  // cell word + visit count
   const int cnt = rst ? 0 : mz_cell_count(ncw, tag);
-  uint2 wr[WIN_IT];  // strip pairs of the final window's rows
+  uint2 wr[win_it(IPWT)];  // strip pairs of the final window's rows
   int geo = 0;
   if (ENRICH) {
     if (live) geo = win_geo<TOR>(tr, tc, N);  // tr, tc = where the agent is after this launch
 #pragma unroll
-    for (int it = 0; it < WIN_IT; ++it) {
+    for (int it = 0; it < win_it(IPWT); ++it) {
       const int j = it * (WAVE / 16) + (lane >> 4), i = lane & 15;
       const int g = __shfl(geo, j);
       wr[it] = make_uint2(0u, 0u);
@@ -387,7 +405,7 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
     const int ps = (int)rst | ((vr + 1) << 8) | ((vc + 1) << 16);
     const int pg = gr | (gc << 8);
 #pragma unroll
-    for (int it = 0; it < WIN_IT; ++it) {
+    for (int it = 0; it < win_it(IPWT); ++it) {
       const int j = it * (WAVE / 16) + (lane >> 4), i = lane & 15;
       const int s_ = __shfl(ps, j), g = __shfl(geo, j), gg = __shfl(pg, j);
       if (j < nb && i < 15) {
@@ -460,14 +478,16 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
   }
 }
 
-// One wave per group of IPW instances. (A persistent variant — each wave stepping several
+// One wave per group of IPWT instances. (A persistent variant — each wave stepping several
 // groups so that its next gathers trail its window stores — measured slower at every
 // groups-per-wave setting: 46 / 60 / 104 us at 2 / 4 / 8 groups per wave vs 40 us at 1, because
 // the gather phase is latency-bound per wave and needs every group's wave in flight at once.)
-template <bool TOR, bool ENRICH, bool ACT, bool AR>
+// IPWT = 16 for large batches; small batches (the per-GPU shares of the 8-GPU configs) take 4,
+// so that four times as many waves share the latency chain and the window stores.
+template <int IPWT, bool TOR, bool ENRICH, bool ACT, bool AR>
 __global__ __launch_bounds__(WAVE * MZ_SPW) void k_step(MzDev d, const int32_t* __restrict__ act,
                                                         MzAct ap, MzOut o) {
-  __shared__ uint32_t cat[MZ_SPW][(CAT_WORDS + 3) & ~3];
+  __shared__ uint32_t cat[MZ_SPW][(cat_words(IPWT) + 3) & ~3];
   __shared__ __align__(16) double pen[512];  // pen_visit[256] | pen_inv[256]
   const int w = MZ_SPW > 1 ? (int)(threadIdx.x / WAVE) : 0;
   int b = blockIdx.x;
@@ -475,7 +495,7 @@ __global__ __launch_bounds__(WAVE * MZ_SPW) void k_step(MzDev d, const int32_t* 
   // instance groups, so the 64-B state / output segments of neighbouring groups (halves of one
   // 128-B line) meet in one XCD's L2 (65,536 x 81: 32.65 -> 31.96 us per launch)
   if ((gridDim.x & 7) == 0) b = (b & 7) * (int)(gridDim.x >> 3) + (b >> 3);
-  step_group<TOR, ENRICH, ACT, AR>(d, act, ap, o, (b * MZ_SPW + w) * IPW, cat[w], pen, true);
+  step_group<IPWT, TOR, ENRICH, ACT, AR>(d, act, ap, o, (b * MZ_SPW + w) * IPWT, cat[w], pen, true);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -740,17 +760,27 @@ hipError_t mz_launch_regen(const MzDev& d, const int32_t* idx, const int32_t* co
   return hipGetLastError();
 }
 
+#ifndef MZ_SMALL_B
+#define MZ_SMALL_B 16384  // batches up to this size step with 4 instances per wave
+#endif
+template <int I, bool T, bool E>
+void launch_step_ite(const MzDev& d, const int32_t* act, const MzAct& a, bool has_act, bool ar,
+                     const MzOut& o, hipStream_t s) {
+  dim3 grid((d.B + I * MZ_SPW - 1) / (I * MZ_SPW)), block(WAVE * MZ_SPW);
+  if (has_act) {
+    if (ar) hipLaunchKernelGGL((k_step<I, T, E, true, true>), grid, block, 0, s, d, act, a, o);
+    else hipLaunchKernelGGL((k_step<I, T, E, true, false>), grid, block, 0, s, d, act, a, o);
+  } else {
+    if (ar) hipLaunchKernelGGL((k_step<I, T, E, false, true>), grid, block, 0, s, d, act, a, o);
+    else hipLaunchKernelGGL((k_step<I, T, E, false, false>), grid, block, 0, s, d, act, a, o);
+  }
+}
+
 template <bool T, bool E>
 void launch_step_te(const MzDev& d, const int32_t* act, const MzAct& a, bool has_act, bool ar,
                     const MzOut& o, hipStream_t s) {
-  dim3 grid((d.B + IPW * MZ_SPW - 1) / (IPW * MZ_SPW)), block(WAVE * MZ_SPW);
-  if (has_act) {
-    if (ar) hipLaunchKernelGGL((k_step<T, E, true, true>), grid, block, 0, s, d, act, a, o);
-    else hipLaunchKernelGGL((k_step<T, E, true, false>), grid, block, 0, s, d, act, a, o);
-  } else {
-    if (ar) hipLaunchKernelGGL((k_step<T, E, false, true>), grid, block, 0, s, d, act, a, o);
-    else hipLaunchKernelGGL((k_step<T, E, false, false>), grid, block, 0, s, d, act, a, o);
-  }
+  if (d.B <= MZ_SMALL_B) launch_step_ite<4, T, E>(d, act, a, has_act, ar, o, s);
+  else launch_step_ite<IPW, T, E>(d, act, a, has_act, ar, o, s);
 }
 
 hipError_t mz_launch_step(const MzDev& d, const int32_t* act, const MzAct* ap, bool autoreset,

@@ -17,6 +17,8 @@ from mazerl.trainers.vector_trainer import make_env  # noqa: E402
 CONFIGS = [
     ("cfg2: 4096 x 15x15 r-prim euclidean", 4096, [15], False, "r-prim"),
     ("cfg3: 65536 x 81x81 r-prim (headline)", 65536, [81], False, "r-prim"),
+    ("cfg3 at 16384: 16384 x 81x81 r-prim", 16384, [81], False, "r-prim"),
+    ("cfg3 at 32768: 32768 x 81x81 r-prim", 32768, [81], False, "r-prim"),
     ("cfg4 per GPU: 8192 x 81x81 mixed algorithms", 8192, [81], False, "mixed"),
     ("cfg5 per GPU: 4096 x toroidal 17..79 variable", 4096, list(range(17, 80, 2)), True, "r-prim"),
     ("cfg5 whole: 32768 x toroidal 17..79 variable (1 GPU)", 32768, list(range(17, 80, 2)), True, "r-prim"),
@@ -25,6 +27,9 @@ CONFIGS = [
 
 def main(steps=500):
     ar_modes = [True, False] if "--both" in sys.argv else [True]
+    if "--lib" in sys.argv:  # A/B against another libmazerl build
+        from mazerl import _build
+        _build.LIB = os.path.abspath(sys.argv[sys.argv.index("--lib") + 1])
     for (name, B, dims, tor, algo), ar in [(c, m) for c in CONFIGS for m in ar_modes]:
         algorithm = algo if algo != "mixed" else torch.arange(B) % 3
         env = make_env(B, dims, toroidal=tor, algorithm=algorithm, seed=0x5EED0000, device="cuda:0",
@@ -38,8 +43,13 @@ def main(steps=500):
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / steps
         print(json.dumps({"config": name, "autoreset": ar, "envs": B, "us_per_vector_step": round(dt * 1e6, 2),
-                          "env_steps_per_s": B / dt}), flush=True)
+                          "env_steps_per_s": B / dt, "lib": os.path.basename(_lib())}), flush=True)
         env.close()
+
+
+def _lib():
+    from mazerl import _build
+    return _build.LIB
 
 
 if __name__ == "__main__":

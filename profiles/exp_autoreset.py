@@ -25,11 +25,18 @@ def main():
     ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--iters", type=int, default=1000)
     ap.add_argument("--lib", default=None)
+    ap.add_argument("--toroidal-variable", action="store_true",
+                    help="config 5 shape: toroidal grids 17..79 (instance i gets 17 + 2 (i mod 32))")
     a = ap.parse_args()
     if a.lib:
         _build.LIB = os.path.abspath(a.lib)
-    env = mazerl.VectorMazeEnv(a.envs, a.dim, enrich=True, device="cuda:0", seed=0x5EED0000,
-                               window=True, window_bits=False, pos=False, done_list=False)
+    if a.toroidal_variable:
+        from mazerl.trainers.vector_trainer import make_env
+        env = make_env(a.envs, list(range(17, 80, 2)), toroidal=True, seed=0x5EED0000, device="cuda:0",
+                       window=True, window_bits=False, pos=False, done_list=False)
+    else:
+        env = mazerl.VectorMazeEnv(a.envs, a.dim, enrich=True, device="cuda:0", seed=0x5EED0000,
+                                   window=True, window_bits=False, pos=False, done_list=False)
     st = torch.cuda.current_stream()
     for k in range(a.warmup):
         env.step_act(eps=1.0, seed=0xBE7C4, counter=k, autoreset=True)
