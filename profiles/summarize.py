@@ -35,7 +35,7 @@ def main():
     ap.add_argument("write")
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--dim", type=int, default=81)
-    ap.add_argument("--kernel", default="k_step<false, true, true, true>")
+    ap.add_argument("--kernel", default="k_step<16, false, true, true, true>")
     a = ap.parse_args()
     stats = glob.glob(os.path.join(a.kt, "**", "*kernel_stats.csv"), recursive=True)[0]
     shutil.copy(stats, os.path.join(HERE, f"{a.tag}_kernel_stats.csv"))
