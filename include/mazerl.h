@@ -320,6 +320,13 @@ int mz_maze_metrics(mz_handle* h, const int32_t* env_ids_dev, int32_t n, double*
 int mz_query(mz_handle* h, int32_t env, mz_env_info* info_host);
 int mz_get_grid(mz_handle* h, int32_t env, uint8_t* grid_host /* [n][n] */);
 
+/* Page-locked host memory mapped into the device's address space (hipHostMalloc, mapped +
+ * coherent): kernels read and write it through *dev_out. The single-env drop-ins keep their
+ * action and per-step outputs there, so one reference step() (base_maze_env.py:163-210) is one
+ * launch + one stream synchronisation, with no device<->host copies. Free with mz_host_free. */
+int mz_host_alloc(uint64_t bytes, int32_t device, void** host_out, void** dev_out);
+int mz_host_free(void* host);
+
 #ifdef __cplusplus
 }
 #endif

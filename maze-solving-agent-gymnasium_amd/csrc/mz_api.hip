@@ -638,4 +638,30 @@ int mz_get_grid(mz_handle* h, int32_t env, uint8_t* grid_host) {
   return MZ_OK;
 }
 
+int mz_host_alloc(uint64_t bytes, int32_t device, void** host_out, void** dev_out) {
+  if (!host_out || !dev_out || bytes == 0) return fail(MZ_EINVAL, "bad arguments");
+  int ndev = 0;
+  MZ_HIP(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(MZ_EINVAL, "device %d not present", device);
+  DeviceGuard g(device);
+  void* hp = nullptr;
+  MZ_HIP(hipHostMalloc(&hp, (size_t)bytes, hipHostMallocMapped | hipHostMallocCoherent));
+  void* dp = nullptr;
+  const hipError_t e = hipHostGetDevicePointer(&dp, hp, 0);
+  if (e != hipSuccess) {
+    (void)hipHostFree(hp);
+    return fail(MZ_EHIP, "hipHostGetDevicePointer: %s", hipGetErrorString(e));
+  }
+  std::memset(hp, 0, (size_t)bytes);
+  *host_out = hp;
+  *dev_out = dp;
+  return MZ_OK;
+}
+
+int mz_host_free(void* host) {
+  if (!host) return MZ_OK;
+  MZ_HIP(hipHostFree(host));
+  return MZ_OK;
+}
+
 }  // extern "C"

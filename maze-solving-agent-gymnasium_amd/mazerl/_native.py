@@ -41,7 +41,7 @@ EXPORTS = ["mz_last_error", "mz_device_count", "mz_create", "mz_destroy", "mz_lo
            "mz_bank_create", "mz_bank_fill", "mz_bank_use", "mz_bank_consumed",
            "mz_stem_forward", "mz_stem_backward", "mz_stem_workspace_floats", "mz_adamw_flat",
            "mz_pair_surrogate", "mz_leaky_relu_bf16", "mz_colsum_f32",
-           "mz_replay_gather"]
+           "mz_replay_gather", "mz_host_alloc", "mz_host_free"]
 
 _lib = None
 
@@ -107,6 +107,8 @@ def load(build_if_missing=True):
     L.mz_pair_surrogate.argtypes = [vp, vp, vp, C.c_int32, C.c_float, vp, vp, vp]
     L.mz_adamw_flat.argtypes = [vp, vp, vp, vp, vp, C.c_int32, vp, vp, C.c_double, C.c_double,
                                 C.c_double, C.c_double, C.c_float, C.c_float, C.c_int32, vp]
+    L.mz_host_alloc.argtypes = [C.c_uint64, C.c_int32, C.POINTER(vp), C.POINTER(vp)]
+    L.mz_host_free.argtypes = [vp]
     for f in EXPORTS:
         if f != "mz_last_error":
             getattr(L, f).restype = C.c_int

@@ -74,8 +74,11 @@ class BaseMazeEnv(_EnvBase):
             shape = tuple(maze_shape)
             max_dim = shape[0]
         self.maze_shape = shape
+        # host_scalars: action / reward / flags / position in mapped host memory, so step() is
+        # one launch + one stream sync (no copies)
         self._venv = VectorMazeEnv(1, shape[0], toroidal=self.TOROIDAL, enrich=self.ENRICH,
-                                   device=device, max_dim=max_dim, generate=False, reward64=True)
+                                   device=device, max_dim=max_dim, generate=False, reward64=True,
+                                   host_scalars=True)
         self.action_space = Discrete(4)
         self.observation_space = _space_dict(shape, self.ENRICH)
         self.mazes = []
@@ -144,9 +147,9 @@ class BaseMazeEnv(_EnvBase):
 
     # --- gym API -------------------------------------------------------------------------------
     def _obs(self):
-        v = self._venv
-        pos = v.pos[0].cpu().numpy().astype(np.int32)
-        bd = v.best_dir[0].cpu().numpy().astype(np.int64)
+        v = self._venv  # host-mapped outputs, written by the launch step()/reset() waited for
+        pos = v.pos[0].numpy().astype(np.int32)
+        bd = v.best_dir[0].numpy().astype(np.int64)
         self._agent_location = pos
         if self.ENRICH:
             shape = np.array(self.maze_shape)
@@ -159,17 +162,18 @@ class BaseMazeEnv(_EnvBase):
 
     def reset(self, seed=None, options=None):
         self._venv.reset()
+        self._venv.sync()
         obs = self._obs()
         self.cum_rew = 0
         return obs, self._info()
 
     def step(self, action):
-        a = torch.tensor([int(action)], dtype=torch.int32, device=self._venv.device)
-        self._venv.step(a)
+        v = self._venv
+        v.step_host(int(action))
         obs = self._obs()
-        truncated = bool(self._venv.truncated[0].item())
-        terminated = bool(self._venv.terminated[0].item())
-        r = float(self._venv.reward64[0].item())
+        truncated = bool(v.truncated[0])
+        terminated = bool(v.terminated[0])
+        r = float(v.reward64[0])
         reward = -1 if truncated else (1 if terminated else r)  # the reference's int literals
         self.cum_rew += reward
         return obs, reward, truncated, terminated, self._info()

@@ -26,7 +26,8 @@ def _ptr(t):
 class VectorMazeEnv:
     def __init__(self, num_envs, maze_dim, toroidal=False, enrich=True, device=None,
                  max_dim=None, algorithm="r-prim", seed=0x5EED0000, generate=True,
-                 window=True, window_bits=True, reward64=False, pos=True, done_list=True):
+                 window=True, window_bits=True, reward64=False, pos=True, done_list=True,
+                 host_scalars=False):
         if not torch.cuda.is_available():
             raise RuntimeError("VectorMazeEnv needs a HIP GPU (libmazerl.so has no CPU path)")
         self.lib = N.load()
@@ -42,21 +43,31 @@ class VectorMazeEnv:
         self._h = h
         B, dev = self.num_envs, self.device
         kw = dict(device=dev)
-        self.reward = torch.zeros(B, dtype=torch.float32, **kw)
-        self.reward64 = torch.zeros(B, dtype=torch.float64, **kw) if reward64 else None
-        self.terminated = torch.zeros(B, dtype=torch.uint8, **kw)
-        self.truncated = torch.zeros(B, dtype=torch.uint8, **kw)
-        self.pos = torch.zeros(B, 2, dtype=torch.int32, **kw) if pos else None
-        self.best_dir = torch.zeros(B, 2, dtype=torch.int32, **kw) if pos else None
+        # host_scalars: the action and the per-instance scalars (reward, flags, position, best
+        # dir) live in mapped page-locked host memory (mz_host_alloc) that the kernels read and
+        # write directly — the single-env drop-ins' step() is then one launch + one stream sync
+        # with no copies. They are CPU tensors then; everything else stays in HBM.
+        self._host = None
+        self._dptr = {}
+        if host_scalars:
+            self._alloc_host(B, reward64, pos)
+        else:
+            self.reward = torch.zeros(B, dtype=torch.float32, **kw)
+            self.reward64 = torch.zeros(B, dtype=torch.float64, **kw) if reward64 else None
+            self.terminated = torch.zeros(B, dtype=torch.uint8, **kw)
+            self.truncated = torch.zeros(B, dtype=torch.uint8, **kw)
+            self.pos = torch.zeros(B, 2, dtype=torch.int32, **kw) if pos else None
+            self.best_dir = torch.zeros(B, 2, dtype=torch.int32, **kw) if pos else None
+            self.actions = torch.zeros(B, dtype=torch.int32, **kw)
         self.obs6 = torch.zeros(B, 6, dtype=torch.float32, **kw)
         self.window = torch.zeros(B, 3, 15, 15, dtype=torch.float32, **kw) if (enrich and window) else None
         self.window_bits = torch.zeros(B, 22, dtype=torch.int32, **kw) if (enrich and window_bits) else None
         self.done_idx = torch.zeros(B, dtype=torch.int32, **kw)
         self.done_count = torch.zeros(1, dtype=torch.int32, **kw)
-        self.actions = torch.zeros(B, dtype=torch.int32, **kw)
+        dp = self._dev_ptr
         self._out = N.StepOut(
-            reward=_ptr(self.reward), reward64=_ptr(self.reward64), terminated=_ptr(self.terminated),
-            truncated=_ptr(self.truncated), pos=_ptr(self.pos), best_dir=_ptr(self.best_dir),
+            reward=dp(self.reward), reward64=dp(self.reward64), terminated=dp(self.terminated),
+            truncated=dp(self.truncated), pos=dp(self.pos), best_dir=dp(self.best_dir),
             obs6=_ptr(self.obs6), window_bits=_ptr(self.window_bits), window=_ptr(self.window),
             done_idx=_ptr(self.done_idx) if done_list else None,
             done_count=_ptr(self.done_count) if done_list else None)
@@ -73,10 +84,47 @@ class VectorMazeEnv:
     def _stream(self):
         return torch.cuda.current_stream(self.device).cuda_stream
 
+    def _alloc_host(self, B, reward64, pos):
+        import numpy as np
+        fields = [("actions", np.int32, (B,)), ("reward", np.float32, (B,)),
+                  ("reward64", np.float64, (B,)) if reward64 else None,
+                  ("terminated", np.uint8, (B,)), ("truncated", np.uint8, (B,)),
+                  ("pos", np.int32, (B, 2)) if pos else None,
+                  ("best_dir", np.int32, (B, 2)) if pos else None]
+        offs, total = [], 0
+        for f in fields:
+            if f is None:
+                continue
+            total = (total + 15) & ~15  # 16-B aligned fields
+            offs.append((f, total))
+            total += int(np.prod(f[2])) * np.dtype(f[1]).itemsize
+        hp, dpp = N.C.c_void_p(), N.C.c_void_p()
+        N.check(self.lib.mz_host_alloc(total, self.device.index or 0, N.C.byref(hp), N.C.byref(dpp)))
+        self._host = hp
+        raw = np.ctypeslib.as_array((N.C.c_uint8 * total).from_address(hp.value))
+        for name in ("reward64", "pos", "best_dir"):
+            setattr(self, name, None)
+        for (name, dt, shape), off in offs:
+            n = int(np.prod(shape)) * np.dtype(dt).itemsize
+            t = torch.from_numpy(raw[off:off + n].view(dt).reshape(shape))
+            setattr(self, name, t)
+            self._dptr[t.data_ptr()] = dpp.value + off
+
+    def _dev_ptr(self, t):
+        """Device address of an output tensor (mapped host memory has its own)."""
+        if t is None:
+            return None
+        return self._dptr.get(t.data_ptr(), t.data_ptr())
+
     def close(self):
         if getattr(self, "_h", None):
             self.lib.mz_destroy(self._h)
             self._h = None
+        if getattr(self, "_host", None) is not None:
+            for name in ("actions", "reward", "reward64", "terminated", "truncated", "pos", "best_dir"):
+                setattr(self, name, None)  # drop the views before the memory goes
+            self.lib.mz_host_free(self._host)
+            self._host = None
 
     def __del__(self):
         try:
@@ -236,6 +284,20 @@ class VectorMazeEnv:
         """Auto-reset from the step's device done list (consumes done_count)."""
         self.reset_list(self.done_idx, self.done_count, regen_won=regen_won, seed=seed)
 
+    def step_host(self, action, env=0):
+        """host_scalars envs: one instance's action straight into the mapped action slot, one
+        launch, one stream synchronisation; the scalar outputs are then readable on the host."""
+        if self._host is None:
+            raise RuntimeError("step_host needs VectorMazeEnv(host_scalars=True)")
+        self.actions[env] = int(action)
+        N.check(self.lib.mz_step_ex(self._h, self._dev_ptr(self.actions), N.C.byref(self._out), 0,
+                                    self._stream()))
+        self._count_zero = False
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def sync(self):
+        torch.cuda.current_stream(self.device).synchronize()
+
     def step(self, actions, autoreset=False):
         """actions: int tensor [B] on the device (negative = observe only). With autoreset,
         instances whose previous step ended are reset by this launch instead (action ignored,
@@ -244,7 +306,7 @@ class VectorMazeEnv:
             actions.to(device=self.device, dtype=torch.int32)
         a = a.contiguous()
         flags = N.MZ_STEP_AUTORESET if autoreset else 0
-        N.check(self.lib.mz_step_ex(self._h, a.data_ptr(), N.C.byref(self._out), flags,
+        N.check(self.lib.mz_step_ex(self._h, self._dev_ptr(a), N.C.byref(self._out), flags,
                                     self._stream()))
         self._count_zero = False
         return self.obs(), self.reward, self.truncated, self.terminated, {}
@@ -253,6 +315,7 @@ class VectorMazeEnv:
         """Fused epsilon-greedy act + step in one launch (actions taken -> actions_out; -1 for
         the instances an autoreset step resets)."""
         out = self.actions if actions_out is None else actions_out
+        out_p = self._dev_ptr(out)
         eps_t = eps if torch.is_tensor(eps) else None
         g = None if greedy is None else greedy.to(dtype=torch.int64).contiguous()
         flags = N.MZ_STEP_COUNT_ZEROED if self._count_zero else 0
@@ -260,7 +323,7 @@ class VectorMazeEnv:
             flags |= N.MZ_STEP_AUTORESET
         N.check(self.lib.mz_step_act(self._h, _ptr(eps_t), float(eps) if eps_t is None else 0.0,
                                      _ptr(g), seed & 0xFFFFFFFFFFFFFFFF,
-                                     counter & 0xFFFFFFFFFFFFFFFF, out.data_ptr(),
+                                     counter & 0xFFFFFFFFFFFFFFFF, out_p,
                                      N.C.byref(self._out), flags, self._stream()))
         self._count_zero = False
         return self.obs(), self.reward, self.truncated, self.terminated, {}
@@ -287,7 +350,7 @@ class VectorMazeEnv:
         g = None if greedy is None else greedy.to(dtype=torch.int64).contiguous()
         N.check(self.lib.mz_act(self._h, _ptr(eps_t), float(eps) if eps_t is None else 0.0,
                                 _ptr(g), seed & 0xFFFFFFFFFFFFFFFF, counter & 0xFFFFFFFFFFFFFFFF,
-                                out.data_ptr(), self._stream()))
+                                self._dev_ptr(out), self._stream()))
         return out
 
     def expand_window(self, bits, out=None):
