@@ -398,3 +398,33 @@ def test_extreme_sizes_vs_oracle(mazerl, tor, dim, B):
             np.testing.assert_array_equal(win[i], o["window"].astype(np.float32))
             was_done[i] = bool(te[i]) or bool(trn[i])
     env.close()
+
+
+def test_host_scalars_match_device_outputs(mazerl):
+    """VectorMazeEnv(host_scalars=True) — action and scalar outputs in mapped host memory
+    (mz_host_alloc) — gives the same actions, rewards, flags, positions and windows as the
+    device-output env on the same mazes and seeds, fused act + step with autoreset."""
+    import torch
+    B = 37
+    A = mazerl.VectorMazeEnv(B, 21, enrich=True, reward64=True, seed=99)
+    H = mazerl.VectorMazeEnv(B, 21, enrich=True, reward64=True, seed=99, host_scalars=True)
+    assert H.reward64.device.type == "cpu" and H.obs6.is_cuda
+    for k in range(120):
+        A.step_act(eps=1.0, seed=4, counter=k, autoreset=True)
+        H.step_act(eps=1.0, seed=4, counter=k, autoreset=True)
+        H.sync()
+        assert torch.equal(A.actions.cpu(), H.actions)
+        assert torch.equal(A.reward64.cpu(), H.reward64)
+        assert torch.equal(A.terminated.cpu(), H.terminated) and torch.equal(A.truncated.cpu(), H.truncated)
+        assert torch.equal(A.pos.cpu(), H.pos) and torch.equal(A.best_dir.cpu(), H.best_dir)
+        assert torch.equal(A.window, H.window) and torch.equal(A.obs6, H.obs6)
+    for k in range(20):  # one instance through step_host (the drop-ins' path)
+        a = int(k % 4)
+        acts = torch.full((B,), -1, dtype=torch.int32, device="cuda")
+        acts[0] = a
+        A.step(acts)
+        H.actions.fill_(-1)
+        H.step_host(a)
+        assert float(A.reward64[0]) == float(H.reward64[0]) and A.pos[0].tolist() == H.pos[0].tolist()
+    A.close()
+    H.close()
