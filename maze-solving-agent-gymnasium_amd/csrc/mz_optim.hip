@@ -176,7 +176,17 @@ static __global__ __launch_bounds__(1024) void k_colsum(const float* __restrict_
   const int c = blockIdx.x * 64 + cq * 4;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (c < m) {
-    for (int r = rg; r < n; r += 64) {
+    // 8 rows' loads in flight before their adds (same summation order): a load-add chain waited
+    // a round trip per row — 22 vs 9 us per call once the acting kernels share the chip
+    int r = rg;
+    for (; r + 7 * 64 < n; r += 8 * 64) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(g + (size_t)(r + 64 * u) * ld + c);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
+    }
+    for (; r < n; r += 64) {
       const float4 v = *reinterpret_cast<const float4*>(g + (size_t)r * ld + c);
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }

@@ -227,14 +227,29 @@ __global__ __launch_bounds__(256) void k_stem_bwd(const uint32_t* __restrict__ b
   float acc[NACC];
 #pragma unroll
   for (int k = 0; k < NACC; ++k) acc[k] = 0.0f;
-  for (int i = tid; i < CHUNK * NPOOL; i += blockDim.x) {
-    const int s = i / NPOOL, q = i - s * NPOOL, nn = n0 + s;
-    if (nn >= n) break;
-    const int j = c * NPOOL + q;
-    const uint32_t cd = code[(size_t)nn * FEAT + j];
+  // every code byte / gradient this thread reads, loaded before any is used (one round trip
+  // instead of one per item; the items are then summed in the same order)
+  constexpr int IT = (CHUNK * NPOOL + 255) / 256;
+  uint32_t cdv[IT];
+  float gv[IT];
+#pragma unroll
+  for (int u = 0; u < IT; ++u) {
+    const int i = tid + 256 * u, s = i / NPOOL, q = i - s * NPOOL, nn = n0 + s;
+    cdv[u] = 0u;  // class 0: contributes nothing
+    gv[u] = 0.0f;
+    if (i < CHUNK * NPOOL && nn < n) {
+      const int j = c * NPOOL + q;
+      cdv[u] = code[(size_t)nn * FEAT + j];
+      gv[u] = g[(size_t)nn * ld + j];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < IT; ++u) {
+    const int i = tid + 256 * u, s = i / NPOOL, q = i - s * NPOOL;
+    const uint32_t cd = cdv[u];
     const uint32_t cls = cd >> 2;
-    if (cls == 0u) continue;  // dropped: dropout backward gives 0
-    const float gs = g[(size_t)nn * ld + j] * scale;  // dropout backward: grad * mask * scale
+    if (cls == 0u) continue;  // dropped (or past the rows): dropout backward gives 0
+    const float gs = gv[u] * scale;  // dropout backward: grad * mask * scale
     const float gc = cls == 1u ? gs : gs * 0.01f;     // LeakyReLU backward
     const int py = q / 7, px = q - py * 7;
     const int y = 2 * py + (int)((cd >> 1) & 1u), x = 2 * px + (int)(cd & 1u);
@@ -267,8 +282,21 @@ __global__ void k_stem_reduce(const float* __restrict__ partial, int chunks, flo
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= 32 * NACC) return;
   const int c = t / NACC, k = t - c * NACC;
+  // 8 chunks' loads in flight before their adds (same order, so the same sums): the serial
+  // load-add chain waited a round trip per chunk — 111 us per call under the acting kernels'
+  // load against 12 us alone (profiles/r01l_train_kernel_stats.csv)
+  const float* pp = partial + (size_t)c * NACC + k;
+  const size_t cs = (size_t)32 * NACC;  // chunk stride
   float s = 0.0f;
-  for (int ch = 0; ch < chunks; ++ch) s += partial[((size_t)ch * 32 + c) * NACC + k];
+  int ch = 0;
+  for (; ch + 8 <= chunks; ch += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = pp[(size_t)(ch + u) * cs];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; ch < chunks; ++ch) s += pp[(size_t)ch * cs];
   if (k < 27) dw[c * 27 + k] = s;  // torch layout [32][3][3][3]: c*27 + ch*9 + ky*3 + kx
   else db[c] = s;
 }
