@@ -428,3 +428,44 @@ def test_host_scalars_match_device_outputs(mazerl):
         assert float(A.reward64[0]) == float(H.reward64[0]) and A.pos[0].tolist() == H.pos[0].tolist()
     A.close()
     H.close()
+
+
+@pytest.mark.parametrize("B", [32768, 16400])
+def test_large_batch_fused_autoreset_every_lane_vs_oracle(mazerl, B):
+    """Batches above 16,384 step with 16 instances per wave, the bench's path (fused act + step +
+    autoreset); 32,768 also takes the XCD-aware group map (grid a multiple of 8), 16,400 ends in
+    a partial group without it. Every lane of several whole groups (first, middle, last) is
+    replayed through the oracle, rewards as float64 ==, windows and positions exactly."""
+    import pyoracle as O
+    dim = 21
+    env = mazerl.VectorMazeEnv(B, dim, enrich=True, reward64=True, seed=0xC0FFEE)
+    groups = sorted({0, 1, (B // 16) // 2, (B - 1) // 16})
+    sample = [i for g in groups for i in range(16 * g, min(B, 16 * g + 16))]
+    ors = {}
+    for i in sample:
+        q = env.query(i)
+        ors[i] = O.Env(env.grid(i), (q["start_r"], q["start_c"]), (q["goal_r"], q["goal_c"]), False, True)
+        ors[i].reset()
+    was_done = {i: False for i in sample}
+    resets = 0
+    for k in range(150):
+        env.step_act(eps=1.0, seed=17, counter=k, autoreset=True)
+        a = env.actions.cpu().numpy()
+        r64 = env.reward64.cpu().numpy()
+        pos, bd = env.pos.cpu().numpy(), env.best_dir.cpu().numpy()
+        te, tr = env.terminated.cpu().numpy(), env.truncated.cpu().numpy()
+        win = env.window[sample].cpu().numpy()
+        for j, i in enumerate(sample):
+            if was_done[i]:
+                assert a[i] == -1, (k, i)
+                o = ors[i].reset()
+                resets += 1
+            else:
+                o = ors[i].step(int(a[i]))
+            assert r64[i] == o["reward"], (k, i)
+            assert tuple(pos[i]) == o["pos"] and tuple(bd[i]) == o["best_dir"], (k, i)
+            assert bool(te[i]) == o["terminated"] and bool(tr[i]) == o["truncated"], (k, i)
+            np.testing.assert_array_equal(win[j], o["window"].astype(np.float32))
+            was_done[i] = o["terminated"] or o["truncated"]
+    assert resets > 0
+    env.close()
