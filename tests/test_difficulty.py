@@ -29,3 +29,19 @@ def test_difficulty_matches_reference(diff):
             exact += d == m["difficulty"]
             total += 1
     assert total >= 200 and exact >= 0.95 * total
+
+
+def test_complexity_evaluation_dropin_matches_reference(diff):
+    """mazerl.lib...ComplexityEvaluation (the reference's class name and methods,
+    maze_complexity_evaluation.py:38-329) on the golden euclidean mazes: difficulty_of_maze()
+    == the reference's value (same tolerance as above); complexity_of_maze() is finite."""
+    from mazerl.lib.maze_difficulty_evaluation.maze_complexity_evaluation import ComplexityEvaluation
+    n = 0
+    for m in G.mazes("gen_euclid.npz"):
+        if math.isnan(m["difficulty"]):
+            continue
+        ce = ComplexityEvaluation(m["grid"].astype(int).tolist(), m["start"], m["goal"])
+        assert ce.difficulty_of_maze() == pytest.approx(m["difficulty"], rel=1e-15, abs=0)
+        assert math.isfinite(ce.complexity_of_maze())
+        n += 1
+    assert n >= 90  # the euclidean fixtures with a reference difficulty (N <= 41)

@@ -199,3 +199,30 @@ def test_dropin_constructor_matches_reference_after_seed(envs):
             env.close()
     finally:
         envs.BaseMazeEnv.ALGORITHM = saved
+
+
+def test_gen_maze_functions_match_reference_mazes(envs):
+    """mazerl.lib.maze_generation.gen_maze / gen_maze_no_border (maze_generation.py:6-56) after
+    random.seed(s): the reference's own mazes (the 240 golden ones: 3 algorithms x 5 sizes x 8
+    seeds), start / goal, gen_maze_no_border's difficulty on the bordered maze, and the global
+    random stream left where the reference leaves it (checked against the oracle's CPython
+    restatement). Even sizes raise IndexError (Q4)."""
+    import random
+    import pyoracle as O
+    from mazerl.lib.maze_generation import gen_maze, gen_maze_no_border
+    for name, fn, tor in (("gen_euclid.npz", gen_maze, False), ("gen_toroid.npz", gen_maze_no_border, True)):
+        for m in G.mazes(name):
+            algo = G.ALGOS[m["algo"]]
+            random.seed(m["seed"])
+            out = fn((m["n"], m["n"]), algo)
+            key = (name, algo, m["n"], m["seed"])
+            np.testing.assert_array_equal(np.array(out[2]), m["grid"], err_msg=str(key))
+            assert out[0] == m["start"] and out[1] == m["goal"], key
+            if tor and not np.isnan(m["difficulty"]):
+                assert out[3] == pytest.approx(m["difficulty"], rel=1e-15, abs=0), key
+            if not tor and m["n"] <= 41:
+                st = O.mt_state(m["seed"])
+                O.generate_py(m["n"], m["algo"], st)
+                assert list(st) == list(random.getstate()[1]), key
+    with pytest.raises(IndexError):
+        gen_maze((40, 40), "r-prim")
