@@ -46,7 +46,8 @@ class VectorMazeEnv:
         # host_scalars: the action and the per-instance scalars (reward, flags, position, best
         # dir) live in mapped page-locked host memory (mz_host_alloc) that the kernels read and
         # write directly — the single-env drop-ins' step() is then one launch + one stream sync
-        # with no copies. They are CPU tensors then; everything else stays in HBM.
+        # with no copies. They are CPU tensors then (valid until close(), which frees the
+        # memory: clone what you keep); everything else stays in HBM.
         self._host = None
         self._dptr = {}
         if host_scalars:
