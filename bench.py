@@ -47,9 +47,11 @@ def parse():
     ap.add_argument("--train-steps", type=int, default=2400,
                     help="DDQN vector steps for the win-rate half of the metric (0 = skip)")
     ap.add_argument("--eval-mazes", type=int, default=1000)
-    # learner: one update of 2,048 per vector step (same replay ratio as 4 x 512, a quarter of
-    # the kernels: 24.9 vs 15.6 M training env steps/s at the same win-rate)
-    ap.add_argument("--batch", type=int, default=2048, help="learner minibatch (win-rate leg)")
+    # learner: one update of 1,024 per vector step. Sweep at 2,400 vector steps (training env
+    # steps/s, greedy win-rate): 256: 58.0 M, 96.0 % / 512: 54.4 M, 95.0-96.0 % / 1,024: 50.6-
+    # 50.8 M, 96.2-96.4 % / 2,048: 40.4 M, 96.5 % / 4,096: 30.4 M, 96.2 % — the win-rate is on its
+    # plateau from 1,024 up, the GEMMs are not
+    ap.add_argument("--batch", type=int, default=1024, help="learner minibatch (win-rate leg)")
     ap.add_argument("--updates-per-step", type=int, default=1)
     ap.add_argument("--target-every", type=int, default=13, help="target sync every N updates")
     ap.add_argument("--overlap", type=int, default=1,
