@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=1024, help="learner minibatch (win-rate leg)")
     ap.add_argument("--updates-per-step", type=int, default=1)
     ap.add_argument("--target-every", type=int, default=13, help="target sync every N updates")
+    ap.add_argument("--greedy-rows", type=int, default=1,
+                    help="1: the acting forward runs over the instances whose epsilon draw says "
+                         "greedy only (dqn_agent.py:104-116); 0: over every instance")
     ap.add_argument("--overlap", type=int, default=1,
                     help="1: learner updates on a side HIP stream, overlapped with acting + env "
                          "step (acting weights one update behind); 0: sequential")
@@ -79,7 +82,8 @@ def win_rate(a, dev, rank=0, world=1):
     L = VectorDQNLearner(a.envs, dev, variant="ddqn", lr=1e-3, eps_start=0.95, eps_final=0.1,
                          eps_decay=decay, gamma=0.7, batch_size=a.batch, capacity=2_000_000,
                          updates_per_step=a.updates_per_step, target_every=a.target_every,
-                         allreduce=GradAllReduce() if world > 1 else None, overlap=bool(a.overlap))
+                         allreduce=GradAllReduce() if world > 1 else None, overlap=bool(a.overlap),
+                         greedy_rows=bool(a.greedy_rows))
     if world > 1:
         broadcast_params(L.source)
         L.target.load_state_dict(L.source.state_dict())
@@ -104,6 +108,8 @@ def win_rate(a, dev, rank=0, world=1):
             "updates": L.n_updates, "batch": a.batch, "updates_per_vector_step": a.updates_per_step,
             "learner_schedule": "side stream, overlapped (acting weights one update behind)"
                                 if L.overlap else "sequential",
+            "acting_rows": "greedy rows only (epsilon draw first, dqn_agent.py:104-116)"
+                           if L.greedy_rows else "every instance",
             "grad_allreduce": (f"{dist.get_backend()} ({'RCCL' if dist.get_backend() == 'nccl' else 'rehearsal'}), "
                                "one 8.56 MB fp32 bucket per update between two graph replays")
                               if world > 1 else None,

@@ -213,6 +213,23 @@ int mz_q_front(const uint32_t* bits_dev, const float* obs6_dev, int32_t n, const
                const float* conv_b_dev, float drop_p, uint64_t seed, uint64_t counter,
                uint16_t* feat_dev, int32_t ld, void* stream);
 
+/* mz_q_front over a row list: output row i is instance rows_dev[i] (i < n) of bits_dev / obs6_dev.
+ * With the list of mz_greedy_rows the acting forward runs over the rows that act greedily only
+ * (dqn_agent.py:104-116 evaluates source_net(state) only when `sample >= eps`). */
+int mz_q_front_rows(const uint32_t* bits_dev, const float* obs6_dev, const int32_t* rows_dev,
+                    int32_t n, const float* conv_w_dev, const float* conv_b_dev, float drop_p,
+                    uint64_t seed, uint64_t counter, uint16_t* feat_dev, int32_t ld, void* stream);
+
+/* Greedy-row list of the next fused act (mz_act / mz_step_act with the same eps, seed, counter;
+ * dqn_agent.py:104-116 draws `sample = random.random()` first and acts greedily iff
+ * sample >= eps): rows_dev[0 .. count) = the instances i < n that will take greedy_dev[i], in
+ * increasing order; count_dev [1] int32 (device) and, if count_host is not NULL, the same count
+ * into mapped host memory (mz_host_alloc) for the caller's GEMM sizes. scratch_dev: int32
+ * [ceil(n / 1024)]. Two launches, no atomics: the list is deterministic. */
+int mz_greedy_rows(const float* eps_dev, float eps_all, uint64_t seed, uint64_t counter, int32_t n,
+                   int32_t* scratch_dev, int32_t* rows_dev, int32_t* count_dev,
+                   int32_t* count_host, void* stream);
+
 /* The same conv stem in f32 for the LEARNER update (optimize_model, dqn_agent.py:121-157,
  * ddqn_agent.py:113-152; forward dqn_agent.py:47-57), forward and backward, from packed windows:
  * feat_dev [n][ld] f32 = [MaxPool2(Dropout(LeakyReLU(Conv3x3(window) + b))) in torch's flatten

@@ -37,6 +37,14 @@
 // less than the workgroup barrier that the shared table needs.
 #define MZ_SPW 1
 #endif
+// Timing probes (profiles/exp_probes.sh; never in the product build — each makes the step wrong):
+// MZ_PROBE mask bits: 1 no penalty-table staging, 2 no window-bit assembly, 4 no autoreset plane /
+// count work, 8 no per-instance output stores, 16 no f32 window stores, 32 window stores of a
+// constant (no LDS reads), 64 no state stores, 128 return at once (launch + dispatch floor),
+// 256 no level-2 loads
+#ifndef MZ_PROBE
+#define MZ_PROBE 0
+#endif
 // LDS words of a wave's window bits: ipw x 675 bits + funnel-shift slack
 __host__ __device__ constexpr int cat_words(int ipw) { return ipw * 675 / 32 + 2; }
 
@@ -189,7 +197,7 @@ __device__ inline void store_window_f32(const uint32_t* cat, float* out, int nb,
   for (; q + 7 * WAVE < nq; q += 8 * WAVE) {
     uint32_t w[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) w[u] = cat[(q >> 3) + 8 * u];
+    for (int u = 0; u < 8; ++u) w[u] = (MZ_PROBE & 32) ? (uint32_t)q * 0x9E3779B9u : cat[(q >> 3) + 8 * u];
 #pragma unroll
     for (int u = 0; u < 8; ++u) put(q + u * WAVE, w[u]);
   }
@@ -223,12 +231,22 @@ __device__ inline void dir_mask(uint32_t pw, uint32_t cw, bool tor, bool probs, 
 // epsilon-greedy with the reference exploration distribution (dqn_agent.py:104-116):
 // u < eps -> np.random.choice(4, p = mask / mask.sum()) by inverse CDF, else greedy.
 // ep / greedy: the instance's epsilon and greedy action (greedy < 0: always explore).
+// The exploration draw of instance e (sample = random.random(), dqn_agent.py:105): Philox(seed,
+// e, counter); u[0] -> `sample`, u[1] -> the masked-direction choice. act_draw and greedy_needed
+// (the greedy-row list) read the same words, so the list is exactly the instances that act greedily.
+__device__ inline void act_u(const MzAct& ap, int e, uint32_t u[4]) {
+  mz_philox(ap.seed, MZ_ACT_STREAM ^ ((uint64_t)e << 32), ap.counter, u);
+}
+__device__ inline bool act_greedy(const uint32_t u[4], float ep) {
+  const float ue = (float)(u[0] >> 8) * (1.0f / 16777216.0f);
+  return !(ue < ep);
+}
+
 __device__ inline int act_draw(const MzAct& ap, int e, float ep, int greedy, uint32_t pw,
                                uint32_t cw, bool tor) {
   uint32_t u[4];
-  mz_philox(ap.seed, MZ_ACT_STREAM ^ ((uint64_t)e << 32), ap.counter, u);
-  const float ue = (float)(u[0] >> 8) * (1.0f / 16777216.0f);
-  if (greedy >= 0 && !(ue < ep)) return greedy;
+  act_u(ap, e, u);
+  if (greedy >= 0 && act_greedy(u, ep)) return greedy;
   float m[4];
   dir_mask(pw, cw, tor, true, m);
   const float tot = m[0] + m[1] + m[2] + m[3];
@@ -306,7 +324,8 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
       araw = act[e];
     }
   }
-  if (load_pen) {
+  if (MZ_PROBE & 128) return;
+  if (load_pen && !(MZ_PROBE & 1)) {
     uint4* pl = reinterpret_cast<uint4*>(pen);
     if (MZ_SPW == 1) {
       const uint4* pv = reinterpret_cast<const uint4*>(d.pen_visit);
@@ -347,7 +366,7 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
   // ---- level 2
   const uint32_t tag = (sw >> MZ_STW_TAG_SHIFT) & 7u;  // the episode's visit-count tag
   uint32_t ncw = 0u;
-  if (mv || rst) ncw = d.cells[es * d.P * d.P + (size_t)tr * d.P + tc];  // cell word + visit count
+  if ((mv || rst) && !(MZ_PROBE & 256)) ncw = d.cells[es * d.P * d.P + (size_t)tr * d.P + tc];  // cell word + visit count
   const int cnt = rst ? 0 : mz_cell_count(ncw, tag);
   uint2 wr[win_it(IPWT)];  // strip pairs of the final window's rows
   int geo = 0;
@@ -358,7 +377,7 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
       const int j = it * (WAVE / 16) + (lane >> 4), i = lane & 15;
       const int g = __shfl(geo, j);
       wr[it] = make_uint2(0u, 0u);
-      if (j < nb && i < 15) wr[it] = *mz_strip_row(d, (size_t)(e0 + j), geo_st(g), geo_row<TOR>(g, i));
+      if (j < nb && i < 15 && !(MZ_PROBE & 256)) wr[it] = *mz_strip_row(d, (size_t)(e0 + j), geo_st(g), geo_row<TOR>(g, i));
     }
   }
   __syncthreads();  // pen[] (single-wave workgroup: an LDS wait, no s_barrier)
@@ -401,7 +420,7 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
 
   // ---- window bits in LDS (compute only: every global store of the step comes after, so no
   // wait in this kernel ever covers a store)
-  if (ENRICH) {
+  if (ENRICH && !(MZ_PROBE & 2)) {
     const int ps = (int)rst | ((vr + 1) << 8) | ((vc + 1) << 16);
     const int pg = gr | (gc << 8);
 #pragma unroll
@@ -421,7 +440,7 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
   }
 
   // ---- stores: state, per-instance outputs, then the windows
-  if (rst || trans) {
+  if ((rst || trans) && !(MZ_PROBE & 64)) {
     d.posw[e] = (uint32_t)r | ((uint32_t)c << 8) | ((uint32_t)nm << 16) | ((uint32_t)la << 18) |
                 ((uint32_t)done << 20);
     d.stw[e] = (uint32_t)steps | ((uint32_t)inv << 16) | (ntag << MZ_STW_TAG_SHIFT);
@@ -434,7 +453,7 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
           (tag << MZ_CELL_TAG_SHIFT);
     }
   }
-  if (live) {
+  if (live && !(MZ_PROBE & 8)) {
     if (ACT && ap.act_out) ap.act_out[e] = rst ? -1 : araw;
     int br, bc;
     best_dir(r, c, cw, N, TOR, br, bc);
@@ -449,10 +468,10 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
   if (ENRICH) {
     __syncthreads();
     if (o.window_bits) store_window_bits(cat, o.window_bits + (size_t)e0 * MZ_WINDOW_WORDS, nb, lane);
-    if (o.window) store_window_f32(cat, o.window + (size_t)e0 * 675, nb, lane);
+    if (o.window && !(MZ_PROBE & 16)) store_window_f32(cat, o.window + (size_t)e0 * 675, nb, lane);
   }
 
-  if (AR) {  // reset instances: visited plane = {start}; counts cleared when the tag wraps
+  if (AR && !(MZ_PROBE & 4)) {  // reset instances: visited plane = {start}; counts cleared when the tag wraps
     unsigned long long bal = __ballot(rst);
     const int sp = sr | (sc << 8) | ((int)ntag << 16) | (N << 19);
     while (bal) {
@@ -682,6 +701,59 @@ __global__ void k_mask(MzDev d, int probs, float* out4) {
   reinterpret_cast<float4*>(out4)[e] = make_float4(m[0], m[1], m[2], m[3]);
 }
 
+// ------------------------------------------------------------------------------------------
+// Greedy-row list (dqn_agent.py:104-116 draws `sample < eps` first and evaluates source_net(state)
+// only when it fails): the instances whose next fused act (same seed / counter / eps) takes
+// greedy_dev[i], in increasing instance order. Two launches, no atomics (a fixed order, so the
+// acting forward over the list is deterministic): per-1024-instance counts, then the list.
+constexpr int GR_BLOCK = 1024;
+__device__ inline bool greedy_needed(const MzAct& ap, int e) {
+  uint32_t u[4];
+  act_u(ap, e, u);
+  return act_greedy(u, ap.eps ? ap.eps[e] : ap.eps_all);
+}
+
+__global__ __launch_bounds__(GR_BLOCK) void k_greedy_count(MzAct ap, int n, int32_t* blk) {
+  const int e = blockIdx.x * GR_BLOCK + threadIdx.x;
+  const int c = __syncthreads_count(e < n && greedy_needed(ap, e));
+  if (threadIdx.x == 0) blk[blockIdx.x] = c;
+}
+
+__global__ __launch_bounds__(GR_BLOCK) void k_greedy_list(MzAct ap, int n, const int32_t* blk,
+                                                          int32_t* rows, int32_t* count,
+                                                          int32_t* count_host) {
+  __shared__ int wsum[GR_BLOCK / WAVE];
+  __shared__ int base;
+  const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+  const int e = blockIdx.x * GR_BLOCK + threadIdx.x;
+  const bool need = e < n && greedy_needed(ap, e);
+  const unsigned long long bal = __ballot(need);
+  if (lane == 0) wsum[w] = __popcll(bal);
+  if (w == 0) {  // this block's offset = the counts of the blocks before it; block 0: the total
+    int pre = 0, tot = 0;
+    for (int i = lane; i < (int)gridDim.x; i += WAVE) {
+      const int v = blk[i];
+      pre += i < (int)blockIdx.x ? v : 0;
+      tot += v;
+    }
+    for (int o = WAVE / 2; o; o >>= 1) {
+      pre += __shfl_xor(pre, o);
+      tot += __shfl_xor(tot, o);
+    }
+    if (lane == 0) {
+      base = pre;
+      if (blockIdx.x == 0) {
+        *count = tot;
+        if (count_host) *count_host = tot;
+      }
+    }
+  }
+  __syncthreads();
+  int off = base;
+  for (int i = 0; i < w; ++i) off += wsum[i];
+  if (need) rows[off + __popcll(bal & ((1ull << lane) - 1ull))] = e;
+}
+
 __global__ void k_act(MzDev d, MzAct ap) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= d.B) return;
@@ -855,6 +927,16 @@ hipError_t mz_launch_returns(const double* rew, int ld, const int32_t* rows, con
 
 hipError_t mz_launch_mask(const MzDev& d, int probs, float* out4, hipStream_t s) {
   hipLaunchKernelGGL(k_mask, dim3((d.B + 255) / 256), dim3(256), 0, s, d, probs, out4);
+  return hipGetLastError();
+}
+
+hipError_t mz_launch_greedy_rows(const MzAct& ap, int n, int32_t* blk, int32_t* rows,
+                                 int32_t* count, int32_t* count_host, hipStream_t s) {
+  const int blocks = (n + GR_BLOCK - 1) / GR_BLOCK;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_greedy_count, dim3(blocks), dim3(GR_BLOCK), 0, s, ap, n, blk);
+  hipLaunchKernelGGL(k_greedy_list, dim3(blocks), dim3(GR_BLOCK), 0, s, ap, n, blk, rows, count,
+                     count_host);
   return hipGetLastError();
 }
 

@@ -88,7 +88,8 @@ __device__ inline void wave_sync() {
 
 template <bool DROP>
 __global__ __launch_bounds__(WAVE * WPB) __attribute__((amdgpu_waves_per_eu(4, 8)))
-void k_qfront(const uint32_t* __restrict__ bits, const float* __restrict__ obs6, int n,
+void k_qfront(const uint32_t* __restrict__ bits, const float* __restrict__ obs6,
+              const int32_t* __restrict__ rows, int n,
               const float* __restrict__ w, const float* __restrict__ bias, uint32_t drop_thresh,
               float drop_scale, uint32_t key0, uint32_t key1, uint32_t* __restrict__ out, int ld) {
   __shared__ uint4 lut[256];                  // 8 patch bits -> 8 bf16 (0 / 1.0)
@@ -130,12 +131,18 @@ void k_qfront(const uint32_t* __restrict__ bits, const float* __restrict__ obs6,
 
   const int ld2 = ld >> 1;  // row pitch in uint32 (bf16 pairs)
   const int ngroups = (n + IPG - 1) / IPG;
-  // the group's 88 window words, loaded one group ahead (2 per lane) to hide HBM latency
+  // the group's 88 window words, loaded one group ahead (2 per lane) to hide HBM latency;
+  // with `rows`, output row i is instance rows[i] (the greedy-row list: only the rows that act
+  // greedily, dqn_agent.py:104-116)
+  auto word = [&](int g, int k) -> uint32_t {
+    if (!rows) return bits[(size_t)g * IPG * 22 + k];
+    const int inst = k / 22;
+    return bits[(size_t)rows[g * IPG + inst] * 22 + (k - inst * 22)];
+  };
   auto load_bits = [&](int g, uint32_t& x0, uint32_t& x1) {
     const int m = g < ngroups ? min(IPG, n - g * IPG) * 22 : 0;
-    const uint32_t* src = bits + (size_t)g * IPG * 22;
-    x0 = lane < m ? src[lane] : 0u;
-    x1 = lane + WAVE < m ? src[lane + WAVE] : 0u;
+    x0 = lane < m ? word(g, lane) : 0u;
+    x1 = lane + WAVE < m ? word(g, lane + WAVE) : 0u;
   };
   uint32_t nb0, nb1;
   const int gstride = gridDim.x * WPB;
@@ -233,7 +240,7 @@ void k_qfront(const uint32_t* __restrict__ bits, const float* __restrict__ obs6,
     const int tail = (ld - CONV_OUT) >> 1;
     for (int i = lane; i < ni * tail; i += WAVE) {
       const int inst = i / tail, k = 2 * (i - inst * tail);
-      const float* o = obs6 + (size_t)(e0 + inst) * 6;
+      const float* o = obs6 + (size_t)(rows ? rows[e0 + inst] : e0 + inst) * 6;
       const float lo = k < 6 ? o[k] : 0.0f, hi = k + 1 < 6 ? o[k + 1] : 0.0f;
       og[inst * ld2 + (CONV_OUT >> 1) + (k >> 1)] = bf16x2(lo, hi);
     }
@@ -242,9 +249,9 @@ void k_qfront(const uint32_t* __restrict__ bits, const float* __restrict__ obs6,
 
 }  // namespace
 
-hipError_t mz_launch_qfront(const uint32_t* bits, const float* obs6, int n, const float* w,
-                            const float* b, float drop_p, uint64_t seed, uint64_t counter,
-                            uint16_t* out, int ld, hipStream_t s) {
+hipError_t mz_launch_qfront(const uint32_t* bits, const float* obs6, const int32_t* rows, int n,
+                            const float* w, const float* b, float drop_p, uint64_t seed,
+                            uint64_t counter, uint16_t* out, int ld, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   // keep iff a 16-bit uniform >= thresh: P(drop) = thresh / 65536 (0.2 -> 13107, 0.19999695)
   const uint32_t thresh = drop_p > 0.0f ? (uint32_t)(drop_p * 65536.0f + 0.5f) : 0u;
@@ -255,10 +262,10 @@ hipError_t mz_launch_qfront(const uint32_t* bits, const float* obs6, int n, cons
   const int blocks = nb < 65536 ? nb : 65536;
   uint32_t* o = reinterpret_cast<uint32_t*>(out);
   if (thresh)
-    hipLaunchKernelGGL(k_qfront<true>, dim3(blocks), dim3(WAVE * WPB), 0, s, bits, obs6, n, w, b, thresh,
+    hipLaunchKernelGGL(k_qfront<true>, dim3(blocks), dim3(WAVE * WPB), 0, s, bits, obs6, rows, n, w, b, thresh,
                        scale, (uint32_t)k, (uint32_t)(k >> 32), o, ld);
   else
-    hipLaunchKernelGGL(k_qfront<false>, dim3(blocks), dim3(WAVE * WPB), 0, s, bits, obs6, n, w, b, 0u,
+    hipLaunchKernelGGL(k_qfront<false>, dim3(blocks), dim3(WAVE * WPB), 0, s, bits, obs6, rows, n, w, b, 0u,
                        1.0f, 0u, 0u, o, ld);
   return hipGetLastError();
 }

@@ -41,7 +41,7 @@ EXPORTS = ["mz_last_error", "mz_device_count", "mz_create", "mz_destroy", "mz_lo
            "mz_bank_create", "mz_bank_fill", "mz_bank_use", "mz_bank_consumed",
            "mz_stem_forward", "mz_stem_backward", "mz_stem_workspace_floats", "mz_adamw_flat",
            "mz_pair_surrogate", "mz_leaky_relu_bf16", "mz_colsum_f32",
-           "mz_replay_gather", "mz_host_alloc", "mz_host_free"]
+           "mz_replay_gather", "mz_host_alloc", "mz_host_free", "mz_q_front_rows", "mz_greedy_rows"]
 
 _lib = None
 
@@ -97,6 +97,10 @@ def load(build_if_missing=True):
     L.mz_bank_consumed.argtypes = [vp, C.c_int32, vp, vp]
     L.mz_q_front.argtypes = [vp, vp, C.c_int32, vp, vp, C.c_float, C.c_uint64, C.c_uint64, vp,
                              C.c_int32, vp]
+    L.mz_q_front_rows.argtypes = [vp, vp, vp, C.c_int32, vp, vp, C.c_float, C.c_uint64,
+                                  C.c_uint64, vp, C.c_int32, vp]
+    L.mz_greedy_rows.argtypes = [vp, C.c_float, C.c_uint64, C.c_uint64, C.c_int32, vp, vp, vp, vp,
+                                 vp]
     L.mz_stem_forward.argtypes = [vp, vp, C.c_int32, vp, vp, C.c_float, vp, C.c_uint32, vp,
                                   C.c_int32, vp, vp]
     L.mz_stem_backward.argtypes = [vp, vp, vp, C.c_int32, C.c_int32, C.c_float, vp, vp, vp, vp]

@@ -199,7 +199,7 @@ class VectorDQNLearner:
                  eps_decay=8000.0, gamma=0.7, batch_size=128, capacity=1_000_000,
                  updates_per_step=1, target_every=100, hidden_dim=1024, h_channels=32,
                  act_bf16=True, t_max=150, updates_per_epoch=100, allreduce=None, seed=0,
-                 use_graph=True, bit_stem=True, overlap=False):
+                 use_graph=True, bit_stem=True, overlap=False, greedy_rows=True):
         self.device = torch.device(device)
         torch.manual_seed(seed)
         self.variant = variant
@@ -238,6 +238,9 @@ class VectorDQNLearner:
         self.n_updates = 0
         self.last_loss = torch.zeros((), device=self.device)
         self.fused = None
+        # acting forward over the rows that act greedily only (agents/fused.py GreedyRows)
+        self.greedy_rows = bool(greedy_rows)
+        self._rows = None
         if self.device.type == "cuda" and act_bf16:
             from .fused import FusedQ
             self.fused = FusedQ(self.source, seed=seed)
@@ -268,13 +271,20 @@ class VectorDQNLearner:
         return self.eps_final + (self.eps_start - self.eps_final) * torch.exp(-self.steps_done / self.eps_decay)
 
     @torch.no_grad()
-    def greedy(self, obs6, window, bits=None):
+    def greedy(self, obs6, window, bits=None, act=None):
         """argmax_a Q_source(s) for every instance. With packed window bits on the GPU the acting
-        forward is the fused HIP stem + bf16 GEMMs (agents/fused.py); otherwise torch."""
+        forward is the fused HIP stem + bf16 GEMMs (agents/fused.py); otherwise torch.
+        act = (eps, seed, counter) of the fused act that will read the result: then only the
+        rows that act greedily are evaluated (dqn_agent.py:104-116 calls source_net only when
+        `sample >= eps`); the other entries are stale and unread."""
         if bits is not None and self.fused is not None:
-            if self._async:
-                return self.actor_fused[self._acting_slot()](obs6, bits).float().argmax(1)
-            return self.fused(obs6, bits).float().argmax(1)
+            f = self.actor_fused[self._acting_slot()] if self._async else self.fused
+            if act is not None and self.greedy_rows:
+                if self._rows is None:
+                    from .fused import GreedyRows
+                    self._rows = GreedyRows(bits.shape[0], self.device)
+                return self._rows(f, obs6, bits, *act)
+            return f(obs6, bits).float().argmax(1)
         if window is None:
             raise ValueError("greedy() needs the f32 window or window bits on the GPU")
         if self.act_bf16 and self.device.type == "cuda":

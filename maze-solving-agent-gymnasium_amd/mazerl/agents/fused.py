@@ -111,21 +111,32 @@ class FusedStem:
         self.counter = 0
         self.lib = N.load()
 
-    def __call__(self, obs6, bits):
-        n = bits.shape[0]
+    def __call__(self, obs6, bits, rows=None, n=None):
+        """Feature rows of every instance, or with `rows` (int32 instance ids) of rows[:n] only."""
         dev = bits.device
         if dev.type != "cuda":
             raise RuntimeError("the fused acting stem runs on the GPU only")
         assert bits.dtype == torch.int32 and bits.shape[1] == 22 and bits.is_contiguous()
         obs6 = obs6.contiguous()
-        assert obs6.dtype == torch.float32 and obs6.shape == (n, 6)
+        assert obs6.dtype == torch.float32 and obs6.shape == (bits.shape[0], 6)
+        if rows is None:
+            n = bits.shape[0]
+        else:
+            assert rows.dtype == torch.int32 and rows.is_contiguous() and rows.device == dev
+            assert 0 <= n <= rows.numel()
         w = self.conv.weight.detach().contiguous()
         b = self.conv.bias.detach().contiguous()
         p = float(self.dropout.p) if (self.dropout is not None and self.dropout.training) else 0.0
         feat = torch.empty(n, LD, dtype=torch.bfloat16, device=dev)
         stream = torch.cuda.current_stream(dev).cuda_stream
-        N.check(self.lib.mz_q_front(bits.data_ptr(), obs6.data_ptr(), n, w.data_ptr(), b.data_ptr(),
-                                    p, self.seed, self.counter, feat.data_ptr(), LD, stream))
+        if rows is None:
+            N.check(self.lib.mz_q_front(bits.data_ptr(), obs6.data_ptr(), n, w.data_ptr(),
+                                        b.data_ptr(), p, self.seed, self.counter, feat.data_ptr(),
+                                        LD, stream))
+        else:
+            N.check(self.lib.mz_q_front_rows(bits.data_ptr(), obs6.data_ptr(), rows.data_ptr(), n,
+                                             w.data_ptr(), b.data_ptr(), p, self.seed, self.counter,
+                                             feat.data_ptr(), LD, stream))
         self.counter += 1
         return feat
 
@@ -143,6 +154,58 @@ class FusedQ:
     @torch.no_grad()
     def __call__(self, obs6, bits):
         return self.head(self.stem(obs6, bits))
+
+    @torch.no_grad()
+    def rows(self, obs6, bits, rows, n):
+        """Q values [n, 4] of instances rows[:n]."""
+        return self.head(self.stem(obs6, bits, rows, n))
+
+
+class GreedyRows:
+    """The greedy-row list of the next fused act (mz_greedy_rows: the instances that will act
+    greedily with this eps / seed / counter, dqn_agent.py:104-116) and the acting forward over
+    those rows only; its count comes back to the host (one stream sync) to size the GEMMs.
+    `greedy` [n] int64 holds the argmax of the listed rows; the other entries are stale — the
+    fused act never reads them (it explores there)."""
+
+    BUCKET = 256  # GEMM rows rounded up (fewer distinct hipBLASLt shapes); extra rows are ignored
+
+    def __init__(self, n, device):
+        self.n = n
+        self.rows = torch.zeros(n, dtype=torch.int32, device=device)  # stale ids stay valid
+        self.scratch = torch.zeros((n + 1023) // 1024, dtype=torch.int32, device=device)
+        self.count = torch.zeros(1, dtype=torch.int32, device=device)
+        self.count_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self.greedy = torch.zeros(n, dtype=torch.int64, device=device)
+        self.event = torch.cuda.Event()
+        self.lib = N.load()
+        self.last_count = None
+
+    def select(self, eps, seed, counter):
+        """Build the list on the current stream; return its length (host-synchronised)."""
+        stream = torch.cuda.current_stream(self.rows.device).cuda_stream
+        eps_t = eps if torch.is_tensor(eps) else None
+        if eps_t is not None:
+            assert eps_t.dtype == torch.float32 and eps_t.is_contiguous() and eps_t.numel() == self.n
+        N.check(self.lib.mz_greedy_rows(eps_t.data_ptr() if eps_t is not None else None,
+                                        0.0 if eps_t is not None else float(eps),
+                                        seed & 0xFFFFFFFFFFFFFFFF, counter & 0xFFFFFFFFFFFFFFFF,
+                                        self.n, self.scratch.data_ptr(), self.rows.data_ptr(),
+                                        self.count.data_ptr(), None, stream))
+        self.count_host.copy_(self.count, non_blocking=True)
+        self.event.record()
+        self.event.synchronize()
+        self.last_count = int(self.count_host[0])
+        return self.last_count
+
+    @torch.no_grad()
+    def __call__(self, fused, obs6, bits, eps, seed, counter):
+        k = self.select(eps, seed, counter)
+        if k:
+            m = min(self.n, -(-k // self.BUCKET) * self.BUCKET)
+            q = fused.rows(obs6, bits, self.rows, m)
+            self.greedy.index_copy_(0, self.rows[:k].long(), q[:k].float().argmax(1))
+        return self.greedy
 
 
 class FusedActorCritic:

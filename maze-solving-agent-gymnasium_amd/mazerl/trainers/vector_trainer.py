@@ -3,7 +3,8 @@
 VectorOffPolicyTrainer.train() is NeuralOffPolicyTrainer.train (lib/trainers/off_policy_trainer.py
 :144-225) over B instances at once. Per vector step:
   greedy  = argmax Q_source(obs)   fused HIP conv stem on the window bits + bf16 MFMA GEMMs
-                                                      (agents/fused.py, dqn_agent.py:113-116)
+                                                      (agents/fused.py, dqn_agent.py:113-116),
+             over the instances whose epsilon draw of this step says "greedy" only
   step    = fused epsilon-greedy act + env step       (one k_step launch, per-instance epsilon)
   replay  <- (s, a, r, s') for every instance, s' = the step's (terminal) observation; terminal
              transitions bootstrap like the reference's
@@ -46,9 +47,12 @@ class VectorOffPolicyTrainer:
 
     def vector_step(self):
         env, L = self.env, self.learner
-        greedy = L.greedy(env.obs6, env.window, env.window_bits)
+        eps = L.epsilon()
+        # (eps, seed, counter) of this step's fused act: the acting forward runs over the rows
+        # that will act greedily only
+        greedy = L.greedy(env.obs6, env.window, env.window_bits, act=(eps, self.seed, self.counter))
         s6, sw = env.obs6.clone(), env.window_bits.clone()
-        env.step_act(eps=L.epsilon(), greedy=greedy, seed=self.seed, counter=self.counter)
+        env.step_act(eps=eps, greedy=greedy, seed=self.seed, counter=self.counter)
         self.counter += 1
         L.replay.push(s6, sw, env.actions, env.reward, env.obs6, env.window_bits)
         term = env.terminated.bool()

@@ -1,0 +1,118 @@
+"""Greedy-row acting (mz_greedy_rows + mz_q_front_rows, agents/fused.py GreedyRows).
+
+The reference draws `sample = random.random()` first and evaluates source_net(state) only when
+sample >= eps (dqn_agent.py:104-116). The vectorised learner builds the list of instances whose
+epsilon draw of the coming fused act says "greedy" and runs the acting forward over those rows
+only. Checked here:
+  * the list is exactly the set of instances the fused act (mz_step_act, same eps / seed /
+    counter) takes greedy_dev[i] for: every greedy entry is set to a sentinel action (7 — the
+    step uses 7 & 3, act_out reports 7), so act_out == 7 marks the greedy branch; sorted, no
+    duplicates, count on the device == host count; partial last block (B not a multiple of 1024),
+    scalar eps, eps 0 / 1;
+  * the row-indexed stem writes, bit for bit, the listed rows of the full stem (no dropout: the
+    DQN stem; the per-row computation does not depend on the row's position);
+  * GreedyRows' argmax equals the argmax of the full forward on the listed rows wherever the Q
+    margin exceeds bf16 GEMM rounding (the GEMM row count differs, so accumulation order may).
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _env(B, dim=21, seed=0x5EED0000):
+    import mazerl
+    return mazerl.VectorMazeEnv(B, dim, enrich=True, device="cuda:0", seed=seed, window=False,
+                                window_bits=True, done_list=False)
+
+
+def _rows(eps, seed, counter, n):
+    from mazerl.agents.fused import GreedyRows
+    gr = GreedyRows(n, torch.device("cuda", 0))
+    k = gr.select(eps, seed, counter)
+    torch.cuda.synchronize()
+    return gr, k
+
+
+@pytest.mark.parametrize("B", [1, 1000, 5000, 32768])
+def test_list_is_the_fused_act_greedy_branch(B):
+    env = _env(B)
+    g = torch.Generator(device="cuda").manual_seed(B)
+    for t, eps in enumerate([torch.rand(B, generator=g, device="cuda"), 0.3, 0.0, 1.0]):
+        seed, counter = 0xC0FFEE + t, 17 * t + 3
+        gr, k = _rows(eps, seed, counter, B)
+        rows = gr.rows[:k].long()
+        assert int(gr.count.item()) == k
+        if k > 1:
+            assert bool((rows[1:] > rows[:-1]).all())  # increasing: sorted, unique
+        sentinel = torch.full((B,), 7, dtype=torch.int64, device="cuda")
+        env.step_act(eps=eps, greedy=sentinel, seed=seed, counter=counter)
+        torch.cuda.synchronize()
+        took = (env.actions == 7).nonzero().flatten()
+        assert torch.equal(took, rows), (B, t, k, took.numel())
+        if not torch.is_tensor(eps):
+            if eps == 0.0:
+                assert k == B
+            if eps == 1.0:
+                assert k == 0
+    env.close()
+
+
+def test_row_stem_equals_full_stem_rows():
+    from mazerl.agents.fused import FusedQ
+    from mazerl.agents.nets import QNet
+    B = 3000
+    env = _env(B)
+    for k in range(5):  # some visited cells in the windows
+        env.step_act(eps=1.0, seed=5, counter=k)
+    torch.manual_seed(0)
+    net = QNet(variant="dqn").cuda()
+    fq = FusedQ(net, seed=3)
+    eps = torch.rand(B, generator=torch.Generator(device="cuda").manual_seed(1), device="cuda")
+    gr, k = _rows(eps, 9, 9, B)
+    assert 0 < k < B
+    full = fq.stem(env.obs6, env.window_bits)
+    part = fq.stem(env.obs6, env.window_bits, gr.rows, k)
+    torch.cuda.synchronize()
+    assert torch.equal(part, full[gr.rows[:k].long()])
+    env.close()
+
+
+def test_greedy_rows_argmax_matches_full_forward():
+    from mazerl.agents.fused import FusedQ, GreedyRows
+    from mazerl.agents.nets import QNet
+    B = 8192
+    env = _env(B, dim=41)
+    for k in range(7):
+        env.step_act(eps=1.0, seed=6, counter=k)
+    torch.manual_seed(1)
+    net = QNet(variant="dqn").cuda()
+    fq = FusedQ(net, seed=3)
+    eps = torch.rand(B, generator=torch.Generator(device="cuda").manual_seed(2), device="cuda")
+    gr = GreedyRows(B, torch.device("cuda", 0))
+    greedy = gr(fq, env.obs6, env.window_bits, eps, 21, 4)
+    k = gr.last_count
+    rows = gr.rows[:k].long()
+    q = fq(env.obs6, env.window_bits).float()[rows]
+    top2 = q.topk(2, dim=1).values
+    clear = (top2[:, 0] - top2[:, 1]) > 0.02 * top2[:, 0].abs().clamp_min(1e-3)
+    assert clear.float().mean() > 0.5
+    assert torch.equal(greedy[rows][clear], q.argmax(1)[clear])
+    env.close()
+
+
+def test_trainer_step_uses_greedy_rows():
+    """One training vector step through VectorOffPolicyTrainer with the row-list acting path."""
+    from mazerl.agents.dqn import VectorDQNLearner
+    from mazerl.trainers.vector_trainer import VectorOffPolicyTrainer
+    B = 2048
+    env = _env(B)
+    L = VectorDQNLearner(B, "cuda:0", variant="ddqn", batch_size=256, capacity=1 << 16,
+                         eps_decay=50.0)
+    tr = VectorOffPolicyTrainer(env, L, seed=3)
+    for _ in range(3):
+        tr.vector_step()
+    torch.cuda.synchronize()
+    assert L._rows is not None and 0 < L._rows.last_count <= B
+    assert int((env.actions < 0).sum()) == 0 and int((env.actions > 3).sum()) == 0
+    env.close()
