@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--greedy-rows", type=int, default=1,
                     help="1: the acting forward runs over the instances whose epsilon draw says "
                          "greedy only (dqn_agent.py:104-116); 0: over every instance")
+    ap.add_argument("--fused-bookkeeping", type=int, default=1,
+                    help="1: per-step trainer bookkeeping + replay push as HIP launches "
+                         "(mz_trainer_tick, mz_replay_push); 0: torch ops")
     ap.add_argument("--overlap", type=int, default=1,
                     help="1: learner updates on a side HIP stream, overlapped with acting + env "
                          "step (acting weights one update behind); 0: sequential")
@@ -87,7 +90,7 @@ def win_rate(a, dev, rank=0, world=1):
     if world > 1:
         broadcast_params(L.source)
         L.target.load_state_dict(L.source.state_dict())
-    tr = VectorOffPolicyTrainer(env, L, seed=3 + 7919 * rank)
+    tr = VectorOffPolicyTrainer(env, L, seed=3 + 7919 * rank, fused=bool(a.fused_bookkeeping))
     tr.train(20)  # warm-up: MIOpen / hipBLASLt first calls
     if world > 1:
         dist.barrier()

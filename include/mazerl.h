@@ -344,6 +344,56 @@ int mz_get_grid(mz_handle* h, int32_t env, uint8_t* grid_host /* [n][n] */);
 int mz_host_alloc(uint64_t bytes, int32_t device, void** host_out, void** dev_out);
 int mz_host_free(void* host);
 
+/* ---- Vectorised trainer bookkeeping (mazerl/trainers/vector_trainer.py; the training loop of
+ * NeuralOffPolicyTrainer.train, lib/trainers/off_policy_trainer.py:144-225, over n instances).
+ * The loop waits once per vector step for the greedy-row count; these calls keep the launches
+ * behind that wait few. */
+
+/* After a vector step: steps_done += 1, = 0 where terminated (off_policy_trainer.py:192, per
+ * instance); eps_out = eps_final + (eps_start - eps_final) * exp(-steps_done / eps_decay) in f32
+ * (dqn_agent.py:118-119 calculate_epsilon, as the learner's torch expression rounds it);
+ * wins += #terminated, episodes += #(terminated | truncated) (int64 device counters, nullable);
+ * and the greedy-row list of the NEXT fused act (seed, counter, eps_out): rows_dev / count_dev as
+ * mz_greedy_rows. scratch_dev: int32 [ceil(n / 1024)]. */
+int mz_trainer_tick(const uint8_t* term_dev, const uint8_t* trunc_dev, float* steps_done_dev,
+                    double eps_start, double eps_final, double eps_decay, float* eps_out_dev,
+                    int64_t* wins_dev, int64_t* episodes_dev, uint64_t seed, uint64_t counter,
+                    int32_t n, int32_t* scratch_dev, int32_t* rows_dev, int32_t* count_dev,
+                    void* stream);
+
+/* greedy_dev[rows_dev[i]] = argmax_a q_dev[i][a] (first maximum, torch.argmax) for
+ * i < min(*count_dev, m): the acting forward's bf16 Q rows [m][ldq] (dqn_agent.py:113-116
+ * `.max(1)[1]`) scattered to the listed instances; the list length is read on the device. */
+int mz_greedy_scatter(const uint16_t* q_dev, int32_t ldq, const int32_t* rows_dev,
+                      const int32_t* count_dev, int32_t m, int64_t* greedy_dev, void* stream);
+
+/* bf16 copy of the acting head's three Linear layers (dqn_agent.py:47-57 / ddqn_agent.py:40-52
+ * fc): w_l f32 [out_l][in_l] -> dw_l bf16 (round to nearest even, torch's .to(bfloat16)); fc1's
+ * first conv_out columns permuted from torch's channel-major flatten (c * Q + q, Q = conv_out /
+ * conv_ch) to the fused stem's position-major order (q * conv_ch + c), rows padded with zeros to
+ * ld0; biases b_l -> db_l. One launch. */
+int mz_head_bf16(const float* w0, const float* b0, const float* w1, const float* b1,
+                 const float* w2, const float* b2, int32_t out0, int32_t in0, int32_t out1,
+                 int32_t in1, int32_t out2, int32_t in2, int32_t ld0, int32_t conv_out,
+                 int32_t conv_ch, uint16_t* dw0, uint16_t* db0, uint16_t* dw1, uint16_t* db1,
+                 uint16_t* dw2, uint16_t* db2, void* stream);
+
+/* Replay ring push (lib/replay_memory.py:14 push, a vector step at once): ring rows ptr ..
+ * ptr + n - 1 (mod capacity) of s6 f32 [C][obs_dim], sw int32 [C][window_words], a int64 [C]
+ * (from int32 actions), r f32 [C], s6n, swn <- the n source rows; a NULL source leaves its array
+ * untouched (the state half can be written before the env step overwrites the observation). */
+int mz_replay_push(int32_t n, int64_t capacity, int64_t ptr, const float* obs6_src,
+                   const int32_t* bits_src, const int32_t* act_src, const float* rew_src,
+                   const float* obs6n_src, const int32_t* bitsn_src, float* s6_dev,
+                   int32_t* sw_dev, int64_t* a_dev, float* r_dev, float* s6n_dev,
+                   int32_t* swn_dev, int32_t obs_dim, int32_t window_words, void* stream);
+
+/* n uniform replay rows (random.sample of replay_memory.py:17, with replacement) among the newest
+ * n_avail ring rows ending at row `newest`: out_dev[i] = (newest - floor(u_i * n_avail)) mod
+ * capacity, u_i a 53-bit uniform from Philox(seed, i, counter). */
+int mz_replay_sample_idx(uint64_t seed, uint64_t counter, int64_t newest, int64_t n_avail,
+                         int64_t capacity, int64_t* out_dev, int32_t n, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

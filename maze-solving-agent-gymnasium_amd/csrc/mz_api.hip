@@ -688,3 +688,75 @@ int mz_host_free(void* host) {
 }
 
 }  // extern "C"
+
+
+// ---- trainer bookkeeping (mz_trainer.hip)
+int mz_trainer_tick(const uint8_t* term_dev, const uint8_t* trunc_dev, float* steps_done_dev,
+                    double eps_start, double eps_final, double eps_decay, float* eps_out_dev,
+                    int64_t* wins_dev, int64_t* episodes_dev, uint64_t seed, uint64_t counter,
+                    int32_t n, int32_t* scratch_dev, int32_t* rows_dev, int32_t* count_dev,
+                    void* stream) {
+  if (n < 0 || (n > 0 && (!term_dev || !trunc_dev || !steps_done_dev || !eps_out_dev ||
+                          !scratch_dev || !rows_dev || !count_dev)))
+    return fail(MZ_EINVAL, "bad arguments");
+  if (!(eps_decay > 0.0)) return fail(MZ_EINVAL, "eps_decay %g", eps_decay);
+  const float inv_decay = 1.0f / (float)eps_decay;  // as torch's division by a CPU scalar
+  MZ_HIP(mz_launch_tick(term_dev, trunc_dev, steps_done_dev, (float)eps_final,
+                        (float)(eps_start - eps_final), inv_decay, eps_out_dev,
+                        reinterpret_cast<unsigned long long*>(wins_dev),
+                        reinterpret_cast<unsigned long long*>(episodes_dev), seed, counter, n,
+                        scratch_dev, rows_dev, count_dev, static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
+int mz_greedy_scatter(const uint16_t* q_dev, int32_t ldq, const int32_t* rows_dev,
+                      const int32_t* count_dev, int32_t m, int64_t* greedy_dev, void* stream) {
+  if (m < 0 || ldq < 4 || (m > 0 && (!q_dev || !rows_dev || !count_dev || !greedy_dev)))
+    return fail(MZ_EINVAL, "bad arguments");
+  MZ_HIP(mz_launch_greedy_scatter(q_dev, ldq, rows_dev, count_dev, m, greedy_dev,
+                                  static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
+int mz_head_bf16(const float* w0, const float* b0, const float* w1, const float* b1,
+                 const float* w2, const float* b2, int32_t out0, int32_t in0, int32_t out1,
+                 int32_t in1, int32_t out2, int32_t in2, int32_t ld0, int32_t conv_out,
+                 int32_t conv_ch, uint16_t* dw0, uint16_t* db0, uint16_t* dw1, uint16_t* db1,
+                 uint16_t* dw2, uint16_t* db2, void* stream) {
+  if (!w0 || !b0 || !w1 || !b1 || !w2 || !b2 || !dw0 || !db0 || !dw1 || !db1 || !dw2 || !db2)
+    return fail(MZ_EINVAL, "bad arguments");
+  if (out0 <= 0 || out1 <= 0 || out2 <= 0 || in1 != out0 || in2 != out1 || in0 > ld0 ||
+      conv_ch <= 0 || conv_out < 0 || conv_out > in0 || conv_out % conv_ch != 0)
+    return fail(MZ_EINVAL, "head shapes");
+  MzHeadBf16 h{{w0, w1, w2}, {b0, b1, b2}, {dw0, dw1, dw2}, {db0, db1, db2},
+               {out0, out1, out2}, {in0, in1, in2}, ld0, conv_out, conv_ch};
+  MZ_HIP(mz_launch_head_bf16(h, static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
+int mz_replay_push(int32_t n, int64_t capacity, int64_t ptr, const float* obs6_src,
+                   const int32_t* bits_src, const int32_t* act_src, const float* rew_src,
+                   const float* obs6n_src, const int32_t* bitsn_src, float* s6_dev,
+                   int32_t* sw_dev, int64_t* a_dev, float* r_dev, float* s6n_dev,
+                   int32_t* swn_dev, int32_t obs_dim, int32_t window_words, void* stream) {
+  if (n < 0 || n > capacity || ptr < 0 || ptr >= capacity || obs_dim <= 0 || window_words <= 0)
+    return fail(MZ_EINVAL, "bad arguments");
+  const void* src[6] = {obs6_src, bits_src, act_src, rew_src, obs6n_src, bitsn_src};
+  void* dst[6] = {s6_dev, sw_dev, a_dev, r_dev, s6n_dev, swn_dev};
+  for (int j = 0; j < 6; ++j)
+    if (src[j] && !dst[j]) return fail(MZ_EINVAL, "replay array %d missing", j);
+  MzReplayPush p{{src[0], src[1], src[2], src[3], src[4], src[5]},
+                 {dst[0], dst[1], dst[2], dst[3], dst[4], dst[5]},
+                 {obs_dim, window_words, 1, 1, obs_dim, window_words}, n, capacity, ptr};
+  MZ_HIP(mz_launch_replay_push(p, static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
+int mz_replay_sample_idx(uint64_t seed, uint64_t counter, int64_t newest, int64_t n_avail,
+                         int64_t capacity, int64_t* out_dev, int32_t n, void* stream) {
+  if (n < 0 || capacity <= 0 || n_avail <= 0 || n_avail > capacity || (n > 0 && !out_dev))
+    return fail(MZ_EINVAL, "bad arguments");
+  MZ_HIP(mz_launch_replay_idx(seed, counter, newest, n_avail, capacity, out_dev, n,
+                              static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}

@@ -719,7 +719,8 @@ __global__ __launch_bounds__(GR_BLOCK) void k_greedy_count(MzAct ap, int n, int3
   if (threadIdx.x == 0) blk[blockIdx.x] = c;
 }
 
-__global__ __launch_bounds__(GR_BLOCK) void k_greedy_list(MzAct ap, int n, const int32_t* blk,
+__global__ __launch_bounds__(GR_BLOCK) void k_greedy_list(MzAct ap, int n,
+                                                          const int32_t* __restrict__ blk,
                                                           int32_t* rows, int32_t* count,
                                                           int32_t* count_host) {
   __shared__ int wsum[GR_BLOCK / WAVE];
@@ -930,14 +931,21 @@ hipError_t mz_launch_mask(const MzDev& d, int probs, float* out4, hipStream_t s)
   return hipGetLastError();
 }
 
+hipError_t mz_launch_greedy_list(const MzAct& ap, int n, const int32_t* blk, int32_t* rows,
+                                 int32_t* count, int32_t* count_host, hipStream_t s) {
+  const int blocks = (n + GR_BLOCK - 1) / GR_BLOCK;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_greedy_list, dim3(blocks), dim3(GR_BLOCK), 0, s, ap, n, blk, rows, count,
+                     count_host);
+  return hipGetLastError();
+}
+
 hipError_t mz_launch_greedy_rows(const MzAct& ap, int n, int32_t* blk, int32_t* rows,
                                  int32_t* count, int32_t* count_host, hipStream_t s) {
   const int blocks = (n + GR_BLOCK - 1) / GR_BLOCK;
   if (blocks == 0) return hipSuccess;
   hipLaunchKernelGGL(k_greedy_count, dim3(blocks), dim3(GR_BLOCK), 0, s, ap, n, blk);
-  hipLaunchKernelGGL(k_greedy_list, dim3(blocks), dim3(GR_BLOCK), 0, s, ap, n, blk, rows, count,
-                     count_host);
-  return hipGetLastError();
+  return mz_launch_greedy_list(ap, n, blk, rows, count, count_host, s);
 }
 
 hipError_t mz_launch_act(const MzDev& d, const MzAct& ap, hipStream_t s) {

@@ -52,3 +52,33 @@ hipError_t mz_launch_replay_gather(const int64_t* idx, int b, int64_t cap, const
                                    const uint32_t* sw, const int64_t* a, const float* r,
                                    const float* s6n, const uint32_t* swn, float* o6, uint32_t* ow,
                                    int64_t* oa, float* orw, hipStream_t s);
+
+// ---- trainer bookkeeping (mz_trainer.hip)
+struct MzHeadBf16 {  // acting head: f32 Linear weights / biases -> bf16 (fc1 permuted + padded)
+  const float* w[3];
+  const float* b[3];
+  uint16_t* dw[3];
+  uint16_t* db[3];
+  int out[3], in[3];
+  int ld0, conv_out, conv_ch;
+};
+struct MzReplayPush {  // ring rows ptr .. ptr + n - 1 <- n source rows, per array (NULL src: skip)
+  const void* src[6];  // obs6, bits, action (int32 -> int64), reward, next obs6, next bits
+  void* dst[6];
+  int words[6];        // 32-bit words per row
+  int n;
+  int64_t cap, ptr;
+};
+hipError_t mz_launch_greedy_list(const MzAct& ap, int n, const int32_t* blk, int32_t* rows,
+                                 int32_t* count, int32_t* count_host, hipStream_t s);
+hipError_t mz_launch_tick(const uint8_t* term, const uint8_t* trunc, float* steps_done,
+                          float eps_final, float eps_span, float inv_decay, float* eps_out,
+                          unsigned long long* wins, unsigned long long* episodes, uint64_t seed,
+                          uint64_t counter, int n, int32_t* scratch, int32_t* rows, int32_t* count,
+                          hipStream_t s);
+hipError_t mz_launch_greedy_scatter(const uint16_t* q, int ldq, const int32_t* rows,
+                                    const int32_t* count, int m, int64_t* greedy, hipStream_t s);
+hipError_t mz_launch_head_bf16(const MzHeadBf16& h, hipStream_t s);
+hipError_t mz_launch_replay_push(const MzReplayPush& p, hipStream_t s);
+hipError_t mz_launch_replay_idx(uint64_t seed, uint64_t counter, int64_t newest, int64_t n_avail,
+                                int64_t cap, int64_t* out, int n, hipStream_t s);

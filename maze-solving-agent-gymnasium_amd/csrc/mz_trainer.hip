@@ -1,0 +1,219 @@
+// mz_trainer.hip — the vectorised DQN/DDQN trainer's per-vector-step bookkeeping as few launches.
+//
+// The training loop (mazerl/trainers/vector_trainer.py, NeuralOffPolicyTrainer.train of
+// lib/trainers/off_policy_trainer.py:144-225 over B instances) waits once per vector step for the
+// length of the greedy-row list (the GEMM sizes of the acting forward), so every launch the host
+// issues after that wait is on the critical path. These kernels replace ~30 small torch launches:
+//
+//   k_tick_count     steps_done += 1, = 0 on a win (off_policy_trainer.py:192); the next step's
+//                    epsilon (dqn_agent.py:118-119, f32 as the learner computed it with torch);
+//                    win / episode counters; per-block counts of the next greedy-row list (the
+//                    list itself is k_greedy_list of mz_env.hip, same draw as the fused act)
+//   k_greedy_scatter argmax of the acting forward's Q rows (first maximum, torch.argmax) written
+//                    to the listed instances' greedy slots; reads the list length on the device
+//   k_head_bf16      the acting head's bf16 weights from the f32 parameters (fc1 columns
+//                    permuted to the fused stem's position-major feature order and zero-padded)
+//   k_replay_push    ring rows ptr .. ptr + n - 1 of the replay's six arrays <- a vector step
+//   k_replay_idx     uniform sample rows over the newest n_avail ring rows (Philox)
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "mz_common.h"
+#include "mz_kernels.h"
+
+namespace {
+
+constexpr int TB = 1024;  // = GR_BLOCK of the greedy-row list (mz_env.hip): same per-block counts
+constexpr int W = 64;
+
+__device__ inline float eps_of(float sd, float eps_final, float eps_span, float inv_decay) {
+  // torch: eps_final + (eps_start - eps_final) * torch.exp(-steps_done / eps_decay), f32 ops each
+  // rounded (no contraction); torch divides by a CPU scalar as a multiply by its f32 reciprocal
+  const float x = __fmul_rn(-sd, inv_decay);
+  return __fadd_rn(eps_final, __fmul_rn(eps_span, expf(x)));
+}
+
+__global__ __launch_bounds__(TB) void k_tick_count(const uint8_t* __restrict__ term,
+                                                   const uint8_t* __restrict__ trunc,
+                                                   float* __restrict__ steps_done, float eps_final,
+                                                   float eps_span, float inv_decay,
+                                                   float* __restrict__ eps_out,
+                                                   unsigned long long* wins,
+                                                   unsigned long long* episodes, uint64_t seed,
+                                                   uint64_t counter, int n, int32_t* blk) {
+  __shared__ int ws[TB / W], es[TB / W];
+  const int e = blockIdx.x * TB + threadIdx.x;
+  const int lane = threadIdx.x & (W - 1), w = threadIdx.x / W;
+  bool need = false, won = false, done = false;
+  if (e < n) {
+    won = term[e] != 0;
+    done = won || trunc[e] != 0;
+    const float sd = won ? 0.0f : steps_done[e] + 1.0f;
+    steps_done[e] = sd;
+    const float ep = eps_of(sd, eps_final, eps_span, inv_decay);
+    eps_out[e] = ep;
+    uint32_t u[4];
+    mz_philox(seed, MZ_ACT_STREAM ^ ((uint64_t)e << 32), counter, u);  // act_u (mz_env.hip)
+    need = !((float)(u[0] >> 8) * (1.0f / 16777216.0f) < ep);          // act_greedy
+  }
+  const int c = __syncthreads_count(need);
+  const unsigned long long bw = __ballot(won), bd = __ballot(done);
+  if (lane == 0) {
+    ws[w] = __popcll(bw);
+    es[w] = __popcll(bd);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    blk[blockIdx.x] = c;
+    int sw = 0, se = 0;
+    for (int i = 0; i < TB / W; ++i) {
+      sw += ws[i];
+      se += es[i];
+    }
+    if (wins && sw) atomicAdd(wins, (unsigned long long)sw);
+    if (episodes && se) atomicAdd(episodes, (unsigned long long)se);
+  }
+}
+
+__device__ inline float bf16f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+
+__global__ void k_greedy_scatter(const uint16_t* __restrict__ q, int ldq,
+                                 const int32_t* __restrict__ rows, const int32_t* __restrict__ count,
+                                 int m, int64_t* __restrict__ greedy) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int k = min(*count, m);
+  if (i >= k) return;
+  const uint16_t* r = q + (size_t)i * ldq;
+  int best = 0;
+  float bv = bf16f(r[0]);
+  for (int a = 1; a < 4; ++a) {  // first maximum; NaN counts as the maximum (torch.argmax)
+    const float v = bf16f(r[a]);
+    if (!isnan(bv) && (v > bv || isnan(v))) {
+      best = a;
+      bv = v;
+    }
+  }
+  greedy[rows[i]] = best;
+}
+
+__device__ inline uint16_t bf16_rne(float f) {  // torch's float -> bfloat16 (round to nearest even)
+  const uint32_t u = __float_as_uint(f);
+  if ((u & 0x7FFFFFFFu) > 0x7F800000u) return (uint16_t)((u >> 16) | 0x40u);  // quiet NaN
+  return (uint16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+
+__global__ __launch_bounds__(256) void k_head_bf16(MzHeadBf16 h) {
+  const int64_t n0 = (int64_t)h.out[0] * h.ld0;
+  const int64_t n1 = (int64_t)h.out[1] * h.in[1];
+  const int64_t n2 = (int64_t)h.out[2] * h.in[2];
+  const int64_t total = n0 + n1 + n2 + h.out[0] + h.out[1] + h.out[2];
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    int64_t k = t;
+    if (k < n0) {  // fc1: row o, column j of the padded, permuted [out0, ld0] weight
+      const int o = (int)(k / h.ld0), j = (int)(k - (int64_t)o * h.ld0);
+      float v = 0.0f;
+      if (j < h.conv_out) {  // kernel feature j = q * C + c  <-  torch column c * Q + q
+        const int c = j % h.conv_ch, q = j / h.conv_ch;
+        v = h.w[0][(size_t)o * h.in[0] + (size_t)c * (h.conv_out / h.conv_ch) + q];
+      } else if (j < h.in[0]) {
+        v = h.w[0][(size_t)o * h.in[0] + j];
+      }
+      h.dw[0][k] = bf16_rne(v);
+      continue;
+    }
+    k -= n0;
+    if (k < n1) { h.dw[1][k] = bf16_rne(h.w[1][k]); continue; }
+    k -= n1;
+    if (k < n2) { h.dw[2][k] = bf16_rne(h.w[2][k]); continue; }
+    k -= n2;
+    for (int l = 0; l < 3; ++l) {
+      if (k < h.out[l]) { h.db[l][k] = bf16_rne(h.b[l][k]); break; }
+      k -= h.out[l];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_replay_push(MzReplayPush p) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  for (int j = 0; j < 6; ++j) {
+    if (!p.src[j]) continue;
+    const int wds = p.words[j];
+    const int64_t tot = (int64_t)p.n * wds;
+    for (int64_t t = t0; t < tot; t += stride) {
+      const int64_t r = t / wds, c = t - r * wds;
+      int64_t dr = p.ptr + r;
+      if (dr >= p.cap) dr -= p.cap;
+      if (j == 2) {  // action: int32 -> int64 ring
+        reinterpret_cast<int64_t*>(p.dst[j])[dr] = reinterpret_cast<const int32_t*>(p.src[j])[r];
+      } else {
+        reinterpret_cast<uint32_t*>(p.dst[j])[dr * wds + c] =
+            reinterpret_cast<const uint32_t*>(p.src[j])[t];
+      }
+    }
+  }
+}
+
+__global__ void k_replay_idx(uint64_t seed, uint64_t counter, int64_t newest, int64_t n_avail,
+                             int64_t cap, int64_t* __restrict__ out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t u[4];
+  mz_philox(seed, MZ_REPLAY_STREAM ^ ((uint64_t)i << 32), counter, u);
+  // 53-bit uniform in [0, 1) -> one of the newest n_avail rows, ending at ring row `newest`
+  const double x = (double)(((uint64_t)u[0] << 21) ^ (u[1] >> 11)) * (1.0 / 9007199254740992.0);
+  int64_t r = newest - (int64_t)(x * (double)n_avail);
+  r %= cap;
+  if (r < 0) r += cap;
+  out[i] = r;
+}
+
+}  // namespace
+
+hipError_t mz_launch_tick(const uint8_t* term, const uint8_t* trunc, float* steps_done,
+                          float eps_final, float eps_span, float inv_decay, float* eps_out,
+                          unsigned long long* wins, unsigned long long* episodes, uint64_t seed,
+                          uint64_t counter, int n, int32_t* scratch, int32_t* rows, int32_t* count,
+                          hipStream_t s) {
+  const int blocks = (n + TB - 1) / TB;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_tick_count, dim3(blocks), dim3(TB), 0, s, term, trunc, steps_done, eps_final,
+                     eps_span, inv_decay, eps_out, wins, episodes, seed, counter, n, scratch);
+  MzAct ap{eps_out, 0.0f, nullptr, seed, counter, nullptr};
+  return mz_launch_greedy_list(ap, n, scratch, rows, count, nullptr, s);
+}
+
+hipError_t mz_launch_greedy_scatter(const uint16_t* q, int ldq, const int32_t* rows,
+                                    const int32_t* count, int m, int64_t* greedy, hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_greedy_scatter, dim3((m + 255) / 256), dim3(256), 0, s, q, ldq, rows, count,
+                     m, greedy);
+  return hipGetLastError();
+}
+
+hipError_t mz_launch_head_bf16(const MzHeadBf16& h, hipStream_t s) {
+  const int64_t total = (int64_t)h.out[0] * h.ld0 + (int64_t)h.out[1] * h.in[1] +
+                        (int64_t)h.out[2] * h.in[2] + h.out[0] + h.out[1] + h.out[2];
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(k_head_bf16, dim3((unsigned)blocks), dim3(256), 0, s, h);
+  return hipGetLastError();
+}
+
+hipError_t mz_launch_replay_push(const MzReplayPush& p, hipStream_t s) {
+  if (p.n <= 0) return hipSuccess;
+  int64_t blocks = ((int64_t)p.n * 22 + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(k_replay_push, dim3((unsigned)blocks), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t mz_launch_replay_idx(uint64_t seed, uint64_t counter, int64_t newest, int64_t n_avail,
+                                int64_t cap, int64_t* out, int n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_replay_idx, dim3((n + 255) / 256), dim3(256), 0, s, seed, counter, newest,
+                     n_avail, cap, out, n);
+  return hipGetLastError();
+}

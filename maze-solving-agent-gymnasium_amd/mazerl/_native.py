@@ -41,7 +41,9 @@ EXPORTS = ["mz_last_error", "mz_device_count", "mz_create", "mz_destroy", "mz_lo
            "mz_bank_create", "mz_bank_fill", "mz_bank_use", "mz_bank_consumed",
            "mz_stem_forward", "mz_stem_backward", "mz_stem_workspace_floats", "mz_adamw_flat",
            "mz_pair_surrogate", "mz_leaky_relu_bf16", "mz_colsum_f32",
-           "mz_replay_gather", "mz_host_alloc", "mz_host_free", "mz_q_front_rows", "mz_greedy_rows"]
+           "mz_replay_gather", "mz_host_alloc", "mz_host_free", "mz_q_front_rows", "mz_greedy_rows",
+           "mz_trainer_tick", "mz_greedy_scatter", "mz_head_bf16", "mz_replay_push",
+           "mz_replay_sample_idx"]
 
 _lib = None
 
@@ -101,6 +103,14 @@ def load(build_if_missing=True):
                                   C.c_uint64, vp, C.c_int32, vp]
     L.mz_greedy_rows.argtypes = [vp, C.c_float, C.c_uint64, C.c_uint64, C.c_int32, vp, vp, vp, vp,
                                  vp]
+    L.mz_trainer_tick.argtypes = [vp, vp, vp, C.c_double, C.c_double, C.c_double, vp, vp, vp,
+                                  C.c_uint64, C.c_uint64, C.c_int32, vp, vp, vp, vp]
+    L.mz_greedy_scatter.argtypes = [vp, C.c_int32, vp, vp, C.c_int32, vp, vp]
+    L.mz_head_bf16.argtypes = [vp] * 6 + [C.c_int32] * 9 + [vp] * 7
+    L.mz_replay_push.argtypes = [C.c_int32, C.c_int64, C.c_int64] + [vp] * 12 + [C.c_int32,
+                                                                                 C.c_int32, vp]
+    L.mz_replay_sample_idx.argtypes = [C.c_uint64, C.c_uint64, C.c_int64, C.c_int64, C.c_int64,
+                                       vp, C.c_int32, vp]
     L.mz_stem_forward.argtypes = [vp, vp, C.c_int32, vp, vp, C.c_float, vp, C.c_uint32, vp,
                                   C.c_int32, vp, vp]
     L.mz_stem_backward.argtypes = [vp, vp, vp, C.c_int32, C.c_int32, C.c_float, vp, vp, vp, vp]

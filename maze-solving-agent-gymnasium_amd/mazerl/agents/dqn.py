@@ -262,6 +262,8 @@ class VectorDQNLearner:
             self._acting = None  # slot greedy() reads
             self._idx = None     # [2][K, batch] sample indices, written on the main stream
             self._par = 0
+            self._sample_seed = 0x5A3B1E + 7919 * int(seed)
+            self._sample_counter = 0
 
     @property
     def supports_bits(self):
@@ -283,7 +285,7 @@ class VectorDQNLearner:
                 if self._rows is None:
                     from .fused import GreedyRows
                     self._rows = GreedyRows(bits.shape[0], self.device)
-                return self._rows(f, obs6, bits, *act)
+                return self._rows(f, obs6, bits, *act)  # (waits for the list's count)
             return f(obs6, bits).float().argmax(1)
         if window is None:
             raise ValueError("greedy() needs the f32 window or window bits on the GPU")
@@ -293,6 +295,30 @@ class VectorDQNLearner:
         else:
             q = self.source((obs6, window))
         return q.float().argmax(1)
+
+    def tick(self, term, trunc, wins, episodes, seed, counter):
+        """The trainer's per-step bookkeeping in one HIP launch pair (mz_trainer_tick):
+        steps_done += 1 / = 0 on a win, wins / episodes counters, the next act's epsilon (returned)
+        and its greedy-row list, issued so that its count reaches the host while the stream runs
+        the work behind it. None when this learner acts without the row list (the trainer then
+        does the bookkeeping with torch)."""
+        if self.fused is None or not self.greedy_rows:
+            return None
+        if self._rows is None:
+            from .fused import GreedyRows
+            self._rows = GreedyRows(self.steps_done.numel(), self.device)
+        return self._rows.tick(term, trunc, self.steps_done, self.eps_start, self.eps_final,
+                               self.eps_decay, wins, episodes, seed, counter)
+
+    def prepare_greedy(self, eps, seed, counter):
+        """Issue the greedy-row list of a coming greedy(act=(eps, seed, counter)) call now (its
+        count then reaches the host while the stream runs the work queued behind it)."""
+        if self.fused is None or not self.greedy_rows:
+            return
+        if self._rows is None:
+            from .fused import GreedyRows
+            self._rows = GreedyRows(self.steps_done.numel(), self.device)
+        self._rows.issue(eps, seed, counter)
 
     def update(self, expand, reserve=0):
         """K updates (graph replays). With overlap, once the graphs exist, they are issued on the
@@ -343,8 +369,7 @@ class VectorDQNLearner:
         while len(self._published) > 1 or (self._acting is None and self._published):
             slot, ev = self._published.popleft()
             M.wait_event(ev)
-            self._acting = slot
-            self.actor_fused[slot].invalidate()
+            self._acting = slot  # its bf16 head was rebuilt on S right after the snapshot
         return self._acting
 
     def _start_async(self):
@@ -352,7 +377,7 @@ class VectorDQNLearner:
         with torch.no_grad():
             for a, f in zip(self.actors, self.actor_fused):
                 copy_flat(a, self.source)
-                f.invalidate()
+                f.refresh()
         K, b = self.updates_per_step, self.batch_size
         self._idx = [torch.zeros(K, b, dtype=torch.int64, device=self.device) for _ in range(2)]
         self._idx_ev = [None, None]
@@ -372,9 +397,12 @@ class VectorDQNLearner:
         if self._idx_ev[slot] is not None:
             M.wait_event(self._idx_ev[slot])  # the last update that read this index buffer
         idx = self._idx[slot]
-        u = torch.rand(idx.shape, dtype=torch.float64, device=self.device)
-        torch.sub(rp.ptr - 1, (u * n_avail).to(torch.int64), out=idx)
-        idx.remainder_(rp.capacity)  # the newest n_avail rows, ending at ptr - 1
+        # the newest n_avail rows, ending at ptr - 1: one Philox launch (mz_replay_sample_idx)
+        from .. import _native as N
+        N.check(N.load().mz_replay_sample_idx(self._sample_seed, self._sample_counter, rp.ptr - 1,
+                                              n_avail, rp.capacity, idx.data_ptr(), idx.numel(),
+                                              M.cuda_stream))
+        self._sample_counter += 1
         if self._acting == slot:  # greedy() must switch to a newer snapshot before reading again
             self._acting = None
         S.wait_stream(M)  # push(t), the indices, and every greedy() that read this slot
@@ -392,6 +420,7 @@ class VectorDQNLearner:
                     self.sched.step()
             with torch.no_grad():
                 copy_flat(self.actors[slot], self.source)
+                self.actor_fused[slot].refresh()  # bf16 head of the snapshot, on S
             ev = torch.cuda.Event()
             ev.record(S)
         self._idx_ev[slot] = ev

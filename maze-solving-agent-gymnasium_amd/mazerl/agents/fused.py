@@ -52,7 +52,9 @@ def _act_fn(m):
 class _Head:
     """bf16 copy of a Linear -> act -> Linear -> act -> Linear stack; the first weight padded to LD
     columns. Refreshed when the f32 parameters changed: eager optimizer steps bump `_version`;
-    updates replayed from a captured HIP graph do not, so their owner calls invalidate()."""
+    updates replayed from a captured HIP graph do not, so their owner calls invalidate(). On the
+    GPU the copy is one mz_head_bf16 launch into persistent buffers (refresh(force=True) on a side
+    stream right after a weight snapshot keeps it off the acting stream)."""
 
     def __init__(self, seq):
         self.seq = seq
@@ -64,26 +66,46 @@ class _Head:
         l0 = self.lin[0]
         if l0.in_features > LD:
             raise ValueError(f"first Linear has {l0.in_features} inputs > {LD}")
-        self.w0 = torch.zeros(l0.out_features, LD, dtype=torch.bfloat16, device=l0.weight.device)
-        self.perm = feature_perm(l0.weight.device)
+        dev = l0.weight.device
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        self.w0 = torch.zeros(l0.out_features, LD, **bf)
+        self.perm = feature_perm(dev)
+        self._w = [(self.w0, torch.empty(l0.out_features, **bf))] + \
+                  [(torch.empty(l.out_features, l.in_features, **bf), torch.empty(l.out_features, **bf))
+                   for l in self.lin[1:]]
         self._ver = None
-        self._w = None
+        self._lib = N.load() if dev.type == "cuda" else None
 
     def invalidate(self):
         self._ver = None
 
-    def _refresh(self):
+    def _refresh(self, force=False):
         ver = tuple(p._version for l in self.lin for p in (l.weight, l.bias))
-        if ver == self._ver and self._w is not None:
+        if ver == self._ver and not force:
             return
         l0, l1, l2 = self.lin
-        w = l0.weight.detach()
-        self.w0[:, :CONV_OUT].copy_(w.index_select(1, self.perm))  # kernel feature order
-        self.w0[:, CONV_OUT:l0.in_features].copy_(w[:, CONV_OUT:])
-        self._w = [(self.w0, l0.bias.detach().to(torch.bfloat16)),
-                   (l1.weight.detach().to(torch.bfloat16), l1.bias.detach().to(torch.bfloat16)),
-                   (l2.weight.detach().to(torch.bfloat16), l2.bias.detach().to(torch.bfloat16))]
+        if self._lib is not None:
+            src = [t.detach() for l in self.lin for t in (l.weight, l.bias)]
+            assert all(t.is_contiguous() and t.dtype == torch.float32 for t in src)
+            (w0, b0), (w1, b1), (w2, b2) = self._w
+            N.check(self._lib.mz_head_bf16(
+                *[t.data_ptr() for t in src], l0.out_features, l0.in_features, l1.out_features,
+                l1.in_features, l2.out_features, l2.in_features, LD, CONV_OUT, 32,
+                w0.data_ptr(), b0.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(),
+                b2.data_ptr(), torch.cuda.current_stream(w0.device).cuda_stream))
+        else:
+            w = l0.weight.detach()
+            self.w0[:, :CONV_OUT].copy_(w.index_select(1, self.perm))  # kernel feature order
+            self.w0[:, CONV_OUT:l0.in_features].copy_(w[:, CONV_OUT:])
+            for (dw, db), l in zip(self._w, self.lin):
+                if dw is not self.w0:
+                    dw.copy_(l.weight.detach())
+                db.copy_(l.bias.detach())
         self._ver = ver
+
+    def refresh(self):
+        """Rebuild the bf16 copy now, on the current stream (after a weight snapshot)."""
+        self._refresh(force=True)
 
     def __call__(self, feat):
         self._refresh()
@@ -151,6 +173,9 @@ class FusedQ:
     def invalidate(self):
         self.head.invalidate()
 
+    def refresh(self):
+        self.head.refresh()
+
     @torch.no_grad()
     def __call__(self, obs6, bits):
         return self.head(self.stem(obs6, bits))
@@ -181,8 +206,10 @@ class GreedyRows:
         self.lib = N.load()
         self.last_count = None
 
-    def select(self, eps, seed, counter):
-        """Build the list on the current stream; return its length (host-synchronised)."""
+    def issue(self, eps, seed, counter):
+        """Launch the list kernels and the count's copy to the host on the current stream; the
+        host reads it later (select). Issued early — right after the bookkeeping that fixes the
+        next step's epsilon — the copy has landed by the time the next acting forward needs it."""
         stream = torch.cuda.current_stream(self.rows.device).cuda_stream
         eps_t = eps if torch.is_tensor(eps) else None
         if eps_t is not None:
@@ -194,6 +221,15 @@ class GreedyRows:
                                         self.count.data_ptr(), None, stream))
         self.count_host.copy_(self.count, non_blocking=True)
         self.event.record()
+        self._issued = (eps_t.data_ptr() if eps_t is not None else float(eps), seed, counter)
+
+    def select(self, eps, seed, counter):
+        """The list for (eps, seed, counter) — issued now unless issue() already did — and its
+        length (waits for the count's copy)."""
+        key = (eps.data_ptr() if torch.is_tensor(eps) else float(eps), seed, counter)
+        if getattr(self, "_issued", None) != key:
+            self.issue(eps, seed, counter)
+        self._issued = None
         self.event.synchronize()
         self.last_count = int(self.count_host[0])
         return self.last_count
@@ -204,8 +240,35 @@ class GreedyRows:
         if k:
             m = min(self.n, -(-k // self.BUCKET) * self.BUCKET)
             q = fused.rows(obs6, bits, self.rows, m)
-            self.greedy.index_copy_(0, self.rows[:k].long(), q[:k].float().argmax(1))
+            assert q.dtype == torch.bfloat16 and q.is_contiguous() and q.shape == (m, 4)
+            N.check(self.lib.mz_greedy_scatter(q.data_ptr(), 4, self.rows.data_ptr(),
+                                               self.count.data_ptr(), m, self.greedy.data_ptr(),
+                                               torch.cuda.current_stream(q.device).cuda_stream))
         return self.greedy
+
+    def tick(self, term, trunc, steps_done, eps_start, eps_final, eps_decay, wins, episodes, seed,
+             counter):
+        """mz_trainer_tick: the step's bookkeeping + the next act's epsilon and greedy-row list
+        (issued, count on its way to the host). Returns the epsilon tensor."""
+        if not hasattr(self, "eps"):
+            self.eps = torch.empty(self.n, dtype=torch.float32, device=self.rows.device)
+        for t in (term, trunc):
+            assert t.dtype == torch.uint8 and t.is_contiguous() and t.numel() == self.n
+        assert steps_done.dtype == torch.float32 and steps_done.is_contiguous()
+        for t in (wins, episodes):
+            assert t is None or (t.dtype == torch.int64 and t.numel() == 1)
+        N.check(self.lib.mz_trainer_tick(
+            term.data_ptr(), trunc.data_ptr(), steps_done.data_ptr(), float(eps_start),
+            float(eps_final), float(eps_decay), self.eps.data_ptr(),
+            wins.data_ptr() if wins is not None else None,
+            episodes.data_ptr() if episodes is not None else None,
+            seed & 0xFFFFFFFFFFFFFFFF, counter & 0xFFFFFFFFFFFFFFFF, self.n, self.scratch.data_ptr(),
+            self.rows.data_ptr(), self.count.data_ptr(),
+            torch.cuda.current_stream(self.rows.device).cuda_stream))
+        self.count_host.copy_(self.count, non_blocking=True)
+        self.event.record()
+        self._issued = (self.eps.data_ptr(), seed, counter)
+        return self.eps
 
 
 class FusedActorCritic:

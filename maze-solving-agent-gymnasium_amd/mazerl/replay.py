@@ -80,6 +80,38 @@ class DeviceReplay:
             self.size_dev.fill_(float(size))
         self.size = size
 
+    def _ring_push(self, n, s6=None, sw=None, a=None, r=None, s6n=None, swn=None):
+        """One mz_replay_push launch: ring rows ptr .. ptr + n - 1 of the arrays given (others
+        untouched; the pointer does not move)."""
+        from . import _native as N
+        if n > self.capacity:
+            raise ValueError("a push larger than the ring")
+        srcs = (s6, sw, a, r, s6n, swn)
+        dts = (torch.float32, torch.int32, torch.int32, torch.float32, torch.float32, torch.int32)
+        for t, dt in zip(srcs, dts):
+            if t is not None:
+                assert t.dtype == dt and t.is_contiguous() and t.shape[0] == n and t.device == self.device
+        ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+        N.check(N.load().mz_replay_push(
+            n, self.capacity, self.ptr, *[ptr(t) for t in srcs], self.s6.data_ptr(),
+            self.sw.data_ptr(), self.a.data_ptr(), self.r.data_ptr(), self.s6n.data_ptr(),
+            self.swn.data_ptr(), self.s6.shape[1], self.sw.shape[1],
+            torch.cuda.current_stream(self.device).cuda_stream))
+
+    def push_state(self, s6, sw):
+        """State half of the next push (before the env step overwrites the observation)."""
+        self._ring_push(s6.shape[0], s6=s6, sw=sw)
+
+    def push_rest(self, a, r, s6n, swn):
+        """Action, reward and next state of the rows push_state wrote; the push is complete."""
+        n = a.shape[0]
+        self._ring_push(n, a=a, r=r, s6n=s6n, swn=swn)
+        self.ptr = (self.ptr + n) % self.capacity
+        size = min(self.size + n, self.capacity)
+        if size != self.size:
+            self.size_dev.fill_(float(size))
+        self.size = size
+
     def _write(self, pairs, n):
         """Ring rows ptr .. ptr + n - 1 (one or two contiguous slices) <- the n source rows, one
         copy kernel per array and slice (dtype conversion included)."""

@@ -16,6 +16,7 @@ VectorOffPolicyTrainer.train() is NeuralOffPolicyTrainer.train (lib/trainers/off
 evaluate() is NeuralOffPolicyTrainer.test(new=True)/infer (:228-299): fresh mazes, one episode
 each, win = terminated; greedy (eps = 0) or the reference's epsilon protocol (Q14).
 """
+import os
 import time
 
 import torch
@@ -25,13 +26,16 @@ from ..vector_env import ALGOS, VectorMazeEnv
 
 class VectorOffPolicyTrainer:
     def __init__(self, env, learner, seed=0, regen_won=True, curriculum=False, allreduce_stats=None,
-                 bank=True):
+                 bank=True, fused=True):
         self.env, self.learner = env, learner
         if regen_won and bank:
             # winners' new mazes come from a bank refilled on a side stream (VectorMazeEnv.
             # enable_bank): a maze build is a ~1 ms serial chain that would stall the step
             env.enable_bank(algorithms=[0, 1, 2] if curriculum else None)
         self.seed = seed
+        # fused: the per-step bookkeeping and the replay push as HIP launches (mz_trainer_tick,
+        # mz_replay_push) instead of ~25 torch ops; False keeps the torch path (A/B, tests)
+        self.fused = bool(fused)
         self.regen_won = regen_won
         self.curriculum = curriculum
         self.allreduce_stats = allreduce_stats
@@ -40,6 +44,7 @@ class VectorOffPolicyTrainer:
         self.episodes = torch.zeros((), dtype=torch.int64, device=dev)
         self.inst_wins = torch.zeros(env.num_envs, dtype=torch.int32, device=dev)
         self.counter = 0
+        self._eps = None  # the next step's epsilon, computed at the end of the previous step
         self.history = []
 
     def _expand(self, bits):
@@ -47,25 +52,45 @@ class VectorOffPolicyTrainer:
 
     def vector_step(self):
         env, L = self.env, self.learner
-        eps = L.epsilon()
+        # epsilon of this step's fused act (fixed by the previous step's bookkeeping)
+        eps = self._eps if self._eps is not None else L.epsilon()
+        self._eps = None
         # (eps, seed, counter) of this step's fused act: the acting forward runs over the rows
-        # that will act greedily only
+        # that will act greedily only (the row list was issued at the end of the previous step)
         greedy = L.greedy(env.obs6, env.window, env.window_bits, act=(eps, self.seed, self.counter))
-        s6, sw = env.obs6.clone(), env.window_bits.clone()
+        rp = L.replay
+        ring = self.fused and hasattr(rp, "push_state") and env.window_bits is not None and \
+            env.device.type == "cuda"
+        if ring:  # the replay rows' state half, straight from the observation the step replaces
+            rp.push_state(env.obs6, env.window_bits)
+        else:
+            s6, sw = env.obs6.clone(), env.window_bits.clone()
         env.step_act(eps=eps, greedy=greedy, seed=self.seed, counter=self.counter)
         self.counter += 1
-        L.replay.push(s6, sw, env.actions, env.reward, env.obs6, env.window_bits)
-        term = env.terminated.bool()
-        done = term | env.truncated.bool()
-        L.steps_done += 1
-        L.steps_done.masked_fill_(term, 0)
-        self.wins += term.sum()
-        self.episodes += done.sum()
-        if self.curriculum:  # change_algorithm (off_policy_trainer.py:302-310), per instance
-            self.inst_wins += term.to(torch.int32)
-            algo = torch.where(self.inst_wins >= 10, ALGOS["dfs"],
-                               torch.where(self.inst_wins >= 5, ALGOS["prim&kill"], ALGOS["r-prim"]))
-            env.set_algorithm(algo.to(torch.uint8))
+        tick = getattr(L, "tick", None) if self.fused and not self.curriculum else None
+        # steps_done (+1, 0 on a win), wins / episodes, the next step's epsilon and its greedy-row
+        # list — issued now, so that its count reaches the host while the stream runs the push
+        # and the resets queued behind it
+        self._eps = tick(env.terminated, env.truncated, self.wins, self.episodes, self.seed,
+                         self.counter) if tick is not None else None
+        if self._eps is None:
+            term = env.terminated.bool()
+            L.steps_done += 1
+            L.steps_done.masked_fill_(term, 0)
+            if hasattr(L, "prepare_greedy"):
+                self._eps = L.epsilon()
+                L.prepare_greedy(self._eps, self.seed, self.counter)
+            self.wins += term.sum()
+            self.episodes += (term | env.truncated.bool()).sum()
+            if self.curriculum:  # change_algorithm (off_policy_trainer.py:302-310), per instance
+                self.inst_wins += term.to(torch.int32)
+                algo = torch.where(self.inst_wins >= 10, ALGOS["dfs"],
+                                   torch.where(self.inst_wins >= 5, ALGOS["prim&kill"], ALGOS["r-prim"]))
+                env.set_algorithm(algo.to(torch.uint8))
+        if ring:
+            rp.push_rest(env.actions, env.reward, env.obs6, env.window_bits)
+        else:
+            rp.push(s6, sw, env.actions, env.reward, env.obs6, env.window_bits)
         env.reset_done(regen_won=self.regen_won)
         # with an overlapped learner the updates run on its side stream; the next push (one row
         # per instance) is kept out of their sample range
@@ -73,6 +98,22 @@ class VectorOffPolicyTrainer:
 
     def train(self, vector_steps, log_every=0, log=print):
         t0 = time.perf_counter()
+        prio = os.environ.get("MZ_ACT_PRIORITY")
+        if prio is None or self.env.device.type != "cuda":
+            return self._train(vector_steps, log_every, log, t0)
+        # acting / env work on a stream of its own priority (the learner's side stream keeps the
+        # default one): the small per-step kernels get CUs ahead of the update's
+        outer = torch.cuda.current_stream(self.env.device)
+        if getattr(self, "_act_stream", None) is None:
+            self._act_stream = torch.cuda.Stream(self.env.device, priority=int(prio))
+        s = self._act_stream
+        s.wait_stream(outer)
+        with torch.cuda.stream(s):
+            secs = self._train(vector_steps, log_every, log, t0)
+        outer.wait_stream(s)
+        return secs
+
+    def _train(self, vector_steps, log_every, log, t0):
         for k in range(vector_steps):
             loss = self.vector_step()
             if log_every and (k + 1) % log_every == 0:
