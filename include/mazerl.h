@@ -394,6 +394,22 @@ int mz_replay_push(int32_t n, int64_t capacity, int64_t ptr, const float* obs6_s
 int mz_replay_sample_idx(uint64_t seed, uint64_t counter, int64_t newest, int64_t n_avail,
                          int64_t capacity, int64_t* out_dev, int32_t n, void* stream);
 
+/* Q-learning loss of optimize_model (dqn_agent.py:129-147, ddqn_agent.py:121-143) from the nets'
+ * f32 output rows: for i < b, Q(s,a) = q_dev[i][action_dev[i]]; V(s') = q_tgt_dev[i][argmax_a
+ * q_next_dev[i][a]] (DDQN; first maximum) or max_a q_tgt_dev[i][a] (DQN: q_next_dev NULL);
+ * diff_dev[i] = Q(s,a) - (V(s') * gamma + reward_dev[i]) — no terminal masking (the reference
+ * bootstraps terminal transitions); *loss_dev = mse_loss (mean) = sum diff^2 / b.
+ * Row strides ldq / ldn / ldt in floats (>= 4). One workgroup. */
+int mz_q_loss(const float* q_dev, int32_t ldq, const float* q_next_dev, int32_t ldn,
+              const float* q_tgt_dev, int32_t ldt, const int64_t* action_dev,
+              const float* reward_dev, double gamma, int32_t b, float* loss_dev, float* diff_dev,
+              void* stream);
+
+/* Its gradient w.r.t. q rows [rows][4] (contiguous; rows >= b — DDQN's stacked s' rows — get 0):
+ * dq[i][action[i]] = diff[i] * (2 / b) * (*grad_dev), 0 elsewhere. */
+int mz_q_loss_backward(const float* grad_dev, const float* diff_dev, const int64_t* action_dev,
+                       int32_t b, int32_t rows, float* dq_dev, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -760,3 +760,25 @@ int mz_replay_sample_idx(uint64_t seed, uint64_t counter, int64_t newest, int64_
                               static_cast<hipStream_t>(stream)));
   return MZ_OK;
 }
+
+int mz_q_loss(const float* q_dev, int32_t ldq, const float* q_next_dev, int32_t ldn,
+              const float* q_tgt_dev, int32_t ldt, const int64_t* action_dev,
+              const float* reward_dev, double gamma, int32_t b, float* loss_dev, float* diff_dev,
+              void* stream) {
+  if (b <= 0 || !q_dev || !q_tgt_dev || !action_dev || !reward_dev || !loss_dev || !diff_dev ||
+      ldq < 4 || ldt < 4 || (q_next_dev && ldn < 4))
+    return fail(MZ_EINVAL, "bad arguments");
+  MZ_HIP(mz_launch_q_loss(q_dev, ldq, q_next_dev, ldn, q_tgt_dev, ldt, action_dev, reward_dev,
+                          (float)gamma, b, loss_dev, diff_dev, static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
+int mz_q_loss_backward(const float* grad_dev, const float* diff_dev, const int64_t* action_dev,
+                       int32_t b, int32_t rows, float* dq_dev, void* stream) {
+  if (b <= 0 || rows < b || !grad_dev || !diff_dev || !action_dev || !dq_dev)
+    return fail(MZ_EINVAL, "bad arguments");
+  const float norm = (float)(2.0 / (double)b);  // mse_loss backward: 2 / numel
+  MZ_HIP(mz_launch_q_loss_bwd(grad_dev, diff_dev, action_dev, b, rows, norm, dq_dev,
+                              static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}

@@ -82,3 +82,8 @@ hipError_t mz_launch_head_bf16(const MzHeadBf16& h, hipStream_t s);
 hipError_t mz_launch_replay_push(const MzReplayPush& p, hipStream_t s);
 hipError_t mz_launch_replay_idx(uint64_t seed, uint64_t counter, int64_t newest, int64_t n_avail,
                                 int64_t cap, int64_t* out, int n, hipStream_t s);
+hipError_t mz_launch_q_loss(const float* q, int ldq, const float* qn, int ldn, const float* qt,
+                            int ldt, const int64_t* action, const float* reward, float gamma, int b,
+                            float* loss, float* diff, hipStream_t s);
+hipError_t mz_launch_q_loss_bwd(const float* g, const float* diff, const int64_t* action, int b,
+                                int rows, float norm, float* dq, hipStream_t s);

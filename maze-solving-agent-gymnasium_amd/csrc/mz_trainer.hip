@@ -15,6 +15,10 @@
 //                    permuted to the fused stem's position-major feature order and zero-padded)
 //   k_replay_push    ring rows ptr .. ptr + n - 1 of the replay's six arrays <- a vector step
 //   k_replay_idx     uniform sample rows over the newest n_avail ring rows (Philox)
+//   k_q_loss_fwd/bwd the Q-learning loss of optimize_model (dqn_agent.py:129-147,
+//                    ddqn_agent.py:121-143) from the nets' output rows, and its gradient w.r.t.
+//                    those rows — what gather / max / argmax / mul / add / mse_loss / mean and
+//                    their backward (zero fills, scatter, slice copy) did in ~15 launches
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -170,7 +174,75 @@ __global__ void k_replay_idx(uint64_t seed, uint64_t counter, int64_t newest, in
   out[i] = r;
 }
 
+// One workgroup: per row i < b, a = action[i], Q(s,a) = q[i][a];
+//   V(s') = q_tgt[i][argmax q_next[i]] (DDQN, first maximum) or max q_tgt[i] (DQN);
+//   diff = Q(s,a) - (V(s') * gamma + r)   (f32, torch's op order, no contraction);
+// loss = (sum diff^2) / b.
+__global__ __launch_bounds__(1024) void k_q_loss_fwd(const float* __restrict__ q, int ldq,
+                                                    const float* __restrict__ qn, int ldn,
+                                                    const float* __restrict__ qt, int ldt,
+                                                    const int64_t* __restrict__ action,
+                                                    const float* __restrict__ reward, float gamma,
+                                                    int b, float* __restrict__ loss,
+                                                    float* __restrict__ diff) {
+  __shared__ float part[1024 / W];
+  float acc = 0.0f;
+  for (int i = threadIdx.x; i < b; i += blockDim.x) {
+    const float* t = qt + (size_t)i * ldt;
+    float v;
+    if (qn) {
+      const float* x = qn + (size_t)i * ldn;
+      int best = 0;
+      for (int k = 1; k < 4; ++k)
+        if (x[k] > x[best]) best = k;
+      v = t[best];
+    } else {
+      v = fmaxf(fmaxf(t[0], t[1]), fmaxf(t[2], t[3]));
+    }
+    const float expected = __fadd_rn(__fmul_rn(v, gamma), reward[i]);
+    const float d = __fsub_rn(q[(size_t)i * ldq + (int)action[i]], expected);
+    diff[i] = d;
+    acc = __fadd_rn(acc, __fmul_rn(d, d));
+  }
+  for (int o = W / 2; o; o >>= 1) acc = __fadd_rn(acc, __shfl_xor(acc, o));
+  if ((threadIdx.x & (W - 1)) == 0) part[threadIdx.x / W] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.0f;
+    for (int k = 0; k < (int)(blockDim.x / W); ++k) s = __fadd_rn(s, part[k]);
+    *loss = __fdiv_rn(s, (float)b);
+  }
+}
+
+// dq[i][k] = diff[i] * (2 / b) * g at k = action[i] for i < b; 0 elsewhere (rows >= b included):
+// mse_loss's mean backward, then gather's and the row slice's (torch's order of the products)
+__global__ void k_q_loss_bwd(const float* __restrict__ g, const float* __restrict__ diff,
+                             const int64_t* __restrict__ action, int b, int rows, float norm,
+                             float* __restrict__ dq) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= rows * 4) return;
+  const int i = t >> 2, k = t & 3;
+  float v = 0.0f;
+  if (i < b && k == (int)action[i]) v = __fmul_rn(__fmul_rn(diff[i], norm), *g);
+  dq[t] = v;
+}
+
 }  // namespace
+
+hipError_t mz_launch_q_loss(const float* q, int ldq, const float* qn, int ldn, const float* qt,
+                            int ldt, const int64_t* action, const float* reward, float gamma, int b,
+                            float* loss, float* diff, hipStream_t s) {
+  hipLaunchKernelGGL(k_q_loss_fwd, dim3(1), dim3(1024), 0, s, q, ldq, qn, ldn, qt, ldt, action,
+                     reward, gamma, b, loss, diff);
+  return hipGetLastError();
+}
+
+hipError_t mz_launch_q_loss_bwd(const float* g, const float* diff, const int64_t* action, int b,
+                                int rows, float norm, float* dq, hipStream_t s) {
+  hipLaunchKernelGGL(k_q_loss_bwd, dim3((rows * 4 + 255) / 256), dim3(256), 0, s, g, diff, action,
+                     b, rows, norm, dq);
+  return hipGetLastError();
+}
 
 hipError_t mz_launch_tick(const uint8_t* term, const uint8_t* trunc, float* steps_done,
                           float eps_final, float eps_span, float inv_decay, float* eps_out,

@@ -18,6 +18,7 @@ VectorDQNLearner    the MI355X learner for VectorMazeEnv: device replay (HBM), b
 import collections
 import copy
 import math
+import os
 import random
 
 import numpy as np
@@ -32,6 +33,48 @@ from .nets import QNet
 
 
 STACK_ROWS = True  # DDQN on packed windows (GPU): source(s) and source(s') as one pass
+# GPU: the loss and its gradient w.r.t. the Q rows as two HIP launches (MZ_FUSED_LOSS=0: torch ops)
+FUSED_LOSS = os.environ.get("MZ_FUSED_LOSS", "1") != "0"
+
+
+class _QLossFn(torch.autograd.Function):
+    """mse_loss(Q(s,a), V(s') * gamma + r) from the nets' output rows (mz_q_loss /
+    mz_q_loss_backward): q [rows, 4] (rows >= b: DDQN's stacked s' rows, zero gradient),
+    q_next [b, 4] (DDQN's argmax rows) or None (DQN: max of q_tgt), q_tgt [b, 4]."""
+
+    @staticmethod
+    def forward(ctx, q, q_next, q_tgt, action, reward, gamma, b):
+        from .. import _native as N
+        dev = q.device
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        diff = torch.empty(b, dtype=torch.float32, device=dev)
+        N.check(N.load().mz_q_loss(
+            q.data_ptr(), q.stride(0), q_next.data_ptr() if q_next is not None else None,
+            q_next.stride(0) if q_next is not None else 0, q_tgt.data_ptr(), q_tgt.stride(0),
+            action.data_ptr(), reward.data_ptr(), float(gamma), b, loss.data_ptr(), diff.data_ptr(),
+            torch.cuda.current_stream(dev).cuda_stream))
+        ctx.save_for_backward(diff, action)
+        ctx.rows, ctx.b = q.shape[0], b
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        from .. import _native as N
+        diff, action = ctx.saved_tensors
+        g = g.contiguous()
+        dq = torch.empty(ctx.rows, 4, dtype=torch.float32, device=diff.device)
+        N.check(N.load().mz_q_loss_backward(g.data_ptr(), diff.data_ptr(), action.data_ptr(), ctx.b,
+                                            ctx.rows, dq.data_ptr(),
+                                            torch.cuda.current_stream(diff.device).cuda_stream))
+        return dq, None, None, None, None, None, None
+
+
+def _fused_ok(q, action, reward, *others):
+    return (FUSED_LOSS and q.is_cuda and q.dtype == torch.float32 and q.dim() == 2 and
+            q.shape[1] == 4 and q.stride(1) == 1 and action.dtype == torch.int64 and
+            action.is_contiguous() and reward.dtype == torch.float32 and reward.is_contiguous() and
+            all(t is None or (t.dtype == torch.float32 and t.stride(1) == 1 and t.shape[1] == 4)
+                for t in others))
 
 
 def _stacked(x, y):
@@ -59,8 +102,26 @@ def q_loss(source, target, state, action, reward, next_state, gamma, double):
         # per update, profiles/r01k_update_target_stem_side_stream.json)
         q = source.forward_rows((_stacked(state[0], next_state[0]),
                                  _stacked(state[1], next_state[1])), b)
-        q_sa = q[:b].gather(1, action.view(-1, 1))
         q_next = q[b:].detach()
+        if q.shape[0] == 2 * b and _fused_ok(q, action, reward, q_next):
+            with torch.no_grad():
+                q_t = target(next_state)
+            if _fused_ok(q, action, reward, q_t):
+                return _QLossFn.apply(q, q_next, q_t.float().contiguous(), action, reward, gamma, b)
+            q_sa = q[:b].gather(1, action.view(-1, 1))
+            v_next = q_t.gather(1, q_next.max(1)[1].unsqueeze(1)).squeeze(1)
+            return F.mse_loss(q_sa, ((v_next * gamma) + reward).unsqueeze(1))
+        q_sa = q[:b].gather(1, action.view(-1, 1))
+    elif not double and state[1].is_cuda:
+        q = source(state)
+        if _fused_ok(q, action, reward):
+            with torch.no_grad():
+                q_t = target(next_state)
+            if _fused_ok(q, action, reward, q_t):
+                return _QLossFn.apply(q, None, q_t.contiguous(), action, reward, gamma, q.shape[0])
+            return F.mse_loss(q.gather(1, action.view(-1, 1)),
+                              ((q_t.max(1)[0] * gamma) + reward).unsqueeze(1))
+        q_sa = q.gather(1, action.view(-1, 1))
     else:
         q_sa = source(state).gather(1, action.view(-1, 1))
     with torch.no_grad():  # the reference detaches V(s'); no graph is built for it here

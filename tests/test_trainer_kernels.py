@@ -155,3 +155,39 @@ def test_vector_step_kernels_match_torch_bookkeeping():
     for x, y in ((r0.s6, r1.s6), (r0.sw, r1.sw), (r0.a, r1.a), (r0.r, r1.r), (r0.s6n, r1.s6n),
                  (r0.swn, r1.swn)):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("variant", ["ddqn", "dqn"])
+def test_fused_q_loss_matches_torch_loss(variant):
+    """mz_q_loss / mz_q_loss_backward (agents/dqn.py _QLossFn) == gather / max / mse_loss and their
+    autograd backward: loss and every parameter gradient, on packed-window replay rows (f32)."""
+    from mazerl.agents import dqn as D
+    from mazerl.agents.nets import QNet
+    torch.manual_seed(7)
+    src = QNet(variant=variant).to(DEV).eval()  # dropout off: both paths see the same stem
+    tgt = QNet(variant=variant).to(DEV).eval()
+    b = 512
+    g = torch.Generator(device=DEV).manual_seed(8)
+
+    def bits():
+        x = torch.randint(-2**31, 2**31 - 1, (b, 22), generator=g, device=DEV, dtype=torch.int32)
+        x[:, 21] &= (1 << (675 - 21 * 32)) - 1
+        return x
+    s = (torch.rand(b, 6, generator=g, device=DEV), bits())
+    sn = (torch.rand(b, 6, generator=g, device=DEV), bits())
+    a = torch.randint(0, 4, (b,), generator=g, device=DEV)
+    r = torch.randn(b, generator=g, device=DEV)
+    out = []
+    for fused in (True, False):
+        D.FUSED_LOSS = fused
+        try:
+            src.zero_grad(set_to_none=True)
+            loss = D.q_loss(src, tgt, s, a, r, sn, 0.7, variant == "ddqn")
+            loss.backward()
+        finally:
+            D.FUSED_LOSS = True
+        out.append((loss.detach().clone(), [p.grad.clone() for p in src.parameters()]))
+    (l0, g0), (l1, g1) = out
+    torch.testing.assert_close(l0, l1, rtol=1e-6, atol=0)
+    for x, y in zip(g0, g1):
+        torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-7)
