@@ -74,17 +74,12 @@ __device__ inline void load_rows(const uint32_t* __restrict__ bits, int n, int n
   __syncthreads();
 }
 
-// LDS written and read by the same wave only: a wave-scope fence orders it, no s_barrier.
-__device__ inline void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
-// Forward, one wave per group of FG = 4 samples (4 x 49 pooled outputs = 49 MFMA row tiles of 16),
-// 4 waves per workgroup, persistent over the groups. The conv is an f32 MFMA GEMM
+// Forward, one workgroup (4 waves) per group of FG = 4 samples (4 x 49 pooled outputs = 49 MFMA
+// row tiles of 16, dealt round-robin to the 4 waves), persistent over the groups. (One wave per
+// group left a 1,024-row update pass with 256 waves on 256 CUs, each walking 49 tiles: 38 us,
+// the same as 2,048 rows.) The conv is an f32 MFMA GEMM
 // (v_mfma_f32_16x16x4_f32, exact f32 products, an fmaf chain per output): rows = conv positions,
 // K = the 27 patch bits in torch's weight order k = ch*9 + ky*3 + kx (padded to 28: 7 MFMAs),
 // columns = the 32 output channels (two 16-column tiles). The window is binary, so A is 0.0/1.0
@@ -103,14 +98,11 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const uint32_t* __restrict__ b
                                                   uint32_t salt, float* __restrict__ feat, int ld,
                                                   uint8_t* __restrict__ code) {
   constexpr int FG = 4, NQ = FG * NPOOL, NT = NQ / 4;  // 196 pooled outputs, 49 tiles
-  __shared__ uint32_t wbs[4][FG * WW];
-  __shared__ uint32_t rws[4][FG * 3 * PR];
-  __shared__ uint32_t pts[4][NQ * 4];
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint32_t* wb = wbs[wid];
-  uint32_t* rows = rws[wid];
-  uint32_t* patch = pts[wid];
+  __shared__ uint32_t wb[FG * WW];
+  __shared__ uint32_t rows[FG * 3 * PR];
+  __shared__ uint32_t patch[NQ * 4];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int col = lane & 15, kq = lane >> 4;
   // B operands: B[k = 4*kc + kq][c] = w[c][k] (0 for k = 27), c = col (tile 0) / 16 + col (tile 1)
   float bw0[7], bw1[7];
@@ -128,16 +120,16 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const uint32_t* __restrict__ b
     k1 = (uint32_t)(key >> 32) + hash32(salt);
   }
   const int ngroups = (n + FG - 1) / FG;
-  for (int grp = blockIdx.x * 4 + wid; grp < ngroups; grp += gridDim.x * 4) {
+  for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
     const int n0 = grp * FG;
-    wave_sync();  // the previous group's LDS fully consumed
-    for (int i = lane; i < FG * WW; i += 64) {
+    __syncthreads();  // the previous group's LDS fully consumed
+    for (int i = tid; i < FG * WW; i += 256) {
       const int s = i / WW;
       wb[i] = n0 + s < n ? bits[(size_t)n0 * WW + i] : 0u;
     }
-    wave_sync();
+    __syncthreads();
     // padded rows: rows[(s*3 + ch)*PR + pr] = grid row pr - 1, column c at bit c + 1
-    for (int i = lane; i < FG * 3 * PR; i += 64) {
+    for (int i = tid; i < FG * 3 * PR; i += 256) {
       const int sc = i / PR, pr = i - sc * PR, s = sc / 3, ch = sc - s * 3;
       uint32_t v = 0u;
       if (pr >= 1 && pr <= 15) {
@@ -147,9 +139,9 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const uint32_t* __restrict__ b
       }
       rows[i] = v;
     }
-    wave_sync();
+    __syncthreads();
     // patch words in A-row order: patch[4*Q + r], Q = group pooled output, r = 2x2 position
-    for (int p = lane; p < NQ * 4; p += 64) {
+    for (int p = tid; p < NQ * 4; p += 256) {
       const int Q = p >> 2, r = p & 3, s = Q / NPOOL, q = Q - s * NPOOL;
       const int y = 2 * (q / 7) + (r >> 1), x = 2 * (q % 7) + (r & 1);
       uint32_t pw = 0u;
@@ -160,8 +152,8 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const uint32_t* __restrict__ b
           pw |= ((rows[(s * 3 + ch) * PR + y + ky] >> x) & 7u) << (ch * 9 + ky * 3);
       patch[p] = pw;
     }
-    wave_sync();
-    for (int t = 0; t < NT; ++t) {
+    __syncthreads();
+    for (int t = wid; t < NT; t += 4) {
       const uint32_t pw = patch[16 * t + col] >> kq;
       f32x4 acc0 = {bias0, bias0, bias0, bias0};
       f32x4 acc1 = {bias1, bias1, bias1, bias1};
@@ -207,7 +199,7 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const uint32_t* __restrict__ b
         if (CODE) code[(size_t)nn * FEAT + j] = (uint8_t)(idx | (cls << 2));
       }
     }
-    for (int i = lane; i < FG * NOBS; i += 64) {  // || obs6 (torch.cat((fw, s), 1))
+    for (int i = tid; i < FG * NOBS; i += 256) {  // || obs6 (torch.cat((fw, s), 1))
       const int s = i / NOBS, k = i - s * NOBS, nn = n0 + s;
       if (nn < n) feat[(size_t)nn * ld + FEAT + k] = obs6[(size_t)nn * NOBS + k];
     }
@@ -312,9 +304,8 @@ hipError_t mz_launch_stem_fwd(const uint32_t* bits, const float* obs6, int n, co
   // keep iff a 16-bit uniform >= thresh: P(drop) = thresh / 65536 (0.2 -> 13107)
   const uint32_t thresh = drop_p > 0.0f ? (uint32_t)(drop_p * 65536.0f + 0.5f) : 0u;
   const float scale = drop_p > 0.0f ? (float)(1.0 / (1.0 - (double)drop_p)) : 1.0f;
-  const int groups = (n + 3) / 4;
-  int blocks = (groups + 3) / 4;
-  if (blocks > 2048) blocks = 2048;
+  int blocks = (n + 3) / 4;  // one workgroup per 4 samples
+  if (blocks > 4096) blocks = 4096;
 #define MZ_SF(D, C)                                                                              \
   hipLaunchKernelGGL((k_stem_fwd<D, C>), dim3(blocks), dim3(256), 0, s, bits, obs6, n, w, b,      \
                      thresh, D ? scale : 1.0f, rng, salt, feat, ld, code)
