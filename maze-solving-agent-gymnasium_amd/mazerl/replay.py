@@ -90,7 +90,7 @@ class DeviceReplay:
         dts = (torch.float32, torch.int32, torch.int32, torch.float32, torch.float32, torch.int32)
         for t, dt in zip(srcs, dts):
             if t is not None:
-                assert t.dtype == dt and t.is_contiguous() and t.shape[0] == n and t.device == self.device
+                assert t.dtype == dt and t.is_contiguous() and t.shape[0] == n and t.is_cuda
         ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
         N.check(N.load().mz_replay_push(
             n, self.capacity, self.ptr, *[ptr(t) for t in srcs], self.s6.data_ptr(),
