@@ -410,6 +410,19 @@ int mz_q_loss(const float* q_dev, int32_t ldq, const float* q_next_dev, int32_t 
 int mz_q_loss_backward(const float* grad_dev, const float* diff_dev, const int64_t* action_dev,
                        int32_t b, int32_t rows, float* dq_dev, void* stream);
 
+/* PPO's optimizer step (ppo_agent.py:232-236, optimize_model): clip_grad_norm_(params, max_norm)
+ * (coef = min(max_norm / (||g||_2 + 1e-6), 1) over every gradient, the gradients scaled in place;
+ * max_norm <= 0: no clipping), then AdamW (torch's defaults: betas, eps, weight_decay given) with
+ * a learning rate per parameter group — segment k of the flat buffer (mz_adamw_flat's layout)
+ * uses lr_dev[seg_group[k]] (ppo_agent.py's three groups: actor lr, critic lr, their mean for
+ * the conv stem). step_dev is incremented on the device (capturable). scratch_dev: >= 513
+ * floats. Three launches. */
+int mz_adamw_groups(float* param_dev, float* exp_avg_dev, float* exp_avg_sq_dev,
+                    const float* const* grads_dev, const int64_t* seg_len,
+                    const int32_t* seg_group, int32_t nseg, const float* lr_dev, float* step_dev,
+                    double beta1, double beta2, double eps, double weight_decay, float max_norm,
+                    float* scratch_dev, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -782,3 +782,31 @@ int mz_q_loss_backward(const float* grad_dev, const float* diff_dev, const int64
                               static_cast<hipStream_t>(stream)));
   return MZ_OK;
 }
+
+int mz_adamw_groups(float* param_dev, float* exp_avg_dev, float* exp_avg_sq_dev,
+                    const float* const* grads_dev, const int64_t* seg_len,
+                    const int32_t* seg_group, int32_t nseg, const float* lr_dev, float* step_dev,
+                    double beta1, double beta2, double eps, double weight_decay, float max_norm,
+                    float* scratch_dev, void* stream) {
+  if (!param_dev || !exp_avg_dev || !exp_avg_sq_dev || !grads_dev || !seg_len || !seg_group ||
+      !lr_dev || !step_dev || !scratch_dev)
+    return fail(MZ_EINVAL, "bad arguments");
+  if (nseg < 1 || nseg > MZ_OPT_MAX_SEGS) return fail(MZ_EINVAL, "segment count %d", nseg);
+  const uintptr_t al = reinterpret_cast<uintptr_t>(param_dev) |
+                       reinterpret_cast<uintptr_t>(exp_avg_dev) |
+                       reinterpret_cast<uintptr_t>(exp_avg_sq_dev);
+  if (al & 15) return fail(MZ_EALIGN, "flat buffers must be 16-byte aligned");
+  for (int k = 0; k < nseg; ++k) {
+    if (!grads_dev[k] || seg_len[k] <= 0 || (seg_len[k] & 3))
+      return fail(MZ_EINVAL, "segment %d: length %lld (multiple of 4 required)", k,
+                  (long long)seg_len[k]);
+    if (reinterpret_cast<uintptr_t>(grads_dev[k]) & 15)
+      return fail(MZ_EALIGN, "gradient %d must be 16-byte aligned", k);
+    if (seg_group[k] < 0) return fail(MZ_EINVAL, "segment %d: group %d", k, seg_group[k]);
+  }
+  MZ_HIP(mz_launch_adamw_groups(param_dev, exp_avg_dev, exp_avg_sq_dev, grads_dev, seg_len,
+                                seg_group, nseg, lr_dev, step_dev, beta1, beta2, eps,
+                                weight_decay, max_norm, scratch_dev,
+                                static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}

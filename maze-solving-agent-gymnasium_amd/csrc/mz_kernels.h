@@ -87,3 +87,7 @@ hipError_t mz_launch_q_loss(const float* q, int ldq, const float* qn, int ldn, c
                             float* loss, float* diff, hipStream_t s);
 hipError_t mz_launch_q_loss_bwd(const float* g, const float* diff, const int64_t* action, int b,
                                 int rows, float norm, float* dq, hipStream_t s);
+hipError_t mz_launch_adamw_groups(float* p, float* m, float* v, const float* const* grads,
+                                  const int64_t* seg_len, const int32_t* seg_group, int nseg,
+                                  const float* lr, float* step, double b1, double b2, double eps,
+                                  double wd, float max_norm, float* scratch, hipStream_t s);

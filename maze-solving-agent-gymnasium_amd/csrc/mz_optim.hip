@@ -87,7 +87,131 @@ __global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, float* __r
   }
 }
 
+// ---- PPO's optimizer step (ppo_agent.py:232-236): clip_grad_norm_(params, 0.5), then AdamW
+// with three parameter groups (actor lr, critic lr, their mean for the conv stem), as three
+// launches over the flat buffer instead of torch's ~13 (per-tensor norms, stack, norm, clamp,
+// foreach mul, a fused AdamW per group).
+struct GSegs {
+  const float* g[MZ_OPT_MAX_SEGS];
+  int64_t off[MZ_OPT_MAX_SEGS + 1];
+  int grp[MZ_OPT_MAX_SEGS];
+  int n;
+};
+
+constexpr int SQ_BLOCKS = 512;
+
+__global__ __launch_bounds__(256) void k_sqnorm(GSegs segs, float* __restrict__ partial) {
+  __shared__ float red[4];
+  float acc = 0.0f;
+  for (int k = 0; k < segs.n; ++k) {
+    const float* g = segs.g[k];
+    const int64_t len = segs.off[k + 1] - segs.off[k];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < len;
+         i += (int64_t)gridDim.x * blockDim.x) {
+      const float x = g[i];
+      acc += x * x;
+    }
+  }
+  for (int o = 32; o; o >>= 1) acc += __shfl_xor(acc, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+// coef = min(max_norm / (||g|| + 1e-6), 1) (clip_grad_norm_'s clip_coef_clamped), and the step
+// count (the AdamW bias corrections of every group read it)
+__global__ __launch_bounds__(SQ_BLOCKS) void k_clip_coef(const float* __restrict__ partial,
+                                                         float max_norm, float* __restrict__ coef,
+                                                         float* __restrict__ step) {
+  __shared__ float red[SQ_BLOCKS / 64];
+  float acc = partial[threadIdx.x];
+  for (int o = 32; o; o >>= 1) acc += __shfl_xor(acc, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.0f;
+    for (int i = 0; i < SQ_BLOCKS / 64; ++i) s += red[i];
+    const float c = max_norm > 0.0f ? max_norm / (sqrtf(s) + 1e-6f) : 1.0f;
+    *coef = c < 1.0f ? c : 1.0f;
+    *step += 1.0f;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_adamw_groups(float* __restrict__ p, float* __restrict__ m,
+                                                      float* __restrict__ v, GSegs segs,
+                                                      const float* __restrict__ lr_dev,
+                                                      const float* __restrict__ step_dev,
+                                                      const float* __restrict__ coef_dev,
+                                                      double b1, double b2, double eps_d,
+                                                      double wd) {
+  const double t = (double)*step_dev;
+  const double bc1 = 1.0 - pow(b1, t);
+  const float bc2_sqrt = (float)sqrt(1.0 - pow(b2, t));
+  const float w1 = (float)(1.0 - b1), b2f = (float)b2, w2 = (float)(1.0 - b2), eps = (float)eps_d;
+  const float gscale = *coef_dev;
+  const int64_t n4 = segs.off[segs.n] >> 2;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = q << 2;
+    int k = 0;
+    while (k + 1 < segs.n && e >= segs.off[k + 1]) ++k;
+    const double lr = (double)lr_dev[segs.grp[k]];
+    const float step_size = (float)(lr / bc1);
+    const float decay = (float)(1.0 - lr * wd);
+    float4* gp = reinterpret_cast<float4*>(const_cast<float*>(segs.g[k]) + (e - segs.off[k]));
+    float4 g4 = *gp;
+    float4 p4 = reinterpret_cast<float4*>(p)[q];
+    float4 m4 = reinterpret_cast<float4*>(m)[q];
+    float4 v4 = reinterpret_cast<float4*>(v)[q];
+    float* gs = &g4.x;
+    float* ps = &p4.x;
+    float* ms = &m4.x;
+    float* vs = &v4.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float g = gs[j] * gscale;  // clip_grad_norm_: g.mul_(clip_coef_clamped)
+      gs[j] = g;
+      float pj = ps[j] * decay;
+      const float mj = ms[j] + w1 * (g - ms[j]);
+      const float vj = vs[j] * b2f + w2 * (g * g);
+      const float denom = sqrtf(vj) / bc2_sqrt + eps;
+      pj = pj - step_size * (mj / denom);
+      ps[j] = pj;
+      ms[j] = mj;
+      vs[j] = vj;
+    }
+    reinterpret_cast<float4*>(p)[q] = p4;
+    reinterpret_cast<float4*>(m)[q] = m4;
+    reinterpret_cast<float4*>(v)[q] = v4;
+    *gp = g4;  // the clipped gradient stays visible, as with clip_grad_norm_ in place
+  }
+}
+
 }  // namespace
+
+hipError_t mz_launch_adamw_groups(float* p, float* m, float* v, const float* const* grads,
+                                  const int64_t* seg_len, const int32_t* seg_group, int nseg,
+                                  const float* lr, float* step, double b1, double b2, double eps,
+                                  double wd, float max_norm, float* scratch, hipStream_t s) {
+  GSegs sg{};
+  sg.n = nseg;
+  sg.off[0] = 0;
+  for (int k = 0; k < nseg; ++k) {
+    sg.g[k] = grads[k];
+    sg.grp[k] = seg_group[k];
+    sg.off[k + 1] = sg.off[k] + seg_len[k];
+  }
+  float* coef = scratch + SQ_BLOCKS;
+  hipLaunchKernelGGL(k_sqnorm, dim3(SQ_BLOCKS), dim3(256), 0, s, sg, scratch);
+  hipLaunchKernelGGL(k_clip_coef, dim3(1), dim3(SQ_BLOCKS), 0, s, scratch, max_norm, coef, step);
+  const int64_t n4 = sg.off[nseg] >> 2;
+  int blocks = (int)((n4 + 255) / 256);
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(k_adamw_groups, dim3(blocks), dim3(256), 0, s, p, m, v, sg, lr, step, coef, b1,
+                     b2, eps, wd);
+  return hipGetLastError();
+}
 
 hipError_t mz_launch_adamw(float* p, float* m, float* v, const float* const* grads,
                            const int64_t* seg_len, int nseg, const float* lr, float* step, double b1,

@@ -43,7 +43,7 @@ EXPORTS = ["mz_last_error", "mz_device_count", "mz_create", "mz_destroy", "mz_lo
            "mz_pair_surrogate", "mz_leaky_relu_bf16", "mz_colsum_f32",
            "mz_replay_gather", "mz_host_alloc", "mz_host_free", "mz_q_front_rows", "mz_greedy_rows",
            "mz_trainer_tick", "mz_greedy_scatter", "mz_head_bf16", "mz_replay_push",
-           "mz_replay_sample_idx", "mz_q_loss", "mz_q_loss_backward"]
+           "mz_replay_sample_idx", "mz_q_loss", "mz_q_loss_backward", "mz_adamw_groups"]
 
 _lib = None
 
@@ -124,6 +124,8 @@ def load(build_if_missing=True):
     L.mz_pair_surrogate.argtypes = [vp, vp, vp, C.c_int32, C.c_float, vp, vp, vp]
     L.mz_adamw_flat.argtypes = [vp, vp, vp, vp, vp, C.c_int32, vp, vp, C.c_double, C.c_double,
                                 C.c_double, C.c_double, C.c_float, C.c_float, C.c_int32, vp]
+    L.mz_adamw_groups.argtypes = [vp, vp, vp, vp, vp, vp, C.c_int32, vp, vp, C.c_double,
+                                  C.c_double, C.c_double, C.c_double, C.c_float, vp, vp]
     L.mz_host_alloc.argtypes = [C.c_uint64, C.c_int32, C.POINTER(vp), C.POINTER(vp)]
     L.mz_host_free.argtypes = [vp]
     for f in EXPORTS:

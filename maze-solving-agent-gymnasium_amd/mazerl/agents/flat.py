@@ -106,3 +106,69 @@ class FlatAdamW(torch.optim.Optimizer):
                                        g["lr"].data_ptr(), self.step_t.data_ptr(), float(b1),
                                        float(b2), float(g["eps"]), float(g["weight_decay"]),
                                        self.clamp, float(self.grad_scale), 1, st))
+
+
+class FlatAdamWGroups(torch.optim.Optimizer):
+    """PPO's optimizer step (ppo_agent.py:232-236): `clip_grad_norm_(params, max_norm)` then
+    `torch.optim.AdamW` with one learning rate per parameter group (ppo_agent.py's actor / critic /
+    conv groups), as three HIP launches over the net's flat buffer (`mz_adamw_groups`: squared-norm
+    partials, the clip coefficient + step count, AdamW) instead of torch's per-tensor norms, clamp,
+    foreach scale and one fused AdamW per group. `groups` = [(params, lr), ...]; the learning rates
+    are fixed (the reference schedules none). step() clips with `self.max_norm` (<= 0: no clip),
+    so the caller skips its own clip_grad_norm_ (`fused_clip`)."""
+
+    fused_clip = True
+
+    def __init__(self, net, groups, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2,
+                 max_norm=0.0):
+        flat = flatten_params(net)
+        params = list(net.parameters())
+        dev = flat.device
+        if dev.type != "cuda":
+            raise RuntimeError("FlatAdamWGroups runs on the GPU (HIP)")
+        if len(params) > 16:
+            raise ValueError("mz_adamw_groups takes at most 16 parameter tensors")
+        groups = [(list(ps), float(lr)) for ps, lr in groups]
+        gid = {}
+        for k, (ps, _) in enumerate(groups):
+            for p in ps:
+                gid[id(p)] = k
+        if len(gid) != len(params) or any(id(p) not in gid for p in params):
+            raise ValueError("every parameter of the net must be in exactly one group")
+        super().__init__([{"params": ps, "lr": lr} for ps, lr in groups],
+                         dict(betas=betas, eps=eps, weight_decay=weight_decay))
+        self.flat = flat
+        self.params = params  # flat-buffer order
+        self.sizes = list(net._flat_sizes)
+        self.exp_avg = torch.zeros_like(flat)
+        self.exp_avg_sq = torch.zeros_like(flat)
+        self.step_t = torch.zeros((), dtype=torch.float32, device=dev)
+        self.lr_dev = torch.tensor([lr for _, lr in groups], dtype=torch.float32, device=dev)
+        self.scratch = torch.zeros(520, dtype=torch.float32, device=dev)
+        self.max_norm = float(max_norm)
+        self.lib = N.load()
+        self._seg_len = (C.c_int64 * len(params))(*self.sizes)
+        self._seg_group = (C.c_int32 * len(params))(*[gid[id(p)] for p in params])
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        if closure is not None:
+            raise ValueError("closures are not supported")
+        ptrs = []
+        for p, n in zip(self.params, self.sizes):
+            if p.grad is None:
+                raise RuntimeError("every parameter needs a gradient")
+            if p.grad.numel() != n or not p.grad.is_contiguous():
+                pad = torch.zeros(n, dtype=p.grad.dtype, device=p.grad.device)  # (tiny biases)
+                pad[:p.numel()].copy_(p.grad.reshape(-1))
+                p.grad = pad[:p.numel()].view_as(p)
+            ptrs.append(p.grad.data_ptr())
+        arr = (C.c_void_p * len(ptrs))(*ptrs)
+        g = self.param_groups[0]
+        b1, b2 = g["betas"]
+        N.check(self.lib.mz_adamw_groups(
+            self.flat.data_ptr(), self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), arr,
+            self._seg_len, self._seg_group, len(ptrs), self.lr_dev.data_ptr(),
+            self.step_t.data_ptr(), float(b1), float(b2), float(g["eps"]),
+            float(g["weight_decay"]), self.max_norm, self.scratch.data_ptr(),
+            torch.cuda.current_stream(self.flat.device).cuda_stream))

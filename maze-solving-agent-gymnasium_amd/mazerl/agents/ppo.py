@@ -14,6 +14,8 @@ PPOAgent        single-env drop-in with the reference constructor (do_episode/op
                 evaluate); evaluate() advances the observation (the reference keeps the first
                 one, SURVEY Q16 — deliberately not copied).
 """
+import os
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -65,8 +67,15 @@ class ActorCriticNet(nn.Module):
 
 
 def make_optimizer(net, actor_lr, critic_lr, capturable=False):
-    """ppo_agent.py's 3-group AdamW; capturable (device step counters, fused kernel) for the
-    graph-captured minibatch step."""
+    """ppo_agent.py's 3-group AdamW. capturable (the graph-captured minibatch step, on the GPU):
+    the flat-buffer HIP optimizer with the clip_grad_norm_ in the same launches (FlatAdamWGroups;
+    MZ_PPO_TORCH_ADAMW=1: torch's capturable fused AdamW)."""
+    groups = [(net.actor_head.parameters(), actor_lr), (net.critic_head.parameters(), critic_lr),
+              (net.conv.parameters(), (actor_lr + critic_lr) / 2)]
+    if capturable and next(net.parameters()).is_cuda and \
+            os.environ.get("MZ_PPO_TORCH_ADAMW", "0") == "0":
+        from .flat import FlatAdamWGroups
+        return FlatAdamWGroups(net, groups)
     kw = dict(capturable=True, fused=True) if capturable else {}
     return optim.AdamW([
         {"params": net.actor_head.parameters(), "lr": actor_lr},
@@ -154,7 +163,10 @@ def ppo_minibatch(net, optimizer, pos, win, act, lp_old, adv, ret, entropy_coef,
     else:
         allreduce.unpack(net)
         total = None
-    torch.nn.utils.clip_grad_norm_(net.parameters(), max_norm=0.5)
+    if getattr(optimizer, "fused_clip", False):
+        optimizer.max_norm = 0.5  # clip_grad_norm_ inside the optimizer's launches
+    else:
+        torch.nn.utils.clip_grad_norm_(net.parameters(), max_norm=0.5)
     optimizer.step()
     return total.detach() if total is not None else None
 

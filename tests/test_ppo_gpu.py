@@ -87,3 +87,33 @@ def test_pair_surrogate_matches_torch_broadcast():
     (g2,) = torch.autograd.grad(ref, lp2)
     assert float(out) == pytest.approx(float(ref), rel=1e-5, abs=1e-7)
     assert torch.allclose(g, g2, rtol=1e-4, atol=1e-6 * float(g2.abs().max()))
+
+
+def test_flat_adamw_groups_matches_torch_clip_and_adamw():
+    """FlatAdamWGroups (mz_adamw_groups: clip_grad_norm_ + 3-group AdamW in three launches) ==
+    torch.nn.utils.clip_grad_norm_(0.5) + torch.optim.AdamW(fused) with the same groups, over
+    steps with the clip active and inactive (ppo_agent.py:232-236)."""
+    from mazerl.agents.flat import FlatAdamWGroups
+    from mazerl.agents.ppo import ActorCriticNet
+    torch.manual_seed(9)
+    A = ActorCriticNet(3, 6, 4, 32, 256).cuda()
+    B = copy.deepcopy(A)
+
+    def groups(n):
+        return [(n.actor_head.parameters(), 3e-4), (n.critic_head.parameters(), 1e-4),
+                (n.conv.parameters(), 2e-4)]
+    oa = FlatAdamWGroups(A, groups(A), max_norm=0.5)
+    ob = torch.optim.AdamW([{"params": list(ps), "lr": lr} for ps, lr in groups(B)], fused=True)
+    g = torch.Generator(device="cuda").manual_seed(10)
+    for k, scale in enumerate([1.0, 1e-4, 3.0, 1e-5, 1.0]):
+        grads = [torch.randn(p.shape, generator=g, device="cuda") * scale for p in A.parameters()]
+        for pa, pb, gr in zip(A.parameters(), B.parameters(), grads):
+            pa.grad = gr.clone()
+            pb.grad = gr.clone()
+        oa.step()
+        torch.nn.utils.clip_grad_norm_(B.parameters(), max_norm=0.5)
+        ob.step()
+        torch.cuda.synchronize()
+        for (name, pa), pb in zip(A.named_parameters(), B.parameters()):
+            assert torch.allclose(pa.grad, pb.grad, rtol=1e-5, atol=1e-9), (k, name)
+            assert torch.allclose(pa, pb, rtol=1e-5, atol=1e-6), (k, name)
