@@ -213,12 +213,15 @@ int mz_q_front(const uint32_t* bits_dev, const float* obs6_dev, int32_t n, const
                const float* conv_b_dev, float drop_p, uint64_t seed, uint64_t counter,
                uint16_t* feat_dev, int32_t ld, void* stream);
 
-/* mz_q_front over a row list: output row i is instance rows_dev[i] (i < n) of bits_dev / obs6_dev.
- * With the list of mz_greedy_rows the acting forward runs over the rows that act greedily only
- * (dqn_agent.py:104-116 evaluates source_net(state) only when `sample >= eps`). */
+/* mz_q_front over a row list: output row i is instance rows_dev[i] (i < n) of bits_dev / obs6_dev;
+ * with count_dev (nullable) the rows i < min(n, *count_dev), the length read on the device (the
+ * stem can run before the caller knows the list's length). With the list of mz_greedy_rows the
+ * acting forward runs over the rows that act greedily only (dqn_agent.py:104-116 evaluates
+ * source_net(state) only when `sample >= eps`). */
 int mz_q_front_rows(const uint32_t* bits_dev, const float* obs6_dev, const int32_t* rows_dev,
-                    int32_t n, const float* conv_w_dev, const float* conv_b_dev, float drop_p,
-                    uint64_t seed, uint64_t counter, uint16_t* feat_dev, int32_t ld, void* stream);
+                    const int32_t* count_dev, int32_t n, const float* conv_w_dev,
+                    const float* conv_b_dev, float drop_p, uint64_t seed, uint64_t counter,
+                    uint16_t* feat_dev, int32_t ld, void* stream);
 
 /* Greedy-row list of the next fused act (mz_act / mz_step_act with the same eps, seed, counter;
  * dqn_agent.py:104-116 draws `sample = random.random()` first and acts greedily iff

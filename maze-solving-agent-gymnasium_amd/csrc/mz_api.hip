@@ -372,20 +372,21 @@ int mz_q_front(const uint32_t* bits_dev, const float* obs6_dev, int32_t n, const
     return fail(MZ_EINVAL, "bad arguments");
   if (ld < 1576 || ld > 1600 || ld % 8 != 0) return fail(MZ_EINVAL, "feature stride %d", ld);
   if (!(drop_p >= 0.0f && drop_p < 1.0f)) return fail(MZ_EINVAL, "dropout p %g", (double)drop_p);
-  MZ_HIP(mz_launch_qfront(bits_dev, obs6_dev, nullptr, n, conv_w_dev, conv_b_dev, drop_p, seed,
-                          counter, feat_dev, ld, static_cast<hipStream_t>(stream)));
+  MZ_HIP(mz_launch_qfront(bits_dev, obs6_dev, nullptr, nullptr, n, conv_w_dev, conv_b_dev, drop_p,
+                          seed, counter, feat_dev, ld, static_cast<hipStream_t>(stream)));
   return MZ_OK;
 }
 
 int mz_q_front_rows(const uint32_t* bits_dev, const float* obs6_dev, const int32_t* rows_dev,
-                    int32_t n, const float* conv_w_dev, const float* conv_b_dev, float drop_p,
-                    uint64_t seed, uint64_t counter, uint16_t* feat_dev, int32_t ld, void* stream) {
+                    const int32_t* count_dev, int32_t n, const float* conv_w_dev,
+                    const float* conv_b_dev, float drop_p, uint64_t seed, uint64_t counter,
+                    uint16_t* feat_dev, int32_t ld, void* stream) {
   if (!bits_dev || !obs6_dev || !rows_dev || !conv_w_dev || !conv_b_dev || !feat_dev || n < 0)
     return fail(MZ_EINVAL, "bad arguments");
   if (ld < 1576 || ld > 1600 || ld % 8 != 0) return fail(MZ_EINVAL, "feature stride %d", ld);
   if (!(drop_p >= 0.0f && drop_p < 1.0f)) return fail(MZ_EINVAL, "dropout p %g", (double)drop_p);
-  MZ_HIP(mz_launch_qfront(bits_dev, obs6_dev, rows_dev, n, conv_w_dev, conv_b_dev, drop_p, seed,
-                          counter, feat_dev, ld, static_cast<hipStream_t>(stream)));
+  MZ_HIP(mz_launch_qfront(bits_dev, obs6_dev, rows_dev, count_dev, n, conv_w_dev, conv_b_dev,
+                          drop_p, seed, counter, feat_dev, ld, static_cast<hipStream_t>(stream)));
   return MZ_OK;
 }
 

@@ -24,9 +24,10 @@ hipError_t mz_launch_act(const MzDev& d, const MzAct& ap, hipStream_t s);
 hipError_t mz_launch_greedy_rows(const MzAct& ap, int n, int32_t* blk, int32_t* rows,
                                  int32_t* count, int32_t* count_host, hipStream_t s);
 hipError_t mz_launch_expand(const uint32_t* bits, float* out, int n, hipStream_t s);
-hipError_t mz_launch_qfront(const uint32_t* bits, const float* obs6, const int32_t* rows, int n,
-                            const float* w, const float* b, float drop_p, uint64_t seed,
-                            uint64_t counter, uint16_t* out, int ld, hipStream_t s);
+hipError_t mz_launch_qfront(const uint32_t* bits, const float* obs6, const int32_t* rows,
+                            const int32_t* count, int n, const float* w, const float* b,
+                            float drop_p, uint64_t seed, uint64_t counter, uint16_t* out, int ld,
+                            hipStream_t s);
 hipError_t mz_launch_bank_fill(const MzDev& bd, const int* head, int K, int algo, int dim,
                                uint64_t seed, uint32_t epoch, hipStream_t s);
 size_t mz_metrics_lds_bytes(int P);

@@ -89,7 +89,7 @@ __device__ inline void wave_sync() {
 template <bool DROP>
 __global__ __launch_bounds__(WAVE * WPB) __attribute__((amdgpu_waves_per_eu(4, 8)))
 void k_qfront(const uint32_t* __restrict__ bits, const float* __restrict__ obs6,
-              const int32_t* __restrict__ rows, int n,
+              const int32_t* __restrict__ rows, const int32_t* __restrict__ count, int n,
               const float* __restrict__ w, const float* __restrict__ bias, uint32_t drop_thresh,
               float drop_scale, uint32_t key0, uint32_t key1, uint32_t* __restrict__ out, int ld) {
   __shared__ uint4 lut[256];                  // 8 patch bits -> 8 bf16 (0 / 1.0)
@@ -130,6 +130,7 @@ void k_qfront(const uint32_t* __restrict__ bits, const float* __restrict__ obs6,
   __syncthreads();  // tables shared by the workgroup's waves
 
   const int ld2 = ld >> 1;  // row pitch in uint32 (bf16 pairs)
+  if (count) n = min(n, *count);  // the row list's length, read on the device
   const int ngroups = (n + IPG - 1) / IPG;
   // the group's 88 window words, loaded one group ahead (2 per lane) to hide HBM latency;
   // with `rows`, output row i is instance rows[i] (the greedy-row list: only the rows that act
@@ -249,9 +250,10 @@ void k_qfront(const uint32_t* __restrict__ bits, const float* __restrict__ obs6,
 
 }  // namespace
 
-hipError_t mz_launch_qfront(const uint32_t* bits, const float* obs6, const int32_t* rows, int n,
-                            const float* w, const float* b, float drop_p, uint64_t seed,
-                            uint64_t counter, uint16_t* out, int ld, hipStream_t s) {
+hipError_t mz_launch_qfront(const uint32_t* bits, const float* obs6, const int32_t* rows,
+                            const int32_t* count, int n, const float* w, const float* b,
+                            float drop_p, uint64_t seed, uint64_t counter, uint16_t* out, int ld,
+                            hipStream_t s) {
   if (n <= 0) return hipSuccess;
   // keep iff a 16-bit uniform >= thresh: P(drop) = thresh / 65536 (0.2 -> 13107, 0.19999695)
   const uint32_t thresh = drop_p > 0.0f ? (uint32_t)(drop_p * 65536.0f + 0.5f) : 0u;
@@ -262,10 +264,10 @@ hipError_t mz_launch_qfront(const uint32_t* bits, const float* obs6, const int32
   const int blocks = nb < 65536 ? nb : 65536;
   uint32_t* o = reinterpret_cast<uint32_t*>(out);
   if (thresh)
-    hipLaunchKernelGGL(k_qfront<true>, dim3(blocks), dim3(WAVE * WPB), 0, s, bits, obs6, rows, n, w, b, thresh,
+    hipLaunchKernelGGL(k_qfront<true>, dim3(blocks), dim3(WAVE * WPB), 0, s, bits, obs6, rows, count, n, w, b, thresh,
                        scale, (uint32_t)k, (uint32_t)(k >> 32), o, ld);
   else
-    hipLaunchKernelGGL(k_qfront<false>, dim3(blocks), dim3(WAVE * WPB), 0, s, bits, obs6, rows, n, w, b, 0u,
+    hipLaunchKernelGGL(k_qfront<false>, dim3(blocks), dim3(WAVE * WPB), 0, s, bits, obs6, rows, count, n, w, b, 0u,
                        1.0f, 0u, 0u, o, ld);
   return hipGetLastError();
 }

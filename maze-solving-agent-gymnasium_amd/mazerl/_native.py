@@ -99,7 +99,7 @@ def load(build_if_missing=True):
     L.mz_bank_consumed.argtypes = [vp, C.c_int32, vp, vp]
     L.mz_q_front.argtypes = [vp, vp, C.c_int32, vp, vp, C.c_float, C.c_uint64, C.c_uint64, vp,
                              C.c_int32, vp]
-    L.mz_q_front_rows.argtypes = [vp, vp, vp, C.c_int32, vp, vp, C.c_float, C.c_uint64,
+    L.mz_q_front_rows.argtypes = [vp, vp, vp, vp, C.c_int32, vp, vp, C.c_float, C.c_uint64,
                                   C.c_uint64, vp, C.c_int32, vp]
     L.mz_greedy_rows.argtypes = [vp, C.c_float, C.c_uint64, C.c_uint64, C.c_int32, vp, vp, vp, vp,
                                  vp]

@@ -133,8 +133,10 @@ class FusedStem:
         self.counter = 0
         self.lib = N.load()
 
-    def __call__(self, obs6, bits, rows=None, n=None):
-        """Feature rows of every instance, or with `rows` (int32 instance ids) of rows[:n] only."""
+    def __call__(self, obs6, bits, rows=None, n=None, count=None, out=None):
+        """Feature rows of every instance, or with `rows` (int32 instance ids) of rows[:n] only —
+        with `count` (int32 [1] on the device) rows[:min(n, count)], the rest of out[:n] left
+        unwritten. `out`: a [>= n, LD] bf16 buffer to write into."""
         dev = bits.device
         if dev.type != "cuda":
             raise RuntimeError("the fused acting stem runs on the GPU only")
@@ -149,14 +151,15 @@ class FusedStem:
         w = self.conv.weight.detach().contiguous()
         b = self.conv.bias.detach().contiguous()
         p = float(self.dropout.p) if (self.dropout is not None and self.dropout.training) else 0.0
-        feat = torch.empty(n, LD, dtype=torch.bfloat16, device=dev)
+        feat = torch.empty(n, LD, dtype=torch.bfloat16, device=dev) if out is None else out[:n]
         stream = torch.cuda.current_stream(dev).cuda_stream
         if rows is None:
             N.check(self.lib.mz_q_front(bits.data_ptr(), obs6.data_ptr(), n, w.data_ptr(),
                                         b.data_ptr(), p, self.seed, self.counter, feat.data_ptr(),
                                         LD, stream))
         else:
-            N.check(self.lib.mz_q_front_rows(bits.data_ptr(), obs6.data_ptr(), rows.data_ptr(), n,
+            N.check(self.lib.mz_q_front_rows(bits.data_ptr(), obs6.data_ptr(), rows.data_ptr(),
+                                             count.data_ptr() if count is not None else None, n,
                                              w.data_ptr(), b.data_ptr(), p, self.seed, self.counter,
                                              feat.data_ptr(), LD, stream))
         self.counter += 1
@@ -185,6 +188,15 @@ class FusedQ:
         """Q values [n, 4] of instances rows[:n]."""
         return self.head(self.stem(obs6, bits, rows, n))
 
+    @torch.no_grad()
+    def rows_stem(self, obs6, bits, rows, count, out):
+        """Stem features of rows[:count] (count on the device) into out [B, LD] (bf16)."""
+        self.stem(obs6, bits, rows, out.shape[0], count=count, out=out)
+
+    @torch.no_grad()
+    def rows_head(self, feat):
+        return self.head(feat)
+
 
 class GreedyRows:
     """The greedy-row list of the next fused act (mz_greedy_rows: the instances that will act
@@ -205,6 +217,7 @@ class GreedyRows:
         self.event = torch.cuda.Event()
         self.lib = N.load()
         self.last_count = None
+        self.feat = None  # [n, LD] bf16 stem features of the listed rows (persistent)
 
     def issue(self, eps, seed, counter):
         """Launch the list kernels and the count's copy to the host on the current stream; the
@@ -236,10 +249,17 @@ class GreedyRows:
 
     @torch.no_grad()
     def __call__(self, fused, obs6, bits, eps, seed, counter):
+        key = (eps.data_ptr() if torch.is_tensor(eps) else float(eps), seed, counter)
+        if getattr(self, "_issued", None) != key:
+            self.issue(eps, seed, counter)
+        if self.feat is None:
+            self.feat = torch.zeros(self.n, LD, dtype=torch.bfloat16, device=self.rows.device)
+        # the stem reads the list's length on the device: it runs while the host waits for it
+        fused.rows_stem(obs6, bits, self.rows, self.count, self.feat)
         k = self.select(eps, seed, counter)
         if k:
             m = min(self.n, -(-k // self.BUCKET) * self.BUCKET)
-            q = fused.rows(obs6, bits, self.rows, m)
+            q = fused.rows_head(self.feat[:m])
             assert q.dtype == torch.bfloat16 and q.is_contiguous() and q.shape == (m, 4)
             N.check(self.lib.mz_greedy_scatter(q.data_ptr(), 4, self.rows.data_ptr(),
                                                self.count.data_ptr(), m, self.greedy.data_ptr(),
