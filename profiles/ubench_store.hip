@@ -75,12 +75,17 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&table, tlines * 128));
   CK(hipMemset(table, 1, tlines * 128));
   const size_t tmask = tlines - 1;
-  struct { const char* name; float us; } r[6];
+  struct { const char* name; float us; } r[11];
   r[0] = {"store sc1 (k_step policy)", run<16, 0>(waves, iters, out, table, tmask)};
   r[1] = {"store plain", run<-1, 0>(waves, iters, out, table, tmask)};
   r[2] = {"store nt", run<2, 0>(waves, iters, out, table, tmask)};
   r[3] = {"gather x2 + store sc1", run<16, 1>(waves, iters, out, table, tmask)};
   r[4] = {"gather x2 + store plain", run<-1, 1>(waves, iters, out, table, tmask)};
+  r[6] = {"store sc0", run<1, 0>(waves, iters, out, table, tmask)};
+  r[7] = {"store sc0 sc1", run<17, 0>(waves, iters, out, table, tmask)};
+  r[8] = {"store sc0 nt", run<3, 0>(waves, iters, out, table, tmask)};
+  r[9] = {"store sc1 nt", run<18, 0>(waves, iters, out, table, tmask)};
+  r[10] = {"store sc0 sc1 nt", run<19, 0>(waves, iters, out, table, tmask)};
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
