@@ -35,6 +35,7 @@ extern "C" {
 #define MZ_EALIGN (-5)       /* output pointer misaligned (window f32 needs 16 B) */
 
 #define MZ_MAX_DIM 127
+#define MZ_BANK_MAX_DIMS 64  /* maze sizes one bank can hold (mz_bank_create_dims) */
 #define MZ_WINDOW 15
 #define MZ_WINDOW_BITS 675   /* 3 x 15 x 15 */
 #define MZ_WINDOW_WORDS 22   /* uint32 words per instance in window_bits (bits 675..703 zero) */
@@ -194,11 +195,18 @@ int mz_expand_window(const uint32_t* bits_dev, float* out_dev, int32_t n, void* 
  * Mazes: Philox seed ^ ((3*bank + algo + 1) << 56) + slot + (fill epoch << 32). An exhausted
  * bank, or an instance whose algorithm / size the bank lacks, falls back to building in place. */
 int mz_bank_create(mz_handle* h, int32_t slots, int32_t dim, uint32_t algo_mask);
+/* The same for a list of ndims (<= MZ_BANK_MAX_DIMS) distinct maze sizes: `slots` mazes per
+ * (algorithm, size) — the variable-size envs (config 5: toroidal 17..79, instance i of size
+ * dims[i mod n]); a win copies a maze of the instance's own size. Size index di keys its slots'
+ * Philox seeds with di << 48 (di = 0: mz_bank_create's). */
+int mz_bank_create_dims(mz_handle* h, int32_t slots, const int32_t* dims, int32_t ndims,
+                        uint32_t algo_mask);
 /* Rebuild the slots of `bank` consumed since its last fill (every slot on the first fill). */
 int mz_bank_fill(mz_handle* h, int32_t bank, uint64_t seed, void* stream);
 /* Bank consumed by later mz_reset_done(regen_won) launches; -1 = none (build in place). */
 int mz_bank_use(mz_handle* h, int32_t bank);
-/* Consumed-slot counters of `bank` per algorithm id -> out3_dev [3] int32 (device). */
+/* Consumed-slot counters of `bank` per algorithm id and size index -> out3_dev [3][ndims] int32
+ * (device; [3] for a single-size bank). */
 int mz_bank_consumed(mz_handle* h, int32_t bank, int32_t* out3_dev, void* stream);
 
 /* Fused conv stem of the DQN/DDQN Q-network for acting (dqn_agent.py:19-57 forward,

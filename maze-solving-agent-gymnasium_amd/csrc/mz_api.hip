@@ -17,14 +17,15 @@
 #include "mz_common.h"
 #include "mz_kernels.h"
 
-struct MzBankStore {  // two banks x the enabled algorithms x K slots (mz_bank_*)
-  int K = 0, dim = 0, nA = 0;
+struct MzBankStore {  // two banks x the enabled algorithms x sizes x K slots (mz_bank_*)
+  int K = 0, nA = 0, nD = 0;
+  int dims[MZ_BANK_MAX_DIMS] = {};
   uint32_t amask = 0;
-  uint32_t* cells = nullptr;   // [2][nA][K][P*P]
-  uint32_t* planes = nullptr;  // [2][nA][K][PW]
-  uint32_t* meta0 = nullptr;   // [2][nA][K]
+  uint32_t* cells = nullptr;   // [2][nA][nD][K][P*P]
+  uint32_t* planes = nullptr;  // [2][nA][nD][K][PW]
+  uint32_t* meta0 = nullptr;   // [2][nA][nD][K]
   uint32_t* meta1 = nullptr;
-  int* heads = nullptr;        // [2][3] consumed slots per algorithm id
+  int* heads = nullptr;        // [2][3][nD] consumed slots per (algorithm id, size)
   // scratch the build writes and nobody reads: [K] ...
   uint32_t *s_posw = nullptr, *s_stw = nullptr, *s_curw = nullptr;
   uint8_t *s_last = nullptr, *s_algo = nullptr;
@@ -499,32 +500,45 @@ int mz_pair_surrogate(const float* lp_new_dev, const float* lp_old_dev, const fl
 
 int mz_stem_workspace_floats(int32_t n) { return n > 0 ? mz_stem_chunks(n) * 32 * 28 : 0; }
 
-int mz_bank_create(mz_handle* h, int32_t slots, int32_t dim, uint32_t algo_mask) {
+int mz_bank_create_dims(mz_handle* h, int32_t slots, const int32_t* dims, int32_t ndims,
+                        uint32_t algo_mask) {
   if (!h) return fail(MZ_EINVAL, "null handle");
   if (h->bank.K) return fail(MZ_EINVAL, "the handle already has a maze bank");
   if (slots < 1) return fail(MZ_EINVAL, "bank slots %d", slots);
   if (algo_mask == 0 || algo_mask > 7u) return fail(MZ_EINVAL, "algorithm mask %u", algo_mask);
-  int rc = check_dim(h, dim);
-  if (rc) return rc;
+  if (!dims || ndims < 1 || ndims > MZ_BANK_MAX_DIMS) return fail(MZ_EINVAL, "bank sizes %d", ndims);
+  for (int i = 0; i < ndims; ++i) {
+    int rc = check_dim(h, dims[i]);
+    if (rc) return rc;
+    for (int j = 0; j < i; ++j)
+      if (dims[j] == dims[i]) return fail(MZ_EINVAL, "bank size %d listed twice", dims[i]);
+  }
   DeviceGuard g(h->cfg.device);
   MzBankStore& b = h->bank;
   const MzDev& d = h->d;
   const int nA = __builtin_popcount(algo_mask);
-  const size_t S = 2 * (size_t)nA * slots, K = (size_t)slots;
+  const size_t S = 2 * (size_t)nA * ndims * slots, K = (size_t)slots;
+  int rc;
   if ((rc = alloc(h, &b.cells, S * d.P * d.P)) || (rc = alloc(h, &b.planes, S * d.PW)) ||
-      (rc = alloc(h, &b.meta0, S)) || (rc = alloc(h, &b.meta1, S)) || (rc = alloc(h, &b.heads, 6)) ||
-      (rc = alloc(h, &b.s_posw, K)) ||
+      (rc = alloc(h, &b.meta0, S)) || (rc = alloc(h, &b.meta1, S)) ||
+      (rc = alloc(h, &b.heads, (size_t)6 * ndims)) || (rc = alloc(h, &b.s_posw, K)) ||
       (rc = alloc(h, &b.s_stw, K)) || (rc = alloc(h, &b.s_curw, K)) || (rc = alloc(h, &b.s_last, K)) ||
       (rc = alloc(h, &b.s_algo, K)))
     return rc;
-  int full[6];  // first fill builds every slot of the algorithms the bank holds
-  for (int i = 0; i < 6; ++i) full[i] = ((algo_mask >> (i % 3)) & 1u) ? slots : 0;
-  MZ_HIP(hipMemcpy(b.heads, full, sizeof full, hipMemcpyHostToDevice));
+  // first fill builds every slot of the algorithms the bank holds
+  std::vector<int> full((size_t)6 * ndims);
+  for (int i = 0; i < 6 * ndims; ++i) full[i] = ((algo_mask >> ((i / ndims) % 3)) & 1u) ? slots : 0;
+  MZ_HIP(hipMemcpy(b.heads, full.data(), full.size() * sizeof(int), hipMemcpyHostToDevice));
   b.K = slots;
-  b.dim = dim;
+  b.nD = ndims;
+  for (int i = 0; i < ndims; ++i) b.dims[i] = dims[i];
   b.nA = nA;
   b.amask = algo_mask;
   return MZ_OK;
+}
+
+int mz_bank_create(mz_handle* h, int32_t slots, int32_t dim, uint32_t algo_mask) {
+  return mz_bank_create_dims(h, slots, &dim, 1, algo_mask);
 }
 
 int mz_bank_fill(mz_handle* h, int32_t bank, uint64_t seed, void* stream) {
@@ -536,7 +550,8 @@ int mz_bank_fill(mz_handle* h, int32_t bank, uint64_t seed, void* stream) {
   const size_t K = (size_t)b.K, P = (size_t)h->d.P;
   for (int a = 0; a < 3; ++a) {
     if (!((b.amask >> a) & 1u)) continue;
-    const size_t blk = ((size_t)bank * b.nA + mz_bank_aidx(b.amask, a)) * K;
+    for (int di = 0; di < b.nD; ++di) {
+      const size_t blk = (((size_t)bank * b.nA + mz_bank_aidx(b.amask, a)) * b.nD + di) * K;
     MzDev bd = h->d;  // same pitch / flags; instance arrays = this block's slots + scratch
     bd.B = b.K;
     bd.cells = b.cells + blk * P * P;
@@ -549,10 +564,12 @@ int mz_bank_fill(mz_handle* h, int32_t bank, uint64_t seed, void* stream) {
     bd.last_term = b.s_last;
     bd.algo = b.s_algo;
     bd.bk_K = 0;
-    int* head = b.heads + 3 * bank + a;
-    const uint64_t key = seed ^ ((uint64_t)(3 * bank + a + 1) << 56);
-    MZ_HIP(mz_launch_bank_fill(bd, head, b.K, a, b.dim, key, b.epoch[bank], s));
+    int* head = b.heads + (3 * bank + a) * b.nD + di;
+    // (size index di = 0 keeps the single-size bank's keys)
+    const uint64_t key = seed ^ ((uint64_t)(3 * bank + a + 1) << 56) ^ ((uint64_t)di << 48);
+    MZ_HIP(mz_launch_bank_fill(bd, head, b.K, a, b.dims[di], key, b.epoch[bank], s));
     MZ_HIP(hipMemsetAsync(head, 0, sizeof(int), s));
+    }
   }
   b.epoch[bank] += 1;
   return MZ_OK;
@@ -568,22 +585,25 @@ int mz_bank_use(mz_handle* h, int32_t bank) {
   const MzBankStore& b = h->bank;
   if (!b.K) return fail(MZ_EINVAL, "no maze bank (mz_bank_create)");
   if (bank > 1) return fail(MZ_EINVAL, "bank %d", bank);
-  const size_t blk = (size_t)bank * b.nA * b.K, P = (size_t)d.P;
+  const size_t blk = (size_t)bank * b.nA * b.nD * b.K, P = (size_t)d.P;
   d.bk_K = b.K;
-  d.bk_dim = b.dim;
+  d.bk_nd = b.nD;
+  for (int i = 0; i < 128; ++i) d.bk_didx[i] = -1;
+  for (int i = 0; i < b.nD; ++i) d.bk_didx[b.dims[i]] = (int8_t)i;
   d.bk_amask = b.amask;
   d.bk_cells = b.cells + blk * P * P;
   d.bk_planes = b.planes + blk * d.PW;
   d.bk_meta0 = b.meta0 + blk;
   d.bk_meta1 = b.meta1 + blk;
-  d.bk_head = b.heads + 3 * bank;
+  d.bk_head = b.heads + 3 * bank * b.nD;
   return MZ_OK;
 }
 
 int mz_bank_consumed(mz_handle* h, int32_t bank, int32_t* out3_dev, void* stream) {
   if (!h || !h->bank.K || !out3_dev || bank < 0 || bank > 1) return fail(MZ_EINVAL, "bad arguments");
   DeviceGuard g(h->cfg.device);
-  MZ_HIP(hipMemcpyAsync(out3_dev, h->bank.heads + 3 * bank, 3 * sizeof(int32_t),
+  const int nd = h->bank.nD;
+  MZ_HIP(hipMemcpyAsync(out3_dev, h->bank.heads + 3 * bank * nd, 3 * nd * sizeof(int32_t),
                         hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)));
   return MZ_OK;
 }

@@ -64,16 +64,18 @@ struct MzDev {
   int* ticket;              // [16]: [0] exit ticket of k_reset_list (done-count consumption),
                             // [MZ_TICKET_PYERR] CPython-generation set-table overflow flag
   // Active maze bank (mz_bank_*): mazes generated ahead of time that a win copies in instead
-  // of building one inside the reset launch. Slot j of algorithm a lives at index
-  // bk_aidx(a) * bk_K + j of the bank arrays; bk_head[a] counts the slots consumed so far.
-  int bk_K;                 // slots per algorithm; 0 = no bank in use
-  int bk_dim;               // maze size of the bank's mazes
+  // of building one inside the reset launch. Slot j of algorithm a and maze size index di lives
+  // at index (bk_aidx(a) * bk_nd + di) * bk_K + j of the bank arrays; bk_head[a * bk_nd + di]
+  // counts the slots consumed so far.
+  int bk_K;                 // slots per (algorithm, size); 0 = no bank in use
+  int bk_nd;                // maze sizes the bank holds
+  int8_t bk_didx[128];      // maze size N -> its index in the bank, -1: not held
   uint32_t bk_amask;        // algorithms the bank holds (bit a)
   const uint32_t* bk_cells; // [slots][P*P]
   const uint32_t* bk_planes;// [slots][PW]
   const uint32_t* bk_meta0; // [slots]
   const uint32_t* bk_meta1; // [slots]
-  int* bk_head;             // [3]
+  int* bk_head;             // [3][bk_nd]
 };
 
 __host__ __device__ inline int mz_bank_aidx(uint32_t amask, int a) {

@@ -592,12 +592,15 @@ __global__ __launch_bounds__(WAVE) void k_reset_list(MzDev d, const int32_t* idx
 // reset_one then rebuilds the per-episode state). Returns false (caller builds in place) when no
 // bank is in use, the bank does not hold algorithm a or size N, or it is exhausted.
 __device__ bool bank_take(const MzDev& d, int e, int a, int N) {
-  if (d.bk_K == 0 || N != d.bk_dim || !((d.bk_amask >> a) & 1u)) return false;
+  if (d.bk_K == 0 || N < 0 || N >= 128 || !((d.bk_amask >> a) & 1u)) return false;
+  const int di = d.bk_didx[N];
+  if (di < 0) return false;
   int slot = 0;
-  if (threadIdx.x == 0) slot = atomicAdd(&d.bk_head[a], 1);
+  if (threadIdx.x == 0) slot = atomicAdd(&d.bk_head[a * d.bk_nd + di], 1);
   slot = __shfl(slot, 0);
   if (slot >= d.bk_K) return false;
-  const size_t src = (size_t)mz_bank_aidx(d.bk_amask, a) * d.bk_K + slot, es = (size_t)e;
+  const size_t src = ((size_t)mz_bank_aidx(d.bk_amask, a) * d.bk_nd + di) * d.bk_K + slot;
+  const size_t es = (size_t)e;
   const size_t pp = (size_t)d.P * d.P;
   const uint32_t* cs = d.bk_cells + src * pp;
   uint32_t* cd = d.cells + es * pp;

@@ -38,7 +38,8 @@ EXPORTS = ["mz_last_error", "mz_device_count", "mz_create", "mz_destroy", "mz_lo
            "mz_generate", "mz_generate_ex", "mz_generate_state", "mz_reset_all", "mz_reset_list", "mz_reset_done", "mz_step", "mz_step_ex", "mz_direction_mask",
            "mz_act", "mz_step_act", "mz_expand_window", "mz_set_algorithm", "mz_query", "mz_get_grid",
            "mz_difficulty", "mz_maze_complexity", "mz_maze_metrics", "mz_get_meta", "mz_discounted_returns", "mz_q_front",
-           "mz_bank_create", "mz_bank_fill", "mz_bank_use", "mz_bank_consumed",
+           "mz_bank_create", "mz_bank_create_dims", "mz_bank_fill", "mz_bank_use",
+           "mz_bank_consumed",
            "mz_stem_forward", "mz_stem_backward", "mz_stem_workspace_floats", "mz_adamw_flat",
            "mz_pair_surrogate", "mz_leaky_relu_bf16", "mz_colsum_f32",
            "mz_replay_gather", "mz_host_alloc", "mz_host_free", "mz_q_front_rows", "mz_greedy_rows",
@@ -94,6 +95,7 @@ def load(build_if_missing=True):
     L.mz_maze_complexity.argtypes = [vp] + [C.c_int32] * 6 + [C.POINTER(C.c_double)] * 2
     L.mz_maze_metrics.argtypes = [vp, vp, C.c_int32, vp, vp]
     L.mz_bank_create.argtypes = [vp, C.c_int32, C.c_int32, C.c_uint32]
+    L.mz_bank_create_dims.argtypes = [vp, C.c_int32, vp, C.c_int32, C.c_uint32]
     L.mz_bank_fill.argtypes = [vp, C.c_int32, C.c_uint64, vp]
     L.mz_bank_use.argtypes = [vp, C.c_int32]
     L.mz_bank_consumed.argtypes = [vp, C.c_int32, vp, vp]

@@ -29,6 +29,8 @@ def main(argv=None):
     ap.add_argument("--eval-mazes", type=int, default=1000)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--eager-update", action="store_true", help="no captured minibatch step")
+    ap.add_argument("--no-bank", action="store_true",
+                    help="build winners' new mazes inline instead of copying them from a maze bank")
     ap.add_argument("--f32-window-update", action="store_true",
                     help="update through the f32 window + torch conv instead of the HIP bit stem")
     a = ap.parse_args(argv)
@@ -44,7 +46,7 @@ def main(argv=None):
                    device=dev, done_list=False, reward64=True, window=False, window_bits=True)
     tr = VectorPPOTrainer(env, dev, gamma=a.gamma, batch_size=a.batch, ppo_steps=a.ppo_steps,
                           pool_size=a.pool, seed=a.seed, use_graph=not a.eager_update,
-                          bit_stem=not a.f32_window_update,
+                          bit_stem=not a.f32_window_update, bank=not a.no_bank,
                           allreduce=GradAllReduce() if world > 1 else None)
     if world > 1:
         broadcast_params(tr.net)

@@ -25,8 +25,12 @@ from ..agents.ppo import ActorCriticNet, PPOMinibatchGraph, make_optimizer, opti
 class VectorPPOTrainer:
     def __init__(self, env, device, actor_lr=3e-4, critic_lr=1e-4, gamma=0.9, batch_size=2048,
                  ppo_steps=4, pool_size=65536, hidden_dim=1024, h_channels=32, seed=0,
-                 allreduce=None, act_bf16=True, use_graph=True, bit_stem=True):
+                 allreduce=None, act_bf16=True, use_graph=True, bit_stem=True, bank=True):
         self.env = env
+        if bank and env.device.type == "cuda":
+            # winners' new mazes (update_maze) copied from a bank built ahead of time on a side
+            # stream, one per grid size of the variable-size env, instead of built inline
+            env.enable_bank(dims=getattr(env, "dims_in_use", None))
         self.device = torch.device(device)
         torch.manual_seed(seed)
         self.net = ActorCriticNet(3, 6, 4, h_channels, hidden_dim).to(self.device)

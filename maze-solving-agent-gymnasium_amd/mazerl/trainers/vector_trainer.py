@@ -31,7 +31,8 @@ class VectorOffPolicyTrainer:
         if regen_won and bank:
             # winners' new mazes come from a bank refilled on a side stream (VectorMazeEnv.
             # enable_bank): a maze build is a ~1 ms serial chain that would stall the step
-            env.enable_bank(algorithms=[0, 1, 2] if curriculum else None)
+            env.enable_bank(algorithms=[0, 1, 2] if curriculum else None,
+                            dims=getattr(env, "dims_in_use", None))
         self.seed = seed
         # fused: the per-step bookkeeping and the replay push as HIP launches (mz_trainer_tick,
         # mz_replay_push) instead of ~25 torch ops; False keeps the torch path (A/B, tests)
@@ -138,6 +139,7 @@ def make_env(num_envs, dims, toroidal=False, algorithm="r-prim", seed=0x5EED0000
     env = VectorMazeEnv(num_envs, dims[0], toroidal=toroidal, enrich=True, device=device,
                         max_dim=max(dims), algorithm=algorithm, seed=seed, generate=len(dims) == 1,
                         **kw)
+    env.dims_in_use = sorted(set(dims))  # (a maze bank for the winners then holds every size)
     if len(dims) > 1:
         ids = torch.arange(num_envs, device=env.device)
         for j, n in enumerate(dims):

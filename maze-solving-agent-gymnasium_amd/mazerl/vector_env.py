@@ -233,21 +233,28 @@ class VectorMazeEnv:
 
     # ---------------------------------------------------------------------------------------
     # Maze bank: winners' new mazes are generated ahead of time, in bulk, on a side stream.
-    def enable_bank(self, slots=None, swap_every=8, algorithms=None, seed=0xBA4C0000):
-        """Two banks of `slots` mazes per algorithm (size maze_dim): reset_done(regen_won=True)
-        consumes the active one; every `swap_every` such calls the banks swap and the retired
-        one is refilled on a side stream (ordered after the launches that consumed it; the main
-        stream waits for a refill only when that bank comes back). Default slots: B / 8."""
+    def enable_bank(self, slots=None, swap_every=8, algorithms=None, seed=0xBA4C0000, dims=None):
+        """Two banks of `slots` mazes per algorithm (size maze_dim, or per size of `dims` — the
+        variable-size envs): reset_done(regen_won=True) consumes the active one; every
+        `swap_every` such calls the banks swap and the retired one is refilled on a side stream
+        (ordered after the launches that consumed it; the main stream waits for a refill only
+        when that bank comes back). Default slots: B / 8 (split over the sizes, >= 16 each)."""
         if self._bank is not None:
             return
-        K = int(slots or max(64, self.num_envs // 8))
+        dims = [self.maze_dim] if dims is None else sorted({int(d) for d in dims})
+        K = int(slots or max(64 // len(dims) if len(dims) > 1 else 64,
+                             self.num_envs // 8 // len(dims), 16))
         if algorithms is None:
             mask = sum(1 << i for i in self.algos_in_use) or 7
         else:
             ids = [ALGOS[a] if isinstance(a, str) else int(a) for a in algorithms]
             mask = sum(1 << i for i in set(ids))
-        N.check(self.lib.mz_bank_create(self._h, K, self.maze_dim, mask))
-        self._bank = dict(K=K, swap=int(swap_every), calls=0, cur=0, seed=int(seed),
+        if len(dims) == 1:
+            N.check(self.lib.mz_bank_create(self._h, K, dims[0], mask))
+        else:
+            arr = (N.C.c_int32 * len(dims))(*dims)
+            N.check(self.lib.mz_bank_create_dims(self._h, K, arr, len(dims), mask))
+        self._bank = dict(K=K, dims=dims, swap=int(swap_every), calls=0, cur=0, seed=int(seed),
                           side=torch.cuda.Stream(self.device), ready=[None, None])
         st = self._stream()
         for b in (0, 1):
@@ -275,11 +282,13 @@ class VectorMazeEnv:
         bk["ready"][old] = ev
 
     def bank_consumed(self, bank=None):
-        """int32 [3]: slots of `bank` (default: the active one) consumed per algorithm id."""
-        out = torch.zeros(3, dtype=torch.int32, device=self.device)
+        """int32 [3] (a single-size bank) or [3, n_sizes]: slots of `bank` (default: the active
+        one) consumed per algorithm id (and size)."""
+        nd = len(self._bank["dims"])
+        out = torch.zeros(3 * nd, dtype=torch.int32, device=self.device)
         b = self._bank["cur"] if bank is None else int(bank)
         N.check(self.lib.mz_bank_consumed(self._h, b, out.data_ptr(), self._stream()))
-        return out
+        return out if nd == 1 else out.view(3, nd)
 
     def reset_done_list(self, regen_won=False, seed=None):
         """Auto-reset from the step's device done list (consumes done_count)."""

@@ -131,3 +131,56 @@ def test_bank_rejects_bad_arguments():
     assert L.mz_bank_use(env._h, 2) != 0
     assert L.mz_bank_use(env._h, -1) == 0
     env.close()
+
+
+def test_multi_size_bank_serves_each_size_its_slots():
+    """A bank over several maze sizes (mz_bank_create_dims, the variable-size configs): a winner
+    gets a slot maze of its own size — slot j of size index di is exactly the maze k_build makes
+    for instance j with seed bank_seed ^ ((3b + a + 1) << 56) ^ (di << 48)."""
+    from mazerl.trainers.vector_trainer import make_env
+    dims = [15, 19, 23]
+    B, K, seed = 48, 32, 0xBA4C0000
+    env = make_env(B, dims, algorithm="dfs", seed=5, device="cuda", done_list=False)
+    env.enable_bank(slots=K, swap_every=10 ** 9, algorithms=["dfs"], seed=seed, dims=dims)
+    size = [env.query(i)["n"] for i in range(B)]
+    assert size == [dims[i % 3] for i in range(B)]
+    won = np.zeros(B, bool)
+    solver = Solver(env)
+    for _ in range(3000):
+        env.step(solver.actions())
+        won |= env.terminated.cpu().numpy().astype(bool)
+        env.reset_done(regen_won=True)
+        if won.all():
+            break
+    assert won.all()
+    torch.cuda.synchronize()
+    consumed = env.bank_consumed().cpu().numpy()
+    assert consumed.shape == (3, 3) and consumed[0].sum() == 0 and consumed[2].sum() == 0
+    assert (consumed[1] >= B // 3).all()
+    for di, dim in enumerate(dims):
+        n = int(min(consumed[1, di], K))
+        from mazerl import VectorMazeEnv
+        ref = VectorMazeEnv(K, dim, enrich=True, device="cuda",
+                            seed=seed ^ ((3 * 0 + 1 + 1) << 56) ^ (di << 48), algorithm="dfs")
+        slots = {signature(ref, j): j for j in range(n)}
+        ref.close()
+        for i in range(di, B, 3):
+            assert env.query(i)["n"] == dim  # same size after the win (bank or fallback build)
+            if consumed[1, di] <= K:
+                assert signature(env, i) in slots, (dim, i)
+    env.close()
+
+
+def test_multi_size_bank_rejects_bad_sizes():
+    from mazerl import VectorMazeEnv, _native as N
+    env = VectorMazeEnv(8, 31, enrich=True, device="cuda", seed=1)
+    L = env.lib
+
+    def create(dims):
+        arr = (N.C.c_int32 * len(dims))(*dims)
+        return L.mz_bank_create_dims(env._h, 4, arr, len(dims), 1)
+    assert create([15, 20]) != 0    # even size
+    assert create([15, 15]) != 0    # listed twice
+    assert create([15, 33]) != 0    # larger than the handle's pitch
+    assert create([15, 21, 31]) == 0
+    env.close()
