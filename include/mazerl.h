@@ -382,7 +382,7 @@ int mz_greedy_scatter(const uint16_t* q_dev, int32_t ldq, const int32_t* rows_de
  * fc): w_l f32 [out_l][in_l] -> dw_l bf16 (round to nearest even, torch's .to(bfloat16)); fc1's
  * first conv_out columns permuted from torch's channel-major flatten (c * Q + q, Q = conv_out /
  * conv_ch) to the fused stem's position-major order (q * conv_ch + c), rows padded with zeros to
- * ld0; biases b_l -> db_l. One launch. */
+ * ld0 (in0 <= 2048); biases b_l -> db_l. One launch. */
 int mz_head_bf16(const float* w0, const float* b0, const float* w1, const float* b1,
                  const float* w2, const float* b2, int32_t out0, int32_t in0, int32_t out1,
                  int32_t in1, int32_t out2, int32_t in2, int32_t ld0, int32_t conv_out,

@@ -747,7 +747,7 @@ int mz_head_bf16(const float* w0, const float* b0, const float* w1, const float*
   if (!w0 || !b0 || !w1 || !b1 || !w2 || !b2 || !dw0 || !db0 || !dw1 || !db1 || !dw2 || !db2)
     return fail(MZ_EINVAL, "bad arguments");
   if (out0 <= 0 || out1 <= 0 || out2 <= 0 || in1 != out0 || in2 != out1 || in0 > ld0 ||
-      conv_ch <= 0 || conv_out < 0 || conv_out > in0 || conv_out % conv_ch != 0)
+      conv_ch <= 0 || conv_out < 0 || conv_out > in0 || conv_out % conv_ch != 0 || in0 > 2048)
     return fail(MZ_EINVAL, "head shapes");
   MzHeadBf16 h{{w0, w1, w2}, {b0, b1, b2}, {dw0, dw1, dw2}, {db0, db1, db2},
                {out0, out1, out2}, {in0, in1, in2}, ld0, conv_out, conv_ch};

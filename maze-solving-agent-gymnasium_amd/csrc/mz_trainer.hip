@@ -107,27 +107,35 @@ __device__ inline uint16_t bf16_rne(float f) {  // torch's float -> bfloat16 (ro
   return (uint16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
 }
 
+// Blocks [0, out0): one fc1 row each — the f32 row read coalesced into LDS, the permuted /
+// padded bf16 row written coalesced from it (a column gather straight from global memory strides
+// 49 floats between neighbouring lanes: 31 us per call vs ~3 for the bytes). The other blocks
+// convert fc2, fc3 and the biases grid-stride.
+constexpr int HEAD_MAX_IN = 2048;
 __global__ __launch_bounds__(256) void k_head_bf16(MzHeadBf16 h) {
-  const int64_t n0 = (int64_t)h.out[0] * h.ld0;
+  __shared__ float row[HEAD_MAX_IN];
+  if ((int)blockIdx.x < h.out[0]) {
+    const int o = blockIdx.x;
+    const float* src = h.w[0] + (size_t)o * h.in[0];
+    for (int j = threadIdx.x; j < h.in[0]; j += blockDim.x) row[j] = src[j];
+    __syncthreads();
+    const int nq = h.conv_out / h.conv_ch;
+    uint16_t* dst = h.dw[0] + (size_t)o * h.ld0;
+    for (int j = threadIdx.x; j < h.ld0; j += blockDim.x) {
+      float v = 0.0f;
+      if (j < h.conv_out) v = row[(j % h.conv_ch) * nq + j / h.conv_ch];  // kernel q*C+c <- torch c*Q+q
+      else if (j < h.in[0]) v = row[j];
+      dst[j] = bf16_rne(v);
+    }
+    return;
+  }
   const int64_t n1 = (int64_t)h.out[1] * h.in[1];
   const int64_t n2 = (int64_t)h.out[2] * h.in[2];
-  const int64_t total = n0 + n1 + n2 + h.out[0] + h.out[1] + h.out[2];
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t total = n1 + n2 + h.out[0] + h.out[1] + h.out[2];
+  const int64_t nb = (int64_t)gridDim.x - h.out[0];
+  for (int64_t t = ((int64_t)blockIdx.x - h.out[0]) * blockDim.x + threadIdx.x; t < total;
+       t += nb * blockDim.x) {
     int64_t k = t;
-    if (k < n0) {  // fc1: row o, column j of the padded, permuted [out0, ld0] weight
-      const int o = (int)(k / h.ld0), j = (int)(k - (int64_t)o * h.ld0);
-      float v = 0.0f;
-      if (j < h.conv_out) {  // kernel feature j = q * C + c  <-  torch column c * Q + q
-        const int c = j % h.conv_ch, q = j / h.conv_ch;
-        v = h.w[0][(size_t)o * h.in[0] + (size_t)c * (h.conv_out / h.conv_ch) + q];
-      } else if (j < h.in[0]) {
-        v = h.w[0][(size_t)o * h.in[0] + j];
-      }
-      h.dw[0][k] = bf16_rne(v);
-      continue;
-    }
-    k -= n0;
     if (k < n1) { h.dw[1][k] = bf16_rne(h.w[1][k]); continue; }
     k -= n1;
     if (k < n2) { h.dw[2][k] = bf16_rne(h.w[2][k]); continue; }
@@ -266,11 +274,12 @@ hipError_t mz_launch_greedy_scatter(const uint16_t* q, int ldq, const int32_t* r
 }
 
 hipError_t mz_launch_head_bf16(const MzHeadBf16& h, hipStream_t s) {
-  const int64_t total = (int64_t)h.out[0] * h.ld0 + (int64_t)h.out[1] * h.in[1] +
-                        (int64_t)h.out[2] * h.in[2] + h.out[0] + h.out[1] + h.out[2];
-  int64_t blocks = (total + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(k_head_bf16, dim3((unsigned)blocks), dim3(256), 0, s, h);
+  if (h.in[0] > HEAD_MAX_IN) return hipErrorInvalidValue;
+  const int64_t rest = (int64_t)h.out[1] * h.in[1] + (int64_t)h.out[2] * h.in[2] + h.out[0] +
+                       h.out[1] + h.out[2];
+  int64_t blocks = (rest + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(k_head_bf16, dim3((unsigned)(h.out[0] + blocks)), dim3(256), 0, s, h);
   return hipGetLastError();
 }
 
