@@ -5,7 +5,7 @@
 #   run (GPU box):          profiles/exp_probes.sh run <outdir>
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
-VARIANTS="0 1 2 4 8 16 32 64 128 256 257 34 335 367"
+VARIANTS="${PROBES:-0 1 2 4 8 16 32 64 128 256 257 34 335 367}"
 if [ "$1" = build ]; then
   for v in $VARIANTS; do
     "$R/profiles/build_variant.sh" "$R/profiles/_bin/probe_$v.so" -DMZ_PROBE=$v &
