@@ -41,7 +41,7 @@
 // MZ_PROBE mask bits: 1 no penalty-table staging, 2 no window-bit assembly, 4 no autoreset plane /
 // count work, 8 no per-instance output stores, 16 no f32 window stores, 32 window stores of a
 // constant (no LDS reads), 64 no state stores, 128 return at once (launch + dispatch floor),
-// 256 no level-2 loads
+// 256 no level-2 loads, 512 window rows loaded but not assembled (zero windows: faster stores)
 #ifndef MZ_PROBE
 #define MZ_PROBE 0
 #endif
@@ -432,9 +432,13 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
         win_row_bits<TOR>(wr[it], g, geo_row<TOR>(g, i), gg & 0xFF, (gg >> 8) & 0xFF,
                           ((s_ >> 8) & 0xFF) - 1, ((s_ >> 16) & 0xFF) - 1, s_ & 1, c0, c1, c2);
         const int base = j * 675 + i * 15;
-        cat_put(cat, base, c0);
-        cat_put(cat, base + 225, c1);
-        cat_put(cat, base + 450, c2);
+        if (MZ_PROBE & 512) {  // probe: the rows are loaded and decoded, not assembled
+          if ((c0 ^ (c1 << 1) ^ (c2 << 2)) == ((uint32_t)(lane * 77 + it) & 0x1FFFFu)) cat[0] = 1u;
+        } else {
+          cat_put(cat, base, c0);
+          cat_put(cat, base + 225, c1);
+          cat_put(cat, base + 450, c2);
+        }
       }
     }
   }
