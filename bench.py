@@ -77,7 +77,7 @@ def win_rate(a, dev, rank=0, world=1):
     from mazerl import VectorMazeEnv
     from mazerl.agents.dqn import VectorDQNLearner
     from mazerl.distributed import GradAllReduce, broadcast_params
-    from mazerl.trainers.vector_trainer import VectorOffPolicyTrainer, evaluate
+    from mazerl.trainers.vector_trainer import VectorOffPolicyTrainer, best_of_mazes, evaluate
     env = VectorMazeEnv(a.envs, a.dim, enrich=True, device=dev, algorithm=a.algo,
                         seed=0xA11CE + rank * a.envs, done_list=False, window=False,
                         window_bits=True)  # acting reads the bits
@@ -104,7 +104,13 @@ def win_rate(a, dev, rank=0, world=1):
         return None
     g, _ = evaluate(L, a.eval_mazes, a.dim, a.algo, seed=0x7E570000, eps=0.0, device=dev)
     e, _ = evaluate(L, a.eval_mazes, a.dim, a.algo, seed=0x7E570000, eps=0.1, device=dev)
-    return {"greedy": g, "eps_0.1": e, "eval_mazes": a.eval_mazes, "variant": "ddqn",
+    # the same protocol on mazes chosen as the reference's env chooses them: the easiest (McClendon
+    # difficulty) of 6 candidates (base_maze_env.py:78-97) — the README's "new mazes" win-rates
+    mz6 = best_of_mazes(a.eval_mazes, a.dim, a.algo, seed=0x7E580000, device=dev)
+    g6, _ = evaluate(L, a.eval_mazes, a.dim, a.algo, seed=0x7E580000, eps=0.0, device=dev, mazes=mz6)
+    e6, _ = evaluate(L, a.eval_mazes, a.dim, a.algo, seed=0x7E580000, eps=0.1, device=dev, mazes=mz6)
+    return {"greedy": g, "eps_0.1": e, "greedy_best_of_6": g6, "eps_0.1_best_of_6": e6,
+            "eval_mazes": a.eval_mazes, "variant": "ddqn",
             "ranks": world, "train_vector_steps": a.train_steps + 20,
             "train_seconds_steady": round(secs, 3),
             "train_env_steps_per_s": a.envs * a.train_steps * world / secs,
@@ -116,7 +122,9 @@ def win_rate(a, dev, rank=0, world=1):
             "grad_allreduce": (f"{dist.get_backend()} ({'RCCL' if dist.get_backend() == 'nccl' else 'rehearsal'}), "
                                "one 8.56 MB fp32 bucket per update between two graph replays")
                               if world > 1 else None,
-            "note": "fresh GPU-generated mazes never seen in training (test(new=True) protocol)"}
+            "note": "fresh GPU-generated mazes never seen in training (test(new=True) protocol); "
+                    "*_best_of_6: each maze the easiest of 6 candidates by McClendon difficulty, "
+                    "as the reference's env selects new mazes (base_maze_env.py:78-97)"}
 
 
 BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X bf16 MFMA, dense (MI355X_MICROARCH.md)

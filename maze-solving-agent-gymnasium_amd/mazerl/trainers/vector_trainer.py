@@ -152,14 +152,46 @@ def make_env(num_envs, dims, toroidal=False, algorithm="r-prim", seed=0x5EED0000
     return env
 
 
+def best_of_mazes(num_mazes, dim, algorithm="r-prim", seed=0x7E57, device=None, candidates=6):
+    """The reference's maze selection for new mazes (BaseMazeEnv.generate_maze,
+    base_maze_env.py:78-97): per maze, `candidates` generated mazes, keep the one with the
+    smallest McClendon difficulty (strict <: the first minimum; native mz_difficulty). The
+    candidates are GPU-generated (Philox); returns (grids uint8 [n, dim, dim], start_goal [n, 4])
+    for VectorMazeEnv.load_mazes."""
+    import numpy as np
+    from ..difficulty import maze_difficulty
+    cand = VectorMazeEnv(num_mazes * candidates, dim, enrich=True, device=device,
+                         algorithm=algorithm, seed=seed, done_list=False, pos=False, window=False,
+                         window_bits=False)
+    grids = np.zeros((num_mazes, dim, dim), np.uint8)
+    sg = np.zeros((num_mazes, 4), np.int32)
+    for k in range(num_mazes):
+        best = None
+        for c in range(candidates):
+            i = k * candidates + c
+            q = cand.query(i)
+            g = cand.grid(i)
+            s, t = (q["start_r"], q["start_c"]), (q["goal_r"], q["goal_c"])
+            d = maze_difficulty(g, s, t)
+            if best is None or d < best[0]:
+                best = (d, g, s + t)
+        grids[k], sg[k] = best[1], best[2]
+    cand.close()
+    return grids, sg
+
+
 @torch.no_grad()
 def evaluate(learner, num_mazes, dim, algorithm="r-prim", seed=0x7E57, eps=0.0, toroidal=False,
-             device=None, max_vector_steps=None):
+             device=None, max_vector_steps=None, mazes=None):
     """Fraction of `num_mazes` fresh mazes solved in one episode (terminated before truncation).
-    `dim` may be a list of sizes (instance i gets dim[i % len])."""
+    `dim` may be a list of sizes (instance i gets dim[i % len]). `mazes` = (grids, start_goal)
+    to play instead of generated ones (e.g. best_of_mazes: the reference's best-of-6 selection)."""
     bits = getattr(learner, "supports_bits", False)
     env = make_env(num_mazes, dim, toroidal=toroidal, algorithm=algorithm, seed=seed,
                    device=device, done_list=False, pos=False, window=not bits, window_bits=True)
+    if mazes is not None:
+        env.load_mazes(*mazes)
+        env.reset()
     dim = max(dim) if not isinstance(dim, int) else dim
     finished = torch.zeros(num_mazes, dtype=torch.bool, device=env.device)
     won = torch.zeros(num_mazes, dtype=torch.bool, device=env.device)

@@ -116,3 +116,32 @@ def test_trainer_step_uses_greedy_rows():
     assert L._rows is not None and 0 < L._rows.last_count <= B
     assert int((env.actions < 0).sum()) == 0 and int((env.actions > 3).sum()) == 0
     env.close()
+
+
+def test_best_of_mazes_picks_the_easiest_candidate():
+    """best_of_mazes == the reference's generate_maze selection (base_maze_env.py:78-97) over the
+    same candidates: min McClendon difficulty, first minimum; evaluate() plays the loaded mazes."""
+    import numpy as np
+    from mazerl import VectorMazeEnv
+    from mazerl.difficulty import maze_difficulty
+    from mazerl.trainers.vector_trainer import best_of_mazes
+    n, dim, c = 5, 21, 6
+    grids, sg = best_of_mazes(n, dim, "dfs", seed=77, device="cuda:0", candidates=c)
+    ref = VectorMazeEnv(n * c, dim, enrich=True, device="cuda:0", algorithm="dfs", seed=77)
+    for k in range(n):
+        ds = []
+        for j in range(c):
+            q = ref.query(k * c + j)
+            ds.append(maze_difficulty(ref.grid(k * c + j), (q["start_r"], q["start_c"]),
+                                      (q["goal_r"], q["goal_c"])))
+        j = int(np.argmin(ds))  # first minimum
+        q = ref.query(k * c + j)
+        assert np.array_equal(grids[k], ref.grid(k * c + j))
+        assert tuple(sg[k]) == (q["start_r"], q["start_c"], q["goal_r"], q["goal_c"])
+    ref.close()
+    env = VectorMazeEnv(n, dim, enrich=True, device="cuda:0", generate=False, done_list=False)
+    env.load_mazes(grids, sg)
+    env.reset()
+    for k in range(n):
+        assert np.array_equal(env.grid(k), grids[k])
+    env.close()
