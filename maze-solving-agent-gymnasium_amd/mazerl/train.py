@@ -14,7 +14,7 @@ import torch
 
 from .agents.dqn import VectorDQNLearner
 from .distributed import GradAllReduce, allreduce_sum, broadcast_params, init_from_env
-from .trainers.vector_trainer import VectorOffPolicyTrainer, evaluate
+from .trainers.vector_trainer import VectorOffPolicyTrainer, best_of_mazes, evaluate
 from .vector_env import VectorMazeEnv
 
 
@@ -81,6 +81,12 @@ def main(argv=None):
         eval_algo = "r-prim" if a.algo == "mixed" else a.algo
         greedy, kg = evaluate(learner, a.eval_mazes, a.dim, eval_algo, seed=0x7E570000, eps=0.0, device=dev)
         epsr, ke = evaluate(learner, a.eval_mazes, a.dim, eval_algo, seed=0x7E570000, eps=a.eps_final, device=dev)
+        # fresh mazes as the reference's env picks them: the easiest of 6 (base_maze_env.py:78-97)
+        mz6 = best_of_mazes(a.eval_mazes, a.dim, eval_algo, seed=0x7E580000, device=dev)
+        g6, _ = evaluate(learner, a.eval_mazes, a.dim, eval_algo, seed=0x7E580000, eps=0.0,
+                         device=dev, mazes=mz6)
+        e6, _ = evaluate(learner, a.eval_mazes, a.dim, eval_algo, seed=0x7E580000,
+                         eps=a.eps_final, device=dev, mazes=mz6)
         res = {
             "variant": a.variant, "envs_per_gpu": B, "n_gpus": world, "dim": a.dim, "algo": a.algo,
             "vector_steps": a.steps, "train_seconds": secs,
@@ -88,6 +94,7 @@ def main(argv=None):
             "updates": learner.n_updates, "updates_per_s": learner.n_updates / secs,
             "batch": a.batch, "train_wins": int(stats[0]), "train_episodes": int(stats[1]),
             "win_rate_greedy": greedy, "win_rate_eps": epsr, "eval_eps": a.eps_final,
+            "win_rate_greedy_best_of_6": g6, "win_rate_eps_best_of_6": e6,
             "eval_mazes": a.eval_mazes, "eval_steps": [kg, ke],
         }
         print(json.dumps(res), flush=True)
