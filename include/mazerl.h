@@ -303,6 +303,13 @@ int mz_replay_gather(const int64_t* idx_dev, int32_t b, int64_t capacity,
 int mz_pair_surrogate(const float* lp_new_dev, const float* lp_old_dev, const float* adv_dev,
                       int32_t b, float clip, float* part_dev, float* dsum_dev, void* stream);
 
+/* The DQN/DDQN optimizer step (dqn_agent.py:152-157, ddqn_agent.py:148-152: grad.clamp_(-c, c)
+ * per parameter, then torch.optim.AdamW) as one launch over a flat f32 parameter buffer whose
+ * segment k (length seg_len[k], a multiple of 4) has its gradient at grads_dev[k] (host array of
+ * nseg <= 16 device pointers). lr_dev: device f32 learning rate. step_dev: device f32 [2] —
+ * [0] the step count (advanced by one by the launch itself, so a captured graph advances it per
+ * replay), [1] a workgroup ticket the launch uses (zero it once at allocation). write_grad: store
+ * the clamped, grad_scale-scaled gradient back (clamp_ in place). */
 int mz_adamw_flat(float* param_dev, float* exp_avg_dev, float* exp_avg_sq_dev,
                   const float* const* grads_dev, const int64_t* seg_len, int32_t nseg,
                   const float* lr_dev, float* step_dev, double beta1, double beta2, double eps,

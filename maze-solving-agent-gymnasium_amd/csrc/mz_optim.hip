@@ -18,9 +18,9 @@
 //   m = lerp(m, g, 1 - b1)                               (m + w * (g - m), w < 0.5)
 //   v = v * b2 + (1 - b2) * g * g
 //   p = p - (lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)
-// with t the step count after this step (incremented on the device by the launcher's first
-// kernel, so a captured HIP graph advances it on every replay) and lr read from the device (the
-// cosine schedule writes it between replays).
+// with t the step count after this step (read as step[0] + 1 by every workgroup; the last
+// workgroup to finish stores it back, so a captured HIP graph advances it on every replay without
+// a second launch) and lr read from the device (the cosine schedule writes it between replays).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -35,17 +35,30 @@ struct Segs {
   int n;
 };
 
-__global__ void k_step_inc(float* step) { *step += 1.0f; }
+// step[0] = the count, step[1] = a workgroup ticket (0 between launches): the last workgroup to
+// take a ticket has seen every other workgroup read step[0] already, and stores the new count.
+__device__ inline void publish_step(float* step, float t) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    unsigned* ticket = reinterpret_cast<unsigned*>(step + 1);
+    if (atomicAdd(ticket, 1u) == gridDim.x - 1) {
+      step[0] = t;
+      *ticket = 0u;
+    }
+  }
+}
 
 __global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, float* __restrict__ m,
                                                float* __restrict__ v, Segs segs,
                                                const float* __restrict__ lr_dev,
-                                               const float* __restrict__ step_dev, double b1,
+                                               float* step_dev, double b1,
                                                double b2, double eps_d, double wd, float clamp,
                                                float gscale, int write_grad) {
   // the per-step scalars as torch's eager AdamW forms them (Python doubles, then f32 operands)
   const double lr = (double)*lr_dev;
-  const double t = (double)*step_dev;
+  const float t_next = step_dev[0] + 1.0f;
+  const double t = (double)t_next;
   const double bc1 = 1.0 - pow(b1, t);
   const float step_size = (float)(lr / bc1);
   const float bc2_sqrt = (float)sqrt(1.0 - pow(b2, t));
@@ -85,6 +98,7 @@ __global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, float* __r
     reinterpret_cast<float4*>(v)[q] = v4;
     if (write_grad) *gp = g4;  // the clamped gradient stays visible, as with clamp_ in place
   }
+  publish_step(step_dev, t_next);
 }
 
 // ---- PPO's optimizer step (ppo_agent.py:232-236): clip_grad_norm_(params, 0.5), then AdamW
@@ -224,7 +238,6 @@ hipError_t mz_launch_adamw(float* p, float* m, float* v, const float* const* gra
     sg.g[k] = grads[k];
     sg.off[k + 1] = sg.off[k] + seg_len[k];
   }
-  hipLaunchKernelGGL(k_step_inc, dim3(1), dim3(1), 0, s, step);
   const int64_t n4 = sg.off[nseg] >> 2;
   int blocks = (int)((n4 + 255) / 256);
   if (blocks > 2048) blocks = 2048;  // 8 workgroups per CU, grid-stride beyond

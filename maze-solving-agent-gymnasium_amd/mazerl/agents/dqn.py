@@ -136,9 +136,17 @@ def q_loss(source, target, state, action, reward, next_state, gamma, double):
     return F.mse_loss(q_sa, expected.unsqueeze(1))
 
 
+_ONES = {}
+
+
 def learner_backward(optimizer, loss):
     optimizer.zero_grad()
-    loss.backward()
+    # a persistent dL/dL = 1 (loss.backward() fills a fresh one: one more launch per update)
+    key = (loss.device, loss.dtype)
+    one = _ONES.get(key)
+    if one is None:
+        one = _ONES[key] = torch.ones((), dtype=loss.dtype, device=loss.device)
+    loss.backward(gradient=one)
 
 
 def learner_step(net, optimizer, clamp=1.0):

@@ -76,7 +76,8 @@ class FlatAdamW(torch.optim.Optimizer):
         self.sizes = list(net._flat_sizes)
         self.exp_avg = torch.zeros_like(flat)
         self.exp_avg_sq = torch.zeros_like(flat)
-        self.step_t = torch.zeros((), dtype=torch.float32, device=dev)
+        self._step_buf = torch.zeros(2, dtype=torch.float32, device=dev)  # count, launch ticket
+        self.step_t = self._step_buf[0]
         self.clamp = float(clamp)
         self.grad_scale = 1.0
         self.lib = N.load()
@@ -103,7 +104,7 @@ class FlatAdamW(torch.optim.Optimizer):
         st = torch.cuda.current_stream(self.flat.device).cuda_stream
         N.check(self.lib.mz_adamw_flat(self.flat.data_ptr(), self.exp_avg.data_ptr(),
                                        self.exp_avg_sq.data_ptr(), arr, self._seg_len, len(ptrs),
-                                       g["lr"].data_ptr(), self.step_t.data_ptr(), float(b1),
+                                       g["lr"].data_ptr(), self._step_buf.data_ptr(), float(b1),
                                        float(b2), float(g["eps"]), float(g["weight_decay"]),
                                        self.clamp, float(self.grad_scale), 1, st))
 
