@@ -274,6 +274,17 @@ def main():
         if p.get("envs") == B and p.get("dim") == a.dim:
             traffic = p.get("hbm_bytes_per_launch")
 
+    # steady-state regeneration of all B mazes per algorithm (after the timed region; the module
+    # is loaded): one mz_generate launch each, HIP events on the launch stream
+    steady = {}
+    for algo in ("dfs", "prim&kill", "r-prim"):  # r-prim last: cpu_baseline reads maze 0
+        g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        g0.record(stream)
+        env.generate(algorithm=algo, seed=0x6E4E0000 + rank * B)
+        g1.record(stream)
+        g1.synchronize()
+        steady[algo] = B / (g0.elapsed_time(g1) * 1e-3)
+
     if rank == 0:
         out = {
             "metric": "env steps/sec (whole node) + DQN win-rate, 40x40 r-prim mazes",
@@ -297,7 +308,10 @@ def main():
                          "timing": "HIP events around the timed region on the launch stream",
                          "alg_bytes_per_instance_step": ALG_BYTES_PER_STEP},
             "generation": {"mazes": B, "seconds": round(gen_s, 3), "mazes_per_s": B / gen_s,
-                           "note": "first build incl. module load; excluded from value"},
+                           "note": "first build incl. module load; excluded from value",
+                           "steady_mazes_per_s": steady,
+                           "steady_note": f"per GPU: all {B} {a.dim}x{a.dim} mazes regenerated in one "
+                                          "launch per algorithm (generation + BFS tables + goal)"},
             "win_rate": None,
         }
         if world == 1 and not a.no_cpu_baseline:
