@@ -3,7 +3,8 @@
 //
 //   generation  random_prim_visit / deept_first_visit / prim_and_kill_visit
 //               (maze_generation.py:59-185) over a Philox stream; lane 0 runs the sequential
-//               carve loop, the prim&kill restart scan (:151) is wave-parallel.
+//               carve loop, the prim&kill restart pick (:151) is a wave scan over a
+//               candidate bit per cell that the walk keeps current.
 //   goal        find_random_position (:187-218): wave BFS from start + wave max-reduce
 //   toroidal    gen_maze_no_border (:37-56): generate (N+2)^2, pick goal, crop the border
 //   tables      BFS distance-to-goal field (replaces per-step A*, a_star.py:9-82), best-next
@@ -163,6 +164,31 @@ __device__ inline int mz_pk_nbrs(const uint16_t* mk, int G, int p, int* out) {
   return cnt;
 }
 
+// The restart candidates of prim_and_kill_visit — marked cells with >= 1 unmarked neighbour
+// (maze_generation.py:151) — as one bit per cell in L.vis, cell q = (r / 2) * W + c / 2 with
+// W = (G - 1) / 2: row-major, the order of the reference's list comprehension. The walk keeps
+// the bits current as it marks cells (only the new cell and its marked neighbours can change),
+// so a restart picks its candidate from a 125-word bit scan instead of two passes over the grid.
+__device__ inline void mz_pk_cand(uint32_t* cb, int G, int p, bool on) {
+  const int r = p / G, c = p - r * G, q = (r >> 1) * ((G - 1) >> 1) + (c >> 1);
+  if (on) cb[q >> 5] |= 1u << (q & 31);
+  else cb[q >> 5] &= ~(1u << (q & 31));
+}
+
+// mark p (lane 0) and refresh the candidate bits that marking it can change
+__device__ inline void mz_pk_mark(const MzBuildLds& L, int G, int p) {
+  int tmp[4];
+  L.dist[p] = 2;
+  mz_pk_cand(L.vis, G, p, mz_pk_nbrs(L.dist, G, p, tmp) > 0);
+  const int x = p / G, y = p - x * G;
+  for (int k = 0; k < 4; ++k) {
+    const int r = x + mz_g2r(k), c = y + mz_g2c(k);
+    if (r < 0 || r >= G || c < 0 || c >= G) continue;
+    const int n = r * G + c;
+    if (L.dist[n] == 2 && mz_pk_nbrs(L.dist, G, n, tmp) == 0) mz_pk_cand(L.vis, G, n, false);
+  }
+}
+
 __device__ void mz_pk_walk(const MzBuildLds& L, int G, int cur, MzRng& rng) {
   int nb[4], cnt;
   while ((cnt = mz_pk_nbrs(L.dist, G, cur, nb)) != 0) {
@@ -170,52 +196,62 @@ __device__ void mz_pk_walk(const MzBuildLds& L, int G, int cur, MzRng& rng) {
     const int cx = cur / G, cy = cur - cx * G, x = nx / G, y = nx - x * G;
     L.g[(cx + (x - cx) / 2) * G + (cy + (y - cy) / 2)] = 1;
     cur = nx;
-    L.dist[cur] = 2;
+    mz_pk_mark(L, G, cur);
     L.sh[1] -= 1;
   }
 }
 
 // wave-cooperative; rng lives in lane 0
 __device__ void mz_gen_primkill(const MzBuildLds& L, int G, int s, MzRng& rng) {
-  const int lane = threadIdx.x, C = G * G;
+  const int lane = threadIdx.x, C = G * G, W = (G - 1) / 2, nw = (W * W + 31) / 32;
   for (int p = lane; p < C; p += 64) {
     const int r = p / G, c = p - r * G;
     const bool cell = (r & 1) && (c & 1) && r < G && c < G;
     L.dist[p] = cell ? 1 : 0;
     if (cell) L.g[p] = 1;
   }
+  for (int w = lane; w < nw; w += 64) L.vis[w] = 0u;
   __syncthreads();
   if (lane == 0) {
-    int cells = ((G - 1) / 2) * ((G - 1) / 2);
-    L.dist[s] = 2;
-    L.sh[1] = cells - 1;  // unmarked count
+    L.sh[1] = W * W - 1;  // unmarked count
+    mz_pk_mark(L, G, s);
     mz_pk_walk(L, G, s, rng);
   }
   __syncthreads();
   while (L.sh[1] > 0) {
-    // marked cells with >= 1 unmarked neighbour, row-major (maze_generation.py:151)
     int total = 0;
-    for (int b = 0; b < C; b += 64) {
-      const int p = b + lane;
-      int tmp[4];
-      const bool cand = p < C && L.dist[p] == 2 && mz_pk_nbrs(L.dist, G, p, tmp) > 0;
-      total += __popcll(__ballot(cand));
+    for (int b = 0; b < nw; b += 64) {
+      int pc = b + lane < nw ? __popc(L.vis[b + lane]) : 0;
+      for (int o = 32; o > 0; o >>= 1) pc += __shfl_xor(pc, o);
+      total += pc;
     }
     int k = 0;
     if (lane == 0) k = (int)rng.below((uint32_t)total);
     k = __shfl(k, 0);
     int chosen = -1;
-    for (int b = 0; b < C && chosen < 0; b += 64) {
-      const int p = b + lane;
-      int tmp[4];
-      const bool cand = p < C && L.dist[p] == 2 && mz_pk_nbrs(L.dist, G, p, tmp) > 0;
-      unsigned long long bal = __ballot(cand);
-      const int pc = __popcll(bal);
-      if (k < pc) {
-        for (int t = 0; t < k; ++t) bal &= bal - 1;  // drop the k lowest set bits
-        chosen = b + __ffsll((long long)bal) - 1;
+    for (int b = 0; b < nw && chosen < 0; b += 64) {
+      const int w = b + lane;
+      const uint32_t v = w < nw ? L.vis[w] : 0u;
+      const int pc = __popc(v);
+      int inc = pc;  // inclusive prefix sum over the lanes' words
+      for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(inc, o);
+        if (lane >= o) inc += t;
+      }
+      const int tot = __shfl(inc, 63);
+      if (k < tot) {
+        const unsigned long long bal = __ballot(inc > k && inc - pc <= k);
+        const int src = __ffsll((long long)bal) - 1;
+        int q = 0;
+        if (lane == src) {
+          uint32_t m = v;
+          for (int t = inc - pc; t < k; ++t) m &= m - 1;  // drop the lower candidates
+          q = w * 32 + __ffs(m) - 1;
+        }
+        q = __shfl(q, src);
+        chosen = (2 * (q / W) + 1) * G + 2 * (q % W) + 1;
       } else {
-        k -= pc;
+        k -= tot;
       }
     }
     __syncthreads();

@@ -104,6 +104,25 @@ def test_generation_matches_oracle(mazerl, tor, dims):
         env.close()
 
 
+@pytest.mark.parametrize("tor,dims", [(False, (81, 127)), (True, (79, 125))])
+def test_primkill_restart_pick_matches_oracle(mazerl, tor, dims):
+    """prim&kill's restart pick (maze_generation.py:151: the k-th marked cell with an unmarked
+    neighbour, row-major) from the candidate bits the walk keeps current == the oracle's full
+    rescan, over many seeds and up to the largest pitch (127)."""
+    import pyoracle as O
+    B, algo = 128, 2
+    for dim in dims:
+        env = mazerl.VectorMazeEnv(B, dim, toroidal=tor, enrich=False, generate=False)
+        env.generate(algorithm="prim&kill", dim=dim, seed=0x9C0000 + dim)
+        torch.cuda.synchronize()
+        for i in range(B):
+            (sr, sc), (gr, gc), g = O.generate(dim, algo, 0x9C0000 + dim + i, tor)
+            q = env.query(i)
+            np.testing.assert_array_equal(env.grid(i), g, err_msg=f"dim {dim} env {i}")
+            assert (q["start_r"], q["start_c"], q["goal_r"], q["goal_c"]) == (sr, sc, gr, gc)
+        env.close()
+
+
 def test_full_size_vs_oracle_sample(mazerl):
     """65,536 x 81x81 r-prim (the headline config): step with the fused exploration kernel; a
     sample of instances is replayed through the oracle with the same actions; size-independent
