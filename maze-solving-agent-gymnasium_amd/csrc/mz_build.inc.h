@@ -325,6 +325,8 @@ __device__ inline MzPyLds mz_py_lds(uint8_t* base, const MzBuildLds& L, int G) {
   Y.cap_b = mz_py_cap_b(G);
   Y.ta = reinterpret_cast<uint16_t*>(base + 2560);
   Y.tb = Y.ta + Y.cap_a;
+  Y.sbits = reinterpret_cast<uint32_t*>(L.queue);
+  Y.slot_of = reinterpret_cast<uint16_t*>(Y.sbits + Y.cap_b / 32);
   Y.scratch = L.dist;  // dist + queue (contiguous, 4 G^2 bytes): free while generating
   Y.G = G;
   return Y;

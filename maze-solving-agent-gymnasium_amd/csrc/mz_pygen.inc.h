@@ -48,6 +48,11 @@ struct MzPyLds {
   uint16_t* ta;   // [cap_a]
   uint16_t* tb;   // [cap_b]
   uint16_t* scratch;  // resize copy (the build's dist + queue region, free during generation)
+  // prim&kill only, in the build's queue region (2 G^2 bytes, free while generating): its two
+  // sets only grow by adds (unmarked is built, then only discarded from), so a resize copies
+  // < 0.42 G^2 u16 slots and stays inside dist; these take cap_b / 8 + 2 cells < 0.7 G^2 bytes
+  uint32_t* sbits;    // [cap_b / 32] slot i of the marked table is a restart candidate
+  uint16_t* slot_of;  // [cells] the marked-table slot of cell (r / 2) * W + c / 2
   int cap_a, cap_b, G;
 };
 
@@ -155,29 +160,32 @@ __device__ inline void mz_ps_resize(const MzPySet& s, int minused, uint16_t* scr
   s.h[1] = s.h[2];
 }
 
-__device__ inline void mz_ps_found_unused(const MzPySet& s, uint32_t i, int key, uint16_t* scratch) {
+// returns the key's slot, or -2 when the insertion resized the table
+__device__ inline int mz_ps_found_unused(const MzPySet& s, uint32_t i, int key, uint16_t* scratch) {
   s.h[1] += 1;
   s.h[2] += 1;
   s.t[i] = (uint16_t)key;
-  if ((long)s.h[1] * 5 < (long)s.h[0] * 3) return;
+  if ((long)s.h[1] * 5 < (long)s.h[0] * 3) return (int)i;
   mz_ps_resize(s, s.h[2] > 50000 ? s.h[2] * 2 : s.h[2] * 4, scratch);
+  return -2;
 }
 
-__device__ inline void mz_ps_add(const MzPySet& s, int key, uint16_t* scratch) {
+// set.add; returns the key's slot, or -2 when the insertion resized the table
+__device__ inline int mz_ps_add(const MzPySet& s, int key, uint16_t* scratch) {
   const uint64_t h = mz_ps_hash(s, key);
   const uint32_t mask = (uint32_t)s.h[0];
   uint32_t i = (uint32_t)(h & mask);
-  if (s.t[i] == MZ_PS_EMPTY) { mz_ps_found_unused(s, i, key, scratch); return; }
+  if (s.t[i] == MZ_PS_EMPTY) return mz_ps_found_unused(s, i, key, scratch);
   int freeslot = -1;
   uint64_t perturb = h;
   for (;;) {
-    if (s.t[i] == key) return;
+    if (s.t[i] == key) return (int)i;
     if (s.t[i] == MZ_PS_DUMMY) freeslot = (int)i;
     if (i + 9 <= mask) {
       for (uint32_t j = 1; j <= 9; ++j) {
         const uint16_t t = s.t[i + j];
         if (t == MZ_PS_EMPTY) { i += j; goto unused_or_dummy; }
-        if (t == key) return;
+        if (t == key) return (int)(i + j);
         if (t == MZ_PS_DUMMY) freeslot = (int)(i + j);
       }
     }
@@ -186,9 +194,10 @@ __device__ inline void mz_ps_add(const MzPySet& s, int key, uint16_t* scratch) {
     if (s.t[i] == MZ_PS_EMPTY) goto unused_or_dummy;
   }
 unused_or_dummy:
-  if (freeslot < 0) { mz_ps_found_unused(s, i, key, scratch); return; }
+  if (freeslot < 0) return mz_ps_found_unused(s, i, key, scratch);
   s.h[2] += 1;
   s.t[freeslot] = (uint16_t)key;
+  return freeslot;
 }
 
 __device__ inline int mz_ps_lookup(const MzPySet& s, int key) {
@@ -347,6 +356,46 @@ __device__ inline void mz_py_inters(const MzBuildLds& L, const MzPySet& un, int 
   }
 }
 
+// prim&kill's restart candidates ([p for p in marked if set(nbrs(p)) & unmarked], :151) in the
+// order of the marked table: Y.sbits holds a bit per slot, Y.slot_of each marked cell's slot.
+// The walk keeps them current as it marks cells — only the new cell and its marked neighbours
+// can change — so a restart picks the k-th candidate from a scan over cap_b / 32 words instead
+// of two passes over the table with four neighbour tests per slot. A resize of the marked table
+// moves every slot: hdr[7] then marks the bits stale and the next restart rebuilds them with
+// the whole wave.
+__device__ inline int mz_py_cell(int G, int p) {
+  const int r = p / G, c = p - r * G;
+  return (r >> 1) * ((G - 1) >> 1) + (c >> 1);
+}
+__device__ inline bool mz_py_has_unmarked(const MzBuildLds& L, int G, int p) {
+  int nb[4];
+  const int n = mz_py_nbrs2(G, p, nb);
+  bool any = false;
+  for (int q = 0; q < n; ++q) any |= mz_py_unmarked(L, nb[q]);
+  return any;
+}
+__device__ inline void mz_py_sbit(uint32_t* sb, int i, bool on) {
+  if (on) sb[i >> 5] |= 1u << (i & 31);
+  else sb[i >> 5] &= ~(1u << (i & 31));
+}
+
+// cur has just moved from unmarked to marked at slot `slot` of the marked table (lane 0)
+__device__ inline void mz_py_pk_marked(const MzBuildLds& L, const MzPyLds& Y, int G, int cur,
+                                       int slot) {
+  if (slot < 0) Y.hdr[7] = 1;  // the add resized the table
+  if (Y.hdr[7]) return;
+  Y.slot_of[mz_py_cell(G, cur)] = (uint16_t)slot;
+  mz_py_sbit(Y.sbits, slot, mz_py_has_unmarked(L, G, cur));
+  int nb[4];
+  const int n = mz_py_nbrs2(G, cur, nb);
+  for (int q = 0; q < n; ++q) {
+    if (mz_py_unmarked(L, nb[q])) continue;  // every other cell 2 away is marked
+    const int sl = Y.slot_of[mz_py_cell(G, nb[q])];
+    if (((Y.sbits[sl >> 5] >> (sl & 31)) & 1u) && !mz_py_has_unmarked(L, G, nb[q]))
+      mz_py_sbit(Y.sbits, sl, false);
+  }
+}
+
 // random_walk (:159-185), lane 0
 __device__ void mz_py_walk(const MzBuildLds& L, const MzPyLds& Y, int G, int cur) {
   const MzPySet un{Y.ta, Y.hdr, Y.cap_a, G, Y.hdr + 6};
@@ -364,7 +413,7 @@ __device__ void mz_py_walk(const MzBuildLds& L, const MzPyLds& Y, int G, int cur
     cur = nx;
     mz_ps_discard(un, cur);
     L.vis[cur >> 5] &= ~(1u << (cur & 31));
-    mz_ps_add(mk, cur, Y.scratch);
+    mz_py_pk_marked(L, Y, G, cur, mz_ps_add(mk, cur, Y.scratch));
     mz_py_inters(L, un, G, cur, it, ih);
   }
 }
@@ -393,42 +442,59 @@ __device__ void mz_py_primkill(const MzBuildLds& L, const MzPyLds& Y, int G, int
     mz_ps_discard(un, s);
     L.vis[s >> 5] &= ~(1u << (s & 31));
     L.g[s] = 1;
+    Y.hdr[7] = 1;  // candidate bits built at the first restart
     mz_py_walk(L, Y, G, s);
   }
   __syncthreads();
   while (un.h[2] > 0 && !Y.hdr[6]) {
-    // [p for p in marked if set(nbrs(p)) & unmarked] in marked's table order, then choice
-    const int n = mk.h[0] + 1;
-    int total = 0;
-    for (int b = 0; b < n; b += 64) {
-      const int i = b + lane;
-      bool cand = false;
-      if (i < n && mk.t[i] < MZ_PS_DUMMY) {
-        int nb[4];
-        const int c = mz_py_nbrs2(G, mk.t[i], nb);
-        for (int q = 0; q < c; ++q) cand |= mz_py_unmarked(L, nb[q]);
+    const int n = mk.h[0] + 1, nw = (n + 31) >> 5;
+    if (Y.hdr[7]) {  // rebuild the slot bits and slot_of over the whole (resized) table
+      for (int b = 0; b < n; b += 64) {
+        const int i = b + lane;
+        bool cand = false;
+        if (i < n && mk.t[i] < MZ_PS_DUMMY) {
+          Y.slot_of[mz_py_cell(G, mk.t[i])] = (uint16_t)i;
+          cand = mz_py_has_unmarked(L, G, mk.t[i]);
+        }
+        const unsigned long long bal = __ballot(cand);
+        if (lane == 0) Y.sbits[b >> 5] = (uint32_t)bal;
+        if (lane == 1 && b + 32 < n) Y.sbits[(b >> 5) + 1] = (uint32_t)(bal >> 32);
       }
-      total += __popcll(__ballot(cand));
+      __syncthreads();
+      if (lane == 0) Y.hdr[7] = 0;
+    }
+    int total = 0;
+    for (int b = 0; b < nw; b += 64) {
+      int pc = b + lane < nw ? __popc(Y.sbits[b + lane]) : 0;
+      for (int o = 32; o > 0; o >>= 1) pc += __shfl_xor(pc, o);
+      total += pc;
     }
     int k = 0;
     if (lane == 0) k = (int)mz_mt_below(Y.mt, (uint32_t)total);
     k = __shfl(k, 0);
     int chosen = -1;
-    for (int b = 0; b < n && chosen < 0; b += 64) {
-      const int i = b + lane;
-      bool cand = false;
-      if (i < n && mk.t[i] < MZ_PS_DUMMY) {
-        int nb[4];
-        const int c = mz_py_nbrs2(G, mk.t[i], nb);
-        for (int q = 0; q < c; ++q) cand |= mz_py_unmarked(L, nb[q]);
+    for (int b = 0; b < nw && chosen < 0; b += 64) {
+      const int w = b + lane;
+      const uint32_t v = w < nw ? Y.sbits[w] : 0u;
+      const int pc = __popc(v);
+      int inc = pc;  // inclusive prefix sum over the lanes' words
+      for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(inc, o);
+        if (lane >= o) inc += t;
       }
-      unsigned long long bal = __ballot(cand);
-      const int pc = __popcll(bal);
-      if (k < pc) {
-        for (int t = 0; t < k; ++t) bal &= bal - 1;
-        chosen = mk.t[b + __ffsll((long long)bal) - 1];
+      const int tot = __shfl(inc, 63);
+      if (k < tot) {
+        const unsigned long long bal = __ballot(inc > k && inc - pc <= k);
+        const int src = __ffsll((long long)bal) - 1;
+        int slot = 0;
+        if (lane == src) {
+          uint32_t m = v;
+          for (int t = inc - pc; t < k; ++t) m &= m - 1;  // drop the lower candidates
+          slot = w * 32 + __ffs(m) - 1;
+        }
+        chosen = mk.t[__shfl(slot, src)];
       } else {
-        k -= pc;
+        k -= tot;
       }
     }
     __syncthreads();
