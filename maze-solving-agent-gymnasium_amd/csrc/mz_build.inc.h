@@ -82,6 +82,13 @@ __device__ void mz_wave_bfs(const MzBuildLds& L, int G, bool tor, int src) {
 }
 
 // --- generators (lane 0 unless noted); G = generation grid size (odd) ------------------------
+// Up to 4 small values (cell keys < 2^16, directions) packed in one u64: the lists stay in
+// registers — an int[4] indexed by a random draw lives in per-lane scratch memory.
+__device__ inline int mz_k4(uint64_t v, int i) { return (int)((v >> (16 * i)) & 0xFFFFu); }
+__device__ inline void mz_k4_push(uint64_t& v, int& n, int x) {
+  v |= (uint64_t)(uint32_t)x << (16 * n);
+  ++n;
+}
 // neighbour order of get_neighbors / random_walk: (-2,0),(2,0),(0,-2),(0,2) (maze_generation.py:72)
 __device__ inline int mz_g2r(int k) { return k == 0 ? -2 : (k == 1 ? 2 : 0); }
 __device__ inline int mz_g2c(int k) { return k == 2 ? -2 : (k == 3 ? 2 : 0); }
@@ -108,14 +115,15 @@ __device__ void mz_gen_rprim(const MzBuildLds& L, int G, int s, MzRng& rng) {
     const int f = fr[i];
     fr[i] = fr[--nf];
     const int fx = f / G, fy = f - fx * G;
-    int nb[4], cnt = 0;
+    uint64_t nb = 0;
+    int cnt = 0;
     for (int k = 0; k < 4; ++k) {
       int r = fx + mz_g2r(k), c = fy + mz_g2c(k);
       if (r < 0 || r >= G || c < 0 || c >= G) continue;
-      if (m[r * G + c] == 1) nb[cnt++] = r * G + c;
+      if (m[r * G + c] == 1) mz_k4_push(nb, cnt, r * G + c);
     }
     if (cnt) {
-      const int nn = nb[rng.below((uint32_t)cnt)];
+      const int nn = mz_k4(nb, (int)rng.below((uint32_t)cnt));
       const int nx = nn / G, ny = nn - nx * G;
       m[f] = 1;
       m[((fx + nx) / 2) * G + (fy + ny) / 2] = 1;
@@ -138,13 +146,14 @@ __device__ void mz_gen_dfs(const MzBuildLds& L, int G, int s, MzRng& rng) {
   st[sp++] = (uint16_t)s;
   while (sp > 0) {
     const int top = st[sp - 1], x = top / G, y = top - x * G;
-    int cand[4], cnt = 0;
+    uint64_t cand = 0;
+    int cnt = 0;
     for (int k = 0; k < 4; ++k) {
       int nx = x + 2 * mz_fr(k), ny = y + 2 * mz_fc(k);
-      if (nx >= 0 && nx < G && ny >= 0 && ny < G && m[nx * G + ny] == 0) cand[cnt++] = k;
+      if (nx >= 0 && nx < G && ny >= 0 && ny < G && m[nx * G + ny] == 0) mz_k4_push(cand, cnt, k);
     }
     if (!cnt) { --sp; continue; }
-    const int k = cand[rng.below((uint32_t)cnt)];
+    const int k = mz_k4(cand, (int)rng.below((uint32_t)cnt));
     m[(x + mz_fr(k)) * G + (y + mz_fc(k))] = 1;
     const int nx = x + 2 * mz_fr(k), ny = y + 2 * mz_fc(k);
     m[nx * G + ny] = 1;
@@ -153,13 +162,14 @@ __device__ void mz_gen_dfs(const MzBuildLds& L, int G, int s, MzRng& rng) {
 }
 
 // prim&kill marks kept in L.dist: 0 = not a cell, 1 = unmarked, 2 = marked
-__device__ inline int mz_pk_nbrs(const uint16_t* mk, int G, int p, int* out) {
+__device__ inline int mz_pk_nbrs(const uint16_t* mk, int G, int p, uint64_t& out) {
   const int x = p / G, y = p - x * G;
   int cnt = 0;
+  out = 0;
   for (int k = 0; k < 4; ++k) {
     int r = x + mz_g2r(k), c = y + mz_g2c(k);
     if (r < 0 || r >= G || c < 0 || c >= G) continue;
-    if (mk[r * G + c] == 1) out[cnt++] = r * G + c;
+    if (mk[r * G + c] == 1) mz_k4_push(out, cnt, r * G + c);
   }
   return cnt;
 }
@@ -177,7 +187,7 @@ __device__ inline void mz_pk_cand(uint32_t* cb, int G, int p, bool on) {
 
 // mark p (lane 0) and refresh the candidate bits that marking it can change
 __device__ inline void mz_pk_mark(const MzBuildLds& L, int G, int p) {
-  int tmp[4];
+  uint64_t tmp;
   L.dist[p] = 2;
   mz_pk_cand(L.vis, G, p, mz_pk_nbrs(L.dist, G, p, tmp) > 0);
   const int x = p / G, y = p - x * G;
@@ -190,9 +200,10 @@ __device__ inline void mz_pk_mark(const MzBuildLds& L, int G, int p) {
 }
 
 __device__ void mz_pk_walk(const MzBuildLds& L, int G, int cur, MzRng& rng) {
-  int nb[4], cnt;
+  uint64_t nb;
+  int cnt;
   while ((cnt = mz_pk_nbrs(L.dist, G, cur, nb)) != 0) {
-    const int nx = nb[rng.below((uint32_t)cnt)];
+    const int nx = mz_k4(nb, (int)rng.below((uint32_t)cnt));
     const int cx = cur / G, cy = cur - cx * G, x = nx / G, y = nx - x * G;
     L.g[(cx + (x - cx) / 2) * G + (cy + (y - cy) / 2)] = 1;
     cur = nx;
@@ -323,7 +334,8 @@ __device__ inline MzPyLds mz_py_lds(uint8_t* base, const MzBuildLds& L, int G) {
   Y.hdr = reinterpret_cast<int*>(base + 2512);
   Y.cap_a = mz_py_cap_a(G);
   Y.cap_b = mz_py_cap_b(G);
-  Y.ta = reinterpret_cast<uint16_t*>(base + 2560);
+  Y.small = reinterpret_cast<uint16_t*>(base + 2560);
+  Y.ta = reinterpret_cast<uint16_t*>(base + 2592);
   Y.tb = Y.ta + Y.cap_a;
   Y.sbits = reinterpret_cast<uint32_t*>(L.queue);
   Y.slot_of = reinterpret_cast<uint16_t*>(Y.sbits + Y.cap_b / 32);

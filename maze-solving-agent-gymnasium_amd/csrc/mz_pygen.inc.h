@@ -39,12 +39,14 @@ __host__ __device__ inline int mz_py_cap_a(int G) {
 }
 __host__ __device__ inline int mz_py_cap_b(int G) { return mz_py_cap_grow(mz_py_cells(G)); }
 __host__ __device__ inline size_t mz_py_lds_bytes(int G) {
-  return 2560 + 2 * (size_t)mz_py_cap_a(G) + 2 * (size_t)mz_py_cap_b(G);
+  return 2592 + 2 * (size_t)mz_py_cap_a(G) + 2 * (size_t)mz_py_cap_b(G);
 }
 
 struct MzPyLds {
   uint32_t* mt;   // [625] MT19937 words + index
   int* hdr;       // per set: mask, fill, used (A: 0..2, B: 3..5); [6] error flag
+  uint16_t* small;  // [16] lane 0's two 8-slot tables (set(nbrs), the intersection): LDS, not
+                    // per-lane scratch memory, which data-dependent slot indices would need
   uint16_t* ta;   // [cap_a]
   uint16_t* tb;   // [cap_b]
   uint16_t* scratch;  // resize copy (the build's dist + queue region, free during generation)
@@ -245,20 +247,22 @@ __device__ inline int mz_ps_kth_wave(const MzPySet& s, int k) {
 }
 
 // small set (<= 4 keys, stays in its 8 slots) built from keys in order: set(list)
-__device__ inline void mz_ps_small(uint16_t t[8], int G, const int* keys, int n) {
+__device__ inline void mz_ps_small(uint16_t* t, int G, uint64_t keys, int n) {
   int h[3];
   MzPySet s{t, h, 8, G, nullptr};
   mz_ps_init(s);
-  for (int i = 0; i < n; ++i) mz_ps_add(s, keys[i], nullptr);
+  for (int i = 0; i < n; ++i) mz_ps_add(s, mz_k4(keys, i), nullptr);
 }
 
 // ---- the visits ----------------------------------------------------------------------------
-__device__ inline int mz_py_nbrs2(int G, int p, int* out) {  // get_neighbors order (:72)
+// get_neighbors order (:72), packed (mz_k4)
+__device__ inline int mz_py_nbrs2(int G, int p, uint64_t& out) {
   const int x = p / G, y = p - (p / G) * G;
   int n = 0;
+  out = 0;
   for (int k = 0; k < 4; ++k) {
     const int a = x + mz_g2r(k), b = y + mz_g2c(k);
-    if (a >= 0 && a < G && b >= 0 && b < G) out[n++] = a * G + b;
+    if (a >= 0 && a < G && b >= 0 && b < G) mz_k4_push(out, n, a * G + b);
   }
   return n;
 }
@@ -268,11 +272,11 @@ __device__ void mz_py_rprim(const MzBuildLds& L, const MzPyLds& Y, int G, int s)
   const int lane = threadIdx.x;
   const MzPySet fr{Y.ta, Y.hdr, Y.cap_a, G, Y.hdr + 6};
   if (lane == 0) {
-    int nb[4];
+    uint64_t nb;
     const int n = mz_py_nbrs2(G, s, nb);
     L.g[s] = 1;
     mz_ps_init(fr);
-    for (int i = 0; i < n; ++i) mz_ps_add(fr, nb[i], Y.scratch);
+    for (int i = 0; i < n; ++i) mz_ps_add(fr, mz_k4(nb, i), Y.scratch);
   }
   __syncthreads();
   for (;;) {
@@ -285,17 +289,18 @@ __device__ void mz_py_rprim(const MzBuildLds& L, const MzPyLds& Y, int G, int s)
     __syncthreads();
     if (lane == 0) {
       mz_ps_discard(fr, f);
-      int nb[4], in[4], cnt = 0;
+      uint64_t nb, in = 0;
+      int cnt = 0;
       const int n = mz_py_nbrs2(G, f, nb);
       for (int i = 0; i < n; ++i)
-        if (L.g[nb[i]] == 1) in[cnt++] = nb[i];
+        if (L.g[mz_k4(nb, i)] == 1) mz_k4_push(in, cnt, mz_k4(nb, i));
       if (cnt) {
-        const int q = in[mz_mt_below(Y.mt, (uint32_t)cnt)];
+        const int q = mz_k4(in, (int)mz_mt_below(Y.mt, (uint32_t)cnt));
         const int fx = f / G, fy = f - fx * G, qx = q / G, qy = q - qx * G;
         L.g[f] = 1;
         L.g[((fx + qx) / 2) * G + (fy + qy) / 2] = 1;
         for (int i = 0; i < n; ++i)
-          if (L.g[nb[i]] == 0) mz_ps_add(fr, nb[i], Y.scratch);
+          if (L.g[mz_k4(nb, i)] == 0) mz_ps_add(fr, mz_k4(nb, i), Y.scratch);
       }
     }
     __syncthreads();
@@ -310,16 +315,18 @@ __device__ void mz_py_dfs(const MzBuildLds& L, const MzPyLds& Y, int G, int s) {
   st[sp++] = (uint16_t)s;
   while (sp > 0) {
     const int top = st[sp - 1], x = top / G, y = top - x * G;
-    int d[4] = {0, 1, 2, 3};
+    uint32_t d = 0xE4u;  // directions 0, 1, 2, 3 as 2-bit fields (registers)
     for (int i = 3; i >= 1; --i) {
       const int j = (int)mz_mt_below(Y.mt, (uint32_t)(i + 1));
-      const int t = d[i]; d[i] = d[j]; d[j] = t;
+      const uint32_t a = (d >> (2 * i)) & 3u, b = (d >> (2 * j)) & 3u;
+      d = (d & ~((3u << (2 * i)) | (3u << (2 * j)))) | (b << (2 * i)) | (a << (2 * j));
     }
     bool found = false;
     for (int k = 0; k < 4 && !found; ++k) {
-      const int nx = x + 2 * mz_fr(d[k]), ny = y + 2 * mz_fc(d[k]);
+      const int dk = (int)((d >> (2 * k)) & 3u);
+      const int nx = x + 2 * mz_fr(dk), ny = y + 2 * mz_fc(dk);
       if (nx >= 0 && nx < G && ny >= 0 && ny < G && m[nx * G + ny] == 0) {
-        m[(x + mz_fr(d[k])) * G + (y + mz_fc(d[k]))] = 1;
+        m[(x + mz_fr(dk)) * G + (y + mz_fc(dk))] = 1;
         m[nx * G + ny] = 1;
         st[sp++] = (uint16_t)(nx * G + ny);
         found = true;
@@ -336,10 +343,9 @@ __device__ inline bool mz_py_unmarked(const MzBuildLds& L, int p) {
 
 // inters = unmarked.intersection(set(nbrs(cur))) into the 8-slot table `it` (lane 0)
 __device__ inline void mz_py_inters(const MzBuildLds& L, const MzPySet& un, int G, int cur,
-                                    uint16_t it[8], int ih[3]) {
-  int nb[4];
+                                    uint16_t* st, uint16_t* it, int ih[3]) {
+  uint64_t nb;
   const int n = mz_py_nbrs2(G, cur, nb);
-  uint16_t st[8];
   mz_ps_small(st, G, nb, n);
   MzPySet res{it, ih, 8, G, nullptr};
   mz_ps_init(res);
@@ -368,10 +374,10 @@ __device__ inline int mz_py_cell(int G, int p) {
   return (r >> 1) * ((G - 1) >> 1) + (c >> 1);
 }
 __device__ inline bool mz_py_has_unmarked(const MzBuildLds& L, int G, int p) {
-  int nb[4];
+  uint64_t nb;
   const int n = mz_py_nbrs2(G, p, nb);
   bool any = false;
-  for (int q = 0; q < n; ++q) any |= mz_py_unmarked(L, nb[q]);
+  for (int q = 0; q < n; ++q) any |= mz_py_unmarked(L, mz_k4(nb, q));
   return any;
 }
 __device__ inline void mz_py_sbit(uint32_t* sb, int i, bool on) {
@@ -386,12 +392,13 @@ __device__ inline void mz_py_pk_marked(const MzBuildLds& L, const MzPyLds& Y, in
   if (Y.hdr[7]) return;
   Y.slot_of[mz_py_cell(G, cur)] = (uint16_t)slot;
   mz_py_sbit(Y.sbits, slot, mz_py_has_unmarked(L, G, cur));
-  int nb[4];
+  uint64_t nb;
   const int n = mz_py_nbrs2(G, cur, nb);
   for (int q = 0; q < n; ++q) {
-    if (mz_py_unmarked(L, nb[q])) continue;  // every other cell 2 away is marked
-    const int sl = Y.slot_of[mz_py_cell(G, nb[q])];
-    if (((Y.sbits[sl >> 5] >> (sl & 31)) & 1u) && !mz_py_has_unmarked(L, G, nb[q]))
+    const int p = mz_k4(nb, q);
+    if (mz_py_unmarked(L, p)) continue;  // every other cell 2 away is marked
+    const int sl = Y.slot_of[mz_py_cell(G, p)];
+    if (((Y.sbits[sl >> 5] >> (sl & 31)) & 1u) && !mz_py_has_unmarked(L, G, p))
       mz_py_sbit(Y.sbits, sl, false);
   }
 }
@@ -400,9 +407,9 @@ __device__ inline void mz_py_pk_marked(const MzBuildLds& L, const MzPyLds& Y, in
 __device__ void mz_py_walk(const MzBuildLds& L, const MzPyLds& Y, int G, int cur) {
   const MzPySet un{Y.ta, Y.hdr, Y.cap_a, G, Y.hdr + 6};
   const MzPySet mk{Y.tb, Y.hdr + 3, Y.cap_b, G, Y.hdr + 6};
-  uint16_t it[8];
+  uint16_t *st = Y.small, *it = Y.small + 8;
   int ih[3];
-  mz_py_inters(L, un, G, cur, it, ih);
+  mz_py_inters(L, un, G, cur, st, it, ih);
   while (ih[2] > 0 && !Y.hdr[6]) {
     L.g[cur] = 1;
     int k = (int)mz_mt_below(Y.mt, (uint32_t)ih[2]), nx = -1;
@@ -414,7 +421,7 @@ __device__ void mz_py_walk(const MzBuildLds& L, const MzPyLds& Y, int G, int cur
     mz_ps_discard(un, cur);
     L.vis[cur >> 5] &= ~(1u << (cur & 31));
     mz_py_pk_marked(L, Y, G, cur, mz_ps_add(mk, cur, Y.scratch));
-    mz_py_inters(L, un, G, cur, it, ih);
+    mz_py_inters(L, un, G, cur, st, it, ih);
   }
 }
 
