@@ -27,6 +27,18 @@
 
 #include "mz_kernels.h"
 
+// k_adamw's grid: every workgroup takes one same-address ticket (publish_step), and those atomics
+// serialise at ~30 ns each — 2,048 workgroups of 256 made the launch 78 us alone (106 us per
+// vector step inside training) for ~60 MB of traffic. 256 workgroups of 512 (grid-stride beyond):
+// 20.4 us alone, DDQN training 60.8 -> 63-64 M env steps/s (profiles/r02z_adamw/,
+// profiles/exp_adamw_ticket.sh).
+#ifndef MZ_ADAMW_MAXWG
+#define MZ_ADAMW_MAXWG 256
+#endif
+#ifndef MZ_ADAMW_TPB
+#define MZ_ADAMW_TPB 512
+#endif
+
 namespace {
 
 struct Segs {
@@ -49,7 +61,7 @@ __device__ inline void publish_step(float* step, float t) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, float* __restrict__ m,
+__global__ __launch_bounds__(MZ_ADAMW_TPB) void k_adamw(float* __restrict__ p, float* __restrict__ m,
                                                float* __restrict__ v, Segs segs,
                                                const float* __restrict__ lr_dev,
                                                float* step_dev, double b1,
@@ -239,10 +251,10 @@ hipError_t mz_launch_adamw(float* p, float* m, float* v, const float* const* gra
     sg.off[k + 1] = sg.off[k] + seg_len[k];
   }
   const int64_t n4 = sg.off[nseg] >> 2;
-  int blocks = (int)((n4 + 255) / 256);
-  if (blocks > 2048) blocks = 2048;  // 8 workgroups per CU, grid-stride beyond
+  int blocks = (int)((n4 + MZ_ADAMW_TPB - 1) / MZ_ADAMW_TPB);
+  if (blocks > MZ_ADAMW_MAXWG) blocks = MZ_ADAMW_MAXWG;  // grid-stride beyond
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(k_adamw, dim3(blocks), dim3(256), 0, s, p, m, v, sg, lr, step, b1, b2, eps, wd,
+  hipLaunchKernelGGL(k_adamw, dim3(blocks), dim3(MZ_ADAMW_TPB), 0, s, p, m, v, sg, lr, step, b1, b2, eps, wd,
                      clamp, gscale, write_grad);
   return hipGetLastError();
 }
