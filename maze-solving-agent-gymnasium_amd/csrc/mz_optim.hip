@@ -318,11 +318,15 @@ hipError_t mz_launch_pair_surrogate(const float* lp_new, const float* lp_old, co
 // against a ones vector took ~20 us for [2,048 x 1,024] (plus the ones fill); here 64 columns
 // per workgroup, 16-B loads (4 columns per lane), 64 row groups summed in LDS in a fixed order
 // (deterministic).
-static __global__ __launch_bounds__(1024) void k_colsum(const float* __restrict__ g, int n, int m,
-                                                        int ld, float* __restrict__ out) {
-  __shared__ float4 part[64][16];
-  const int cq = threadIdx.x & 15, rg = threadIdx.x >> 4;
-  const int c = blockIdx.x * 64 + cq * 4;
+#ifndef MZ_COLSUM_CQ
+#define MZ_COLSUM_CQ 16  // column quads per workgroup (64 row groups each)
+#endif
+static __global__ __launch_bounds__(64 * MZ_COLSUM_CQ) void k_colsum(const float* __restrict__ g,
+                                                                    int n, int m, int ld,
+                                                                    float* __restrict__ out) {
+  __shared__ float4 part[64][MZ_COLSUM_CQ];
+  const int cq = threadIdx.x % MZ_COLSUM_CQ, rg = threadIdx.x / MZ_COLSUM_CQ;
+  const int c = blockIdx.x * (4 * MZ_COLSUM_CQ) + cq * 4;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (c < m) {
     // 8 rows' loads in flight before their adds (same summation order): a load-add chain waited
@@ -354,7 +358,9 @@ static __global__ __launch_bounds__(1024) void k_colsum(const float* __restrict_
 
 hipError_t mz_launch_colsum(const float* g, int n, int m, int ld, float* out, hipStream_t s) {
   if (m <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_colsum, dim3((m + 63) / 64), dim3(1024), 0, s, g, n, m, ld, out);
+  constexpr int cols = 4 * MZ_COLSUM_CQ;
+  hipLaunchKernelGGL(k_colsum, dim3((m + cols - 1) / cols), dim3(64 * MZ_COLSUM_CQ), 0, s, g, n, m,
+                     ld, out);
   return hipGetLastError();
 }
 
