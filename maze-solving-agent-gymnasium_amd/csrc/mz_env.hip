@@ -10,8 +10,8 @@
 //                   reading 15 consecutive 32-B rows of one instance (few cache lines per load);
 //                 phase 3, the wave's IPW windows (675 bits each, back to back in LDS) leave as f32
 //                   with 16-B stores, 1 KiB contiguous per wave instruction.
-//   k_reset_list  one wave per listed instance: BaseMazeEnv.reset (:136-161); consumes the
-//                 device done count it was given (zeroes it when the grid has read it).
+//   k_reset_list  one wave per listed instance: BaseMazeEnv.reset (:136-161); the device done
+//                 count it was given is consumed (zeroed) by a memset after the launch.
 //   k_build / k_regen_list  maze generation + tables (mz_build.inc.h).
 //   k_act / k_mask / k_expand  exploration act, get_mask_direction, bits -> f32.
 //
@@ -580,16 +580,8 @@ __global__ __launch_bounds__(WAVE) void k_reset_list(MzDev d, const int32_t* idx
     reset_one<TOR, ENRICH>(d, e, o, wsh);
     __syncthreads();
   }
-  if (count && threadIdx.x == 0) {
-    // Consume the count: zero it once every block has read it. Each block's read of *count
-    // has returned before its ticket add issues (the add follows the loop whose bound is that
-    // value), so a relaxed device-scope ticket suffices — no per-block L2 write-back fence.
-    const int t = atomicAdd(d.ticket, 1);
-    if (t == (int)gridDim.x - 1) {
-      __hip_atomic_store(count, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(d.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
+  // the count is consumed (zeroed) by a stream-ordered memset after the launch: a last-block
+  // ticket here cost one same-address atomic per block, serialised (~30 ns each, up to 1,024)
 }
 
 // Copy the next unconsumed bank maze of algorithm a into instance e (cells + plane rows + meta;
@@ -886,7 +878,9 @@ hipError_t mz_launch_reset_list(const MzDev& d, const int32_t* idx, int32_t* cou
   if (d.toroidal) { if (d.enrich) MZ_RL(true, true); else MZ_RL(true, false); }
   else { if (d.enrich) MZ_RL(false, true); else MZ_RL(false, false); }
 #undef MZ_RL
-  return hipGetLastError();
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess && count) e = hipMemsetAsync(count, 0, sizeof(int32_t), s);  // consumed
+  return e;
 }
 
 hipError_t mz_launch_reset_done(const MzDev& d, int regen, uint64_t seed, uint32_t epoch,
