@@ -29,7 +29,39 @@ sys.path.insert(0, os.path.join(ROOT, "maze-solving-agent-gymnasium_amd"))
 # Algorithmic bytes per instance-step of k_step: 66 B compact state/outputs
 # + 2,955 B for the Enrich window (2,700 B f32 window write + 225 B visit plane + 30 B wall rows)
 ALG_BYTES_PER_STEP = 3021
+# the same step in the mode the trainers run (window_bits=True, window=False): the 675-bit
+# window written as 88 B of bits instead of 2,700 B of f32 — 3,021 - 2,700 + 88
+ALG_BYTES_PER_STEP_BITS = 409
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# the sources k_step is built from: the PMC traffic file is only used when it was taken from them
+KSTEP_SOURCES = ("mz_env.hip", "mz_common.h", "mz_kernels.h", "mz_build.inc.h")
+
+
+def kstep_source_sha():
+    import hashlib
+    h = hashlib.sha256()
+    for f in KSTEP_SOURCES:
+        with open(os.path.join(ROOT, "maze-solving-agent-gymnasium_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(mode, envs, dim):
+    """HBM bytes per k_step launch from profiles/pmc_k_step.json (separate rocprofv3 --pmc
+    passes, profiles/collect.sh) — None unless taken from the current k_step sources at this
+    config."""
+    pmc = os.path.join(ROOT, "profiles", "pmc_k_step.json")
+    if not os.path.exists(pmc):
+        return None, "no PMC file"
+    with open(pmc) as f:
+        p = json.load(f)
+    rec = p.get(mode)
+    if not rec or rec.get("envs") != envs or rec.get("dim") != dim:
+        return None, f"no PMC record for {mode} mode at {envs} x {dim}"
+    if rec.get("source_sha") != kstep_source_sha():
+        return None, "PMC record is stale: k_step's sources changed since it was taken"
+    return rec.get("hbm_bytes_per_launch"), (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes "
+                                              f"({rec.get('tag')}), k_step sources {rec['source_sha']}")
 
 
 def parse():
@@ -42,6 +74,9 @@ def parse():
     ap.add_argument("--algo", default="r-prim")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="cpu_baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--legs", default="window,bits",
+                    help="env-step legs: window (f32 Enrich window, the headline) and bits (the "
+                         "trainers' mode: 88-B window bits)")
     # 2,400 vector steps (157 M env steps, ~4 s): greedy win-rate 94.4 / 95.4 / 96.5 / 96.1 /
     # 95.9 % after 600 / 1,200 / 2,400 / 4,800 / 9,600 (one run each) — the plateau
     ap.add_argument("--train-steps", type=int, default=2400,
@@ -102,6 +137,7 @@ def win_rate(a, dev, rank=0, world=1):
     env.close()
     if rank != 0:
         return None
+    agree = acting_agreement(L)
     g, _ = evaluate(L, a.eval_mazes, a.dim, a.algo, seed=0x7E570000, eps=0.0, device=dev)
     e, _ = evaluate(L, a.eval_mazes, a.dim, a.algo, seed=0x7E570000, eps=0.1, device=dev)
     # the same protocol on mazes chosen as the reference's env chooses them: the easiest (McClendon
@@ -122,9 +158,41 @@ def win_rate(a, dev, rank=0, world=1):
             "grad_allreduce": (f"{dist.get_backend()} ({'RCCL' if dist.get_backend() == 'nccl' else 'rehearsal'}), "
                                "one 8.56 MB fp32 bucket per update between two graph replays")
                               if world > 1 else None,
+            "acting_argmax_agreement": agree,
             "note": "fresh GPU-generated mazes never seen in training (test(new=True) protocol); "
                     "*_best_of_6: each maze the easiest of 6 candidates by McClendon difficulty, "
                     "as the reference's env selects new mazes (base_maze_env.py:78-97)"}
+
+
+def acting_agreement(L, n=65536):
+    """How often the acting head's greedy action (the fused stem + GEMMs the trainer acts with)
+    equals argmax of the f32 QNet (the reference's source_net(state).max(1), dqn_agent.py:
+    113-116) on the newest n replay states — real trainer observations — with train-mode
+    dropout off on both sides (the same stem on both: the comparison isolates precision)."""
+    import torch
+    rp = L.replay
+    n = min(n, rp.size)
+    idx = (torch.arange(rp.ptr - n, rp.ptr, device=rp.s6.device) % rp.capacity)
+    s6, sw = rp.s6.index_select(0, idx), rp.sw.index_select(0, idx)
+    net, fused = L.source, L.fused
+    was = net.training
+    net.eval()
+    try:
+        with torch.no_grad():
+            q32 = net((s6, sw)).float()
+            fused.invalidate()
+            qa = fused(s6, sw).float()
+    finally:
+        net.train(was)
+        fused.invalidate()
+    a32, aa = q32.argmax(1), qa.argmax(1)
+    top2 = q32.topk(2, dim=1).values
+    gap = (top2[:, 0] - top2[:, 1]) / q32.abs().amax(1).clamp_min(1e-30)
+    clear = gap > 1e-2
+    return {"rows": n, "agreement": float((a32 == aa).float().mean()),
+            "agreement_f32_gap_over_1pct": float((a32 == aa)[clear].float().mean()),
+            "rows_f32_gap_over_1pct": int(clear.sum()),
+            "acting_dtype": getattr(fused, "dtype_note", "bf16 GEMMs (f32 accumulate), bf16 stem")}
 
 
 BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X bf16 MFMA, dense (MI355X_MICROARCH.md)
@@ -173,6 +241,23 @@ def q_head(dev, n, iters=50):
             "dtype": "bf16 (f32 accumulate)", "peak_tflops": BF16_DENSE_PEAK_TFLOPS}
 
 
+def host_threads():
+    """Every host core this process may use: the CPU affinity set, capped by the cgroup's CPU
+    quota when one is set (a GPU box's share of a larger machine: os.cpu_count() and the
+    affinity set show the whole machine there, the quota is what the threads get)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    n = min(aff, quota) if quota else aff
+    return n, {"affinity_cpus": aff, "cgroup_cpu_quota": quota, "threads": n}
+
+
 def cpu_baseline(env, seconds):
     """Oracle (oracle/mzoracle.c, 'port' of the reference algorithm at its cost model: heap A*
     for every find_path) timed on this host's cores on one of the benchmark's own mazes."""
@@ -182,7 +267,7 @@ def cpu_baseline(env, seconds):
     q = env.query(0)
     grid = env.grid(0)
     start, goal = (q["start_r"], q["start_c"]), (q["goal_r"], q["goal_c"])
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads, cpu_note = host_threads()
     # calibrate on a short run, then size the sample to ~`seconds`
     t, n = O.bench(grid, start, goal, False, True, True, threads, 20, threads)
     rate = n / max(t, 1e-9)
@@ -204,6 +289,7 @@ def cpu_baseline(env, seconds):
         tc, nc = O.bench(g2, s2, g2p, tor, True, True, threads, per, threads, seed=5)
         per_config[name] = {"value": nc / tc, "steps": nc, "seconds": round(tc, 2)}
     return {"value": n / t, "unit": "env steps/s", "cores": threads, "kind": "port",
+            "cores_note": cpu_note,
             "single_core": {"value": n1 / t1, "steps": n1, "seconds": round(t1, 2)},
             "per_config": per_config,
             "sample": f"{threads} envs x {per_env} steps (81x81 r-prim Enrich, masked-exploration "
@@ -229,50 +315,65 @@ def main():
 
     import mazerl
     B = a.envs
-    # global instance ids rank*B .. : Philox seed 0x5EED0000 + global id
-    t0 = time.perf_counter()
-    env = mazerl.VectorMazeEnv(B, a.dim, enrich=True, device=dev, algorithm=a.algo,
-                               seed=0x5EED0000 + rank * B, window=True, window_bits=False,
-                               pos=False, done_list=False)
-    torch.cuda.synchronize()
-    gen_s = time.perf_counter() - t0
+    legs = [x for x in a.legs.split(",") if x]
+
+    def leg(mode):
+        """One env-step leg: generate B mazes (global instance ids rank*B.. : Philox seed
+        0x5EED0000 + global id), W untimed + K timed vector steps, each one k_step
+        launch (fused act + step + autoreset), inputs resident in HBM."""
+        t0 = time.perf_counter()
+        env = mazerl.VectorMazeEnv(B, a.dim, enrich=True, device=dev, algorithm=a.algo,
+                                   seed=0x5EED0000 + rank * B, window=mode == "window",
+                                   window_bits=mode == "bits", pos=False, done_list=False)
+        torch.cuda.synchronize()
+        gen_s = time.perf_counter() - t0
+        stream = torch.cuda.current_stream(dev)
+
+        def vstep(k):
+            # one launch: fused act + step, autoreset of the instances that finished last step
+            env.step_act(eps=1.0, seed=0xBE7C4 + rank, counter=k, autoreset=True)
+
+        for k in range(a.warmup):
+            vstep(k)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for k in range(a.steps):
+            vstep(a.warmup + k)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        avg_kernel_ms = ev0.elapsed_time(ev1) / a.steps
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        alg = ALG_BYTES_PER_STEP if mode == "window" else ALG_BYTES_PER_STEP_BITS
+        achieved = alg * B / (avg_kernel_ms * 1e-3) / 1e9
+        traffic, tnote = pmc_traffic(mode, B, a.dim)
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "kernel": "k_step", "avg_kernel_ms": avg_kernel_ms,
+                "timing": "HIP events around the timed region on the launch stream",
+                "alg_bytes_per_instance_step": alg, "traffic_source": tnote}
+        return env, {"value": B * a.steps * world / el, "ms_per_step": el / a.steps * 1e3,
+                     "roofline": roof, "gen_s": gen_s}
+
+    res = {}
+    env = None
+    for mode in legs:
+        if env is not None:
+            env.close()
+        env, res[mode] = leg(mode)
+    head = res["window"] if "window" in res else res[legs[0]]
+    value, gen_s = head["value"], head["gen_s"]
     stream = torch.cuda.current_stream(dev)
-
-    def vstep(k):
-        # one launch: fused act + step, autoreset of the instances that finished last step
-        env.step_act(eps=1.0, seed=0xBE7C4 + rank, counter=k, autoreset=True)
-
-    for k in range(a.warmup):
-        vstep(k)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for k in range(a.steps):
-        vstep(a.warmup + k)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    avg_kernel_ms = ev0.elapsed_time(ev1) / a.steps
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    total_steps = B * a.steps * world
-    value = total_steps / el
-    achieved = ALG_BYTES_PER_STEP * B / (avg_kernel_ms * 1e-3) / 1e9
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_k_step.json")
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            p = json.load(f)
-        if p.get("envs") == B and p.get("dim") == a.dim:
-            traffic = p.get("hbm_bytes_per_launch")
 
     # steady-state regeneration of all B mazes per algorithm (after the timed region; the module
     # is loaded): one mz_generate launch each, HIP events on the launch stream
@@ -293,7 +394,7 @@ def main():
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": el / a.steps * 1e3,
+            "ms_per_step": head["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -302,11 +403,13 @@ def main():
             "config": {"workload": f"{B} x 40x40-cell ({a.dim}x{a.dim} grid) {a.algo} Enrich mazes "
                                    f"per GPU: fused act + env step (f32 3x15x15 window) with autoreset, one launch per step",
                        "envs_per_gpu": B, "grid": a.dim, "algo": a.algo, "parallelism": f"dp{world} env shards"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_step", "avg_kernel_ms": avg_kernel_ms,
-                         "timing": "HIP events around the timed region on the launch stream",
-                         "alg_bytes_per_instance_step": ALG_BYTES_PER_STEP},
+            "roofline": head["roofline"],
+            "bits_mode": ({"value": res["bits"]["value"], "unit": "env steps/s",
+                           "ms_per_step": res["bits"]["ms_per_step"],
+                           "roofline": res["bits"]["roofline"],
+                           "note": "the same step in the trainers' mode (window_bits=True: the "
+                                   "675-bit window as 88 B of bits, no f32 window)"}
+                          if "bits" in res and "window" in res else None),
             "generation": {"mazes": B, "seconds": round(gen_s, 3), "mazes_per_s": B / gen_s,
                            "note": "first build incl. module load; excluded from value",
                            "steady_mazes_per_s": steady,

@@ -306,10 +306,11 @@ int mz_pair_surrogate(const float* lp_new_dev, const float* lp_old_dev, const fl
 /* The DQN/DDQN optimizer step (dqn_agent.py:152-157, ddqn_agent.py:148-152: grad.clamp_(-c, c)
  * per parameter, then torch.optim.AdamW) as one launch over a flat f32 parameter buffer whose
  * segment k (length seg_len[k], a multiple of 4) has its gradient at grads_dev[k] (host array of
- * nseg <= 16 device pointers). lr_dev: device f32 learning rate. step_dev: device f32 [2] —
- * [0] the step count (advanced by one by the launch itself, so a captured graph advances it per
- * replay), [1] a workgroup ticket the launch uses (zero it once at allocation). write_grad: store
- * the clamped, grad_scale-scaled gradient back (clamp_ in place). */
+ * nseg <= 16 device pointers). lr_dev: device f32 learning rate. step_dev: device f32 [1], the
+ * step count, advanced by one by the launch itself (so a captured graph advances it per replay;
+ * the workgroup ticket that finds the last workgroup is library-owned device memory, one slot
+ * per step_dev address, at most 4,096 distinct counters per process). write_grad: store the
+ * clamped, grad_scale-scaled gradient back (clamp_ in place). */
 int mz_adamw_flat(float* param_dev, float* exp_avg_dev, float* exp_avg_sq_dev,
                   const float* const* grads_dev, const int64_t* seg_len, int32_t nseg,
                   const float* lr_dev, float* step_dev, double beta1, double beta2, double eps,
@@ -440,6 +441,50 @@ int mz_adamw_groups(float* param_dev, float* exp_avg_dev, float* exp_avg_sq_dev,
                     const int32_t* seg_group, int32_t nseg, const float* lr_dev, float* step_dev,
                     double beta1, double beta2, double eps, double weight_decay, float max_norm,
                     float* scratch_dev, void* stream);
+
+/* ---- Config 5's PPO rollout on the device (VectorPPOTrainer; no host round trip per step) ----
+ * B instances, per-instance episode records [B][L] at the instance's own step index t_dev[i]
+ * (L > the longest possible episode). Replaces, per instance, PPOAgent.do_episode's loop
+ * (agents/ppo_agent.py:143-169) and PPOTrainer.train's Buffer.add (lib/trainers/ppo_trainer.py
+ * :15-46, :66-67). */
+
+/* ActorCriticNet.act (ppo_agent.py:55-68) from the f32 actor logits [B][ldl] and critic values
+ * [B] (stride ldv): softmax as torch forms it for a 4-wide row, one draw per instance (inverse
+ * CDF of a Philox uniform: P(a) = softmax(logits)[a], torch.multinomial's distribution), the
+ * draw's log-prob log(p[a]); records obs6, the 22 window-bit words, action (int64), log-prob and
+ * value at [i][t_dev[i]] (do_episode's appends, :150-156) and writes the action to act_out_dev
+ * (int32, mz_step's input). */
+int mz_ppo_act(const float* logits_dev, int32_t ldl, const float* value_dev, int32_t ldv,
+               const float* obs6_dev, const uint32_t* bits_dev, int32_t B, int32_t L, uint64_t seed,
+               uint64_t counter, const int32_t* t_dev, float* rec_s6_dev, uint32_t* rec_w_dev,
+               int64_t* rec_a_dev, float* rec_lp_dev, float* rec_v_dev, int32_t* act_out_dev,
+               void* stream);
+
+/* After mz_step: the float64 reward at [i][t_dev[i]] (rewards.append, :158), t_dev[i] += 1, and
+ * for every instance whose step ended (terminated | truncated, :161): t_dev[i] = 0, stats_dev
+ * [0] += 1 (episodes), [1] += terminated (wins), and — for episodes of >= 2 steps (a 1-step
+ * episode's returns are NaN: torch.std of one element; counted in stats_dev[2] instead) — an
+ * entry in the finished list (instance fin_id, pool row fin_off, length fin_len; instance order)
+ * placed after the pool's current *pool_fill_dev rows; *pool_fill_dev and the monotonic
+ * *pool_total_dev grow by the listed rows. One workgroup. */
+int mz_ppo_scan(const double* reward64_dev, const uint8_t* term_dev, const uint8_t* trunc_dev,
+                int32_t B, int32_t L, int32_t* t_dev, double* rec_r_dev, int32_t* fin_id_dev,
+                int64_t* fin_off_dev, int32_t* fin_len_dev, int32_t* fin_count_dev,
+                int64_t* pool_fill_dev, int64_t* pool_total_dev, int64_t* stats_dev,
+                void* stream);
+
+/* For every listed episode: calculate_returns (ppo_agent.py:171-181: acc = r + acc * gamma
+ * backwards in float64, float32, (R - mean) / std, unbiased std) and calculate_advantages
+ * (:183-186: A = R - V, (A - mean) / (std + 1e-8)) — sums in float64, mean / std rounded to
+ * float32 — and the episode's rows (obs6, window bits, action, log-prob, advantage, return)
+ * into the pool columns at its rows (rows past `capacity` are not written: the caller checks
+ * *pool_fill_dev <= capacity). One workgroup per episode. */
+int mz_ppo_finish(const double* rec_r_dev, const float* rec_s6_dev, const uint32_t* rec_w_dev,
+                  const int64_t* rec_a_dev, const float* rec_lp_dev, const float* rec_v_dev,
+                  int32_t B, int32_t L, const int32_t* fin_id_dev, const int64_t* fin_off_dev,
+                  const int32_t* fin_len_dev, const int32_t* fin_count_dev, double gamma,
+                  int64_t capacity, float* pool_s6_dev, uint32_t* pool_w_dev, int64_t* pool_a_dev,
+                  float* pool_lp_dev, float* pool_adv_dev, float* pool_ret_dev, void* stream);
 
 #ifdef __cplusplus
 }

@@ -73,6 +73,22 @@ struct DeviceGuard {  // run a call on the handle's device, restore the caller's
   }
 };
 
+// Entry points that take device pointers and a stream but no handle run on the stream's device
+// (the caller's current device for the null stream), restoring the caller's device afterwards.
+struct StreamGuard {
+  int prev = -1;
+  explicit StreamGuard(void* stream) {
+    hipDevice_t dev;
+    if (!stream || hipStreamGetDevice(static_cast<hipStream_t>(stream), &dev) != hipSuccess) return;
+    if (hipGetDevice(&prev) != hipSuccess) { prev = -1; return; }
+    if (prev != (int)dev) (void)hipSetDevice((int)dev);
+  }
+  ~StreamGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
 MzOut to_dev(const mz_step_out* o) {
   MzOut m;
   std::memset(&m, 0, sizeof m);
@@ -642,6 +658,7 @@ int mz_discounted_returns(const double* rew_dev, int32_t ld, const int32_t* rows
                           const int32_t* lens_dev, int32_t n, double gamma, float* out_dev,
                           int32_t ldo, void* stream) {
   if (!rew_dev || !rows_dev || !lens_dev || !out_dev || n < 0) return fail(MZ_EINVAL, "bad arguments");
+  StreamGuard g(stream);
   MZ_HIP(mz_launch_returns(rew_dev, ld, rows_dev, lens_dev, n, gamma, out_dev, ldo,
                            static_cast<hipStream_t>(stream)));
   return MZ_OK;
@@ -831,3 +848,56 @@ int mz_adamw_groups(float* param_dev, float* exp_avg_dev, float* exp_avg_sq_dev,
                                 static_cast<hipStream_t>(stream)));
   return MZ_OK;
 }
+
+int mz_ppo_act(const float* logits_dev, int32_t ldl, const float* value_dev, int32_t ldv,
+               const float* obs6_dev, const uint32_t* bits_dev, int32_t B, int32_t L, uint64_t seed,
+               uint64_t counter, const int32_t* t_dev, float* rec_s6_dev, uint32_t* rec_w_dev,
+               int64_t* rec_a_dev, float* rec_lp_dev, float* rec_v_dev, int32_t* act_out_dev,
+               void* stream) {
+  if (!logits_dev || !value_dev || !obs6_dev || !bits_dev || !t_dev || !rec_s6_dev || !rec_w_dev ||
+      !rec_a_dev || !rec_lp_dev || !rec_v_dev || !act_out_dev || B < 0 || L < 1 || ldl < 4 ||
+      ldv < 1)
+    return fail(MZ_EINVAL, "bad arguments");
+  StreamGuard g(stream);
+  MzPpoAct q{logits_dev, ldl, value_dev, ldv, obs6_dev, bits_dev, B, L, seed, counter, t_dev,
+             rec_s6_dev, rec_w_dev, rec_a_dev, rec_lp_dev, rec_v_dev, act_out_dev};
+  MZ_HIP(mz_launch_ppo_act(q, static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
+int mz_ppo_scan(const double* reward64_dev, const uint8_t* term_dev, const uint8_t* trunc_dev,
+                int32_t B, int32_t L, int32_t* t_dev, double* rec_r_dev, int32_t* fin_id_dev,
+                int64_t* fin_off_dev, int32_t* fin_len_dev, int32_t* fin_count_dev,
+                int64_t* pool_fill_dev, int64_t* pool_total_dev, int64_t* stats_dev,
+                void* stream) {
+  if (!reward64_dev || !term_dev || !trunc_dev || !t_dev || !rec_r_dev || !fin_id_dev ||
+      !fin_off_dev || !fin_len_dev || !fin_count_dev || !pool_fill_dev || !pool_total_dev ||
+      !stats_dev || B < 0 || L < 1)
+    return fail(MZ_EINVAL, "bad arguments");
+  StreamGuard g(stream);
+  MzPpoScan q{reward64_dev, term_dev, trunc_dev, B, L, t_dev, rec_r_dev, fin_id_dev, fin_off_dev,
+              fin_len_dev, fin_count_dev, pool_fill_dev, pool_total_dev,
+              reinterpret_cast<long long*>(stats_dev)};
+  MZ_HIP(mz_launch_ppo_scan(q, static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
+int mz_ppo_finish(const double* rec_r_dev, const float* rec_s6_dev, const uint32_t* rec_w_dev,
+                  const int64_t* rec_a_dev, const float* rec_lp_dev, const float* rec_v_dev,
+                  int32_t B, int32_t L, const int32_t* fin_id_dev, const int64_t* fin_off_dev,
+                  const int32_t* fin_len_dev, const int32_t* fin_count_dev, double gamma,
+                  int64_t capacity, float* pool_s6_dev, uint32_t* pool_w_dev, int64_t* pool_a_dev,
+                  float* pool_lp_dev, float* pool_adv_dev, float* pool_ret_dev, void* stream) {
+  if (!rec_r_dev || !rec_s6_dev || !rec_w_dev || !rec_a_dev || !rec_lp_dev || !rec_v_dev ||
+      !fin_id_dev || !fin_off_dev || !fin_len_dev || !fin_count_dev || !pool_s6_dev ||
+      !pool_w_dev || !pool_a_dev || !pool_lp_dev || !pool_adv_dev || !pool_ret_dev || B < 0 ||
+      L < 1 || capacity < 0)
+    return fail(MZ_EINVAL, "bad arguments");
+  StreamGuard g(stream);
+  MzPpoFinish q{rec_r_dev, rec_s6_dev, rec_w_dev, rec_a_dev, rec_lp_dev, rec_v_dev, L, fin_id_dev,
+                fin_off_dev, fin_len_dev, fin_count_dev, gamma, capacity, pool_s6_dev, pool_w_dev,
+                pool_a_dev, pool_lp_dev, pool_adv_dev, pool_ret_dev};
+  MZ_HIP(mz_launch_ppo_finish(q, B, static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+

@@ -136,6 +136,7 @@ __host__ __device__ inline void mz_philox(uint64_t key, uint64_t ctr_hi, uint64_
 #define MZ_GEN_STREAM 0x6D617A65ull  // 'maze': generation draws
 #define MZ_ACT_STREAM 0x61637421ull  // 'act!': exploration draws
 #define MZ_REPLAY_STREAM 0x72706c79ull  // 'rply': replay sample rows
+#define MZ_PPO_STREAM 0x70706f21ull  // 'ppo!': PPO policy draws
 
 // Sequential draw stream (one per maze): draw k = word (k & 3) of philox(key, {GEN, k >> 2}).
 struct MzRng {

@@ -705,7 +705,7 @@ __global__ void k_mask(MzDev d, int probs, float* out4) {
 // only when it fails): the instances whose next fused act (same seed / counter / eps) takes
 // greedy_dev[i], in increasing instance order. Two launches, no atomics (a fixed order, so the
 // acting forward over the list is deterministic): per-1024-instance counts, then the list.
-constexpr int GR_BLOCK = 1024;
+constexpr int GR_BLOCK = MZ_GR_BLOCK;  // shared with k_tick_count (mz_trainer.hip)
 __device__ inline bool greedy_needed(const MzAct& ap, int e) {
   uint32_t u[4];
   act_u(ap, e, u);

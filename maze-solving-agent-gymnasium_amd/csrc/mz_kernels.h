@@ -41,6 +41,11 @@ hipError_t mz_launch_stem_bwd(const uint32_t* bits, const uint8_t* code, const f
                               int n, float drop_p, float* partial, float* dw, float* db,
                               hipStream_t s);
 #define MZ_OPT_MAX_SEGS 16
+
+// Instances per workgroup of the greedy-row list (k_greedy_count / k_greedy_list, mz_env.hip) and
+// of the trainer tick's per-block counts (k_tick_count, mz_trainer.hip): the tick writes the
+// per-block counts the list kernel then reads as its block prefix sums, so both must use this.
+constexpr int MZ_GR_BLOCK = 1024;
 hipError_t mz_launch_adamw(float* p, float* m, float* v, const float* const* grads,
                            const int64_t* seg_len, int nseg, const float* lr, float* step, double b1,
                            double b2, double eps, double wd, float clamp, float gscale,
@@ -92,3 +97,32 @@ hipError_t mz_launch_adamw_groups(float* p, float* m, float* v, const float* con
                                   const int64_t* seg_len, const int32_t* seg_group, int nseg,
                                   const float* lr, float* step, double b1, double b2, double eps,
                                   double wd, float max_norm, float* scratch, hipStream_t s);
+
+// ---- PPO rollout (mz_ppo.hip) ------------------------------------------------------------
+struct MzPpoAct {
+  const float* logits; int ldl;     // actor logits [B][ldl >= 4], f32
+  const float* value; int ldv;      // critic values [B] (stride ldv)
+  const float* obs6; const uint32_t* bits;
+  int B, L;                         // instances, episode buffer length
+  uint64_t seed, counter;
+  const int32_t* t;                 // per-instance step index
+  float* b_s6; uint32_t* b_w; int64_t* b_a; float* b_lp; float* b_v;  // [B][L] records
+  int32_t* act_out;                 // [B] actions for mz_step
+};
+struct MzPpoScan {
+  const double* reward64; const uint8_t* term; const uint8_t* trunc;
+  int B, L;
+  int32_t* t; double* b_r;
+  int32_t* fin_id; int64_t* fin_off; int32_t* fin_len; int32_t* fin_count;
+  int64_t* pool_fill; int64_t* pool_total; long long* stats;
+};
+struct MzPpoFinish {
+  const double* b_r; const float* b_s6; const uint32_t* b_w; const int64_t* b_a; const float* b_lp;
+  const float* b_v; int L;
+  const int32_t* fin_id; const int64_t* fin_off; const int32_t* fin_len; const int32_t* fin_count;
+  double gamma; int64_t cap;
+  float* p_s6; uint32_t* p_w; int64_t* p_a; float* p_lp; float* p_adv; float* p_ret;
+};
+hipError_t mz_launch_ppo_act(const MzPpoAct& q, hipStream_t s);
+hipError_t mz_launch_ppo_scan(const MzPpoScan& q, hipStream_t s);
+hipError_t mz_launch_ppo_finish(const MzPpoFinish& q, int max_episodes, hipStream_t s);

@@ -19,11 +19,14 @@
 //   v = v * b2 + (1 - b2) * g * g
 //   p = p - (lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)
 // with t the step count after this step (read as step[0] + 1 by every workgroup; the last
-// workgroup to finish stores it back, so a captured HIP graph advances it on every replay without
-// a second launch) and lr read from the device (the cosine schedule writes it between replays).
+// workgroup to finish — found with a ticket the library owns — stores it back, so a captured HIP
+// graph advances it on every replay without a second launch) and lr read from the device (the cosine schedule writes it between replays).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+
+#include <mutex>
+#include <unordered_map>
 
 #include "mz_kernels.h"
 
@@ -47,13 +50,19 @@ struct Segs {
   int n;
 };
 
-// step[0] = the count, step[1] = a workgroup ticket (0 between launches): the last workgroup to
-// take a ticket has seen every other workgroup read step[0] already, and stores the new count.
-__device__ inline void publish_step(float* step, float t) {
+// The workgroup tickets live in library-owned device memory, one slot per step counter (the
+// caller's step_dev stays a plain f32 [1], mz_adamw_flat's contract): zero at module load, and the
+// last workgroup of every launch puts its slot back to zero. Slots are assigned per step_dev
+// address on the host (mz_launch_adamw) — two optimizers never share one.
+constexpr int ADAMW_TICKETS = 4096;
+__device__ unsigned g_adamw_ticket[ADAMW_TICKETS];
+
+// The last workgroup to take a ticket has seen every other workgroup read step[0] already, and
+// stores the new count.
+__device__ inline void publish_step(float* step, unsigned* ticket, float t) {
   __syncthreads();
   if (threadIdx.x == 0) {
     __threadfence();
-    unsigned* ticket = reinterpret_cast<unsigned*>(step + 1);
     if (atomicAdd(ticket, 1u) == gridDim.x - 1) {
       step[0] = t;
       *ticket = 0u;
@@ -64,7 +73,7 @@ __device__ inline void publish_step(float* step, float t) {
 __global__ __launch_bounds__(MZ_ADAMW_TPB) void k_adamw(float* __restrict__ p, float* __restrict__ m,
                                                float* __restrict__ v, Segs segs,
                                                const float* __restrict__ lr_dev,
-                                               float* step_dev, double b1,
+                                               float* step_dev, unsigned* ticket, double b1,
                                                double b2, double eps_d, double wd, float clamp,
                                                float gscale, int write_grad) {
   // the per-step scalars as torch's eager AdamW forms them (Python doubles, then f32 operands)
@@ -110,7 +119,7 @@ __global__ __launch_bounds__(MZ_ADAMW_TPB) void k_adamw(float* __restrict__ p, f
     reinterpret_cast<float4*>(v)[q] = v4;
     if (write_grad) *gp = g4;  // the clamped gradient stays visible, as with clamp_ in place
   }
-  publish_step(step_dev, t_next);
+  publish_step(step_dev, ticket, t_next);
 }
 
 // ---- PPO's optimizer step (ppo_agent.py:232-236): clip_grad_norm_(params, 0.5), then AdamW
@@ -250,11 +259,32 @@ hipError_t mz_launch_adamw(float* p, float* m, float* v, const float* const* gra
     sg.g[k] = grads[k];
     sg.off[k + 1] = sg.off[k] + seg_len[k];
   }
+  // the ticket slot of this step counter (assigned on first use; hipGetSymbolAddress is not a
+  // stream operation, so this also works while a graph is being captured)
+  static std::mutex mu;
+  static std::unordered_map<const float*, int> slots;
+  static unsigned* base = nullptr;
+  unsigned* ticket;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!base) {
+      void* p = nullptr;
+      const hipError_t e = hipGetSymbolAddress(&p, HIP_SYMBOL(g_adamw_ticket));
+      if (e != hipSuccess) return e;
+      base = static_cast<unsigned*>(p);
+    }
+    auto it = slots.find(step);
+    if (it == slots.end()) {
+      if ((int)slots.size() >= ADAMW_TICKETS) return hipErrorOutOfMemory;
+      it = slots.emplace(step, (int)slots.size()).first;
+    }
+    ticket = base + it->second;
+  }
   const int64_t n4 = sg.off[nseg] >> 2;
   int blocks = (int)((n4 + MZ_ADAMW_TPB - 1) / MZ_ADAMW_TPB);
   if (blocks > MZ_ADAMW_MAXWG) blocks = MZ_ADAMW_MAXWG;  // grid-stride beyond
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(k_adamw, dim3(blocks), dim3(MZ_ADAMW_TPB), 0, s, p, m, v, sg, lr, step, b1, b2, eps, wd,
+  hipLaunchKernelGGL(k_adamw, dim3(blocks), dim3(MZ_ADAMW_TPB), 0, s, p, m, v, sg, lr, step, ticket, b1, b2, eps, wd,
                      clamp, gscale, write_grad);
   return hipGetLastError();
 }

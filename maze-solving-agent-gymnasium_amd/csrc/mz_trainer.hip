@@ -28,7 +28,7 @@
 
 namespace {
 
-constexpr int TB = 1024;  // = GR_BLOCK of the greedy-row list (mz_env.hip): same per-block counts
+constexpr int TB = MZ_GR_BLOCK;  // the greedy-row list reads these per-block counts (mz_kernels.h)
 constexpr int W = 64;
 
 __device__ inline float eps_of(float sd, float eps_final, float eps_span, float inv_decay) {
@@ -198,14 +198,18 @@ __global__ __launch_bounds__(1024) void k_q_loss_fwd(const float* __restrict__ q
   for (int i = threadIdx.x; i < b; i += blockDim.x) {
     const float* t = qt + (size_t)i * ldt;
     float v;
+    // NaN as torch has it (a diverging net must not report a finite loss): argmax takes the
+    // first NaN as the maximum, max(1)[0] propagates any NaN
     if (qn) {
       const float* x = qn + (size_t)i * ldn;
       int best = 0;
       for (int k = 1; k < 4; ++k)
-        if (x[k] > x[best]) best = k;
+        if (!isnan(x[best]) && (isnan(x[k]) || x[k] > x[best])) best = k;
       v = t[best];
     } else {
-      v = fmaxf(fmaxf(t[0], t[1]), fmaxf(t[2], t[3]));
+      v = t[0];
+      for (int k = 1; k < 4; ++k)
+        if (!isnan(v) && (isnan(t[k]) || t[k] > v)) v = t[k];
     }
     const float expected = __fadd_rn(__fmul_rn(v, gamma), reward[i]);
     const float d = __fsub_rn(q[(size_t)i * ldq + (int)action[i]], expected);

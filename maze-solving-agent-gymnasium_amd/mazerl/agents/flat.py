@@ -76,7 +76,7 @@ class FlatAdamW(torch.optim.Optimizer):
         self.sizes = list(net._flat_sizes)
         self.exp_avg = torch.zeros_like(flat)
         self.exp_avg_sq = torch.zeros_like(flat)
-        self._step_buf = torch.zeros(2, dtype=torch.float32, device=dev)  # count, launch ticket
+        self._step_buf = torch.zeros(1, dtype=torch.float32, device=dev)  # the step count
         self.step_t = self._step_buf[0]
         self.clamp = float(clamp)
         self.grad_scale = 1.0

@@ -31,8 +31,6 @@ def main(argv=None):
     ap.add_argument("--eager-update", action="store_true", help="no captured minibatch step")
     ap.add_argument("--no-bank", action="store_true",
                     help="build winners' new mazes inline instead of copying them from a maze bank")
-    ap.add_argument("--f32-window-update", action="store_true",
-                    help="update through the f32 window + torch conv instead of the HIP bit stem")
     a = ap.parse_args(argv)
     if "-" in a.dims:
         lo, hi = (int(x) for x in a.dims.split("-"))
@@ -46,7 +44,7 @@ def main(argv=None):
                    device=dev, done_list=False, reward64=True, window=False, window_bits=True)
     tr = VectorPPOTrainer(env, dev, gamma=a.gamma, batch_size=a.batch, ppo_steps=a.ppo_steps,
                           pool_size=a.pool, seed=a.seed, use_graph=not a.eager_update,
-                          bit_stem=not a.f32_window_update, bank=not a.no_bank,
+                          bank=not a.no_bank,
                           allreduce=GradAllReduce() if world > 1 else None)
     if world > 1:
         broadcast_params(tr.net)
@@ -60,6 +58,7 @@ def main(argv=None):
                           "dims": [dims[0], dims[-1]], "vector_steps": a.steps, "train_seconds": secs,
                           "train_env_steps_per_s": a.envs * a.steps * world / secs,
                           "episodes": int(st[0]), "wins": int(st[1]), "updates": tr.updates,
+                          "acting": "f32 (ActorCriticNet.act as the reference)",
                           "win_rate_greedy": rate, "eval_steps": k}), flush=True)
     env.close()
 

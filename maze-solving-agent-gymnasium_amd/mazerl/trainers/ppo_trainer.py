@@ -1,17 +1,26 @@
 """Vectorised PPO (config 5: variable-size toroidal mazes) — PPOTrainer.train/PPOAgent.do_episode
 (lib/trainers/ppo_trainer.py:62-99, agents/ppo_agent.py:143-169) over B instances at once.
 
-Per vector step every instance acts (softmax sample of the actor head, log-prob, critic value —
-ActorCriticNet.act) and steps; its transition goes to its own episode buffer in HBM
-(obs6 f32[B,L,6], packed windows i32[B,L,22], action, log-prob, value, float64 reward; L = the
-largest possible episode, (N-1)^2 + 1). When an instance's episode ends, the episode is finished
-exactly like do_episode: discounted returns accumulated backwards in float64 on the GPU
-(mz_discounted_returns), normalised per episode with the unbiased std, advantages = returns -
-values normalised per episode; the episode's rows are appended to the update pool. When the pool
-holds `pool_size` transitions, optimize_model runs ppo_steps passes over unshuffled minibatches
-(clipped surrogate incl. the reference's [b,b] ratio broadcast, entropy bonus with the linear
-1e-2 -> 5e-4 schedule, 0.5 * value MSE, clip_grad_norm 0.5). Winners get new mazes (update_maze),
-truncated instances restart theirs.
+Per vector step, with no host round trip (csrc/mz_ppo.hip):
+  act      the f32 ActorCriticNet forward (HIP f32 conv stem from the window bits + f32 GEMMs —
+           the reference acts in f32, ppo_agent.py:55-68), then mz_ppo_act: softmax, one draw per
+           instance, the draw's log-prob, and the record of (obs6, window bits, action, log-prob,
+           value) at the instance's step index t[i] of [B, L] episode buffers in HBM (L = the
+           longest possible episode, (N-1)^2 + 2);
+  step     the env step (float64 rewards: the reference's Python floats);
+  scan     mz_ppo_scan: the reward at t[i], t[i] += 1; for finished episodes the counters, t[i] = 0
+           and the list of finished episodes with their pool offsets (instance order);
+  finish   mz_ppo_finish: per finished episode calculate_returns / calculate_advantages
+           (:171-186; returns in float64, normalised with the unbiased std) and its rows appended
+           to the update pool (fixed-capacity SoA columns in HBM);
+  reset    winners get new mazes (update_maze), truncated instances restart theirs.
+The pool's appended-rows total is copied to the host one step late (it only grows), so the
+"pool holds `pool_size` rows" test costs no synchronisation; when it passes, the update runs:
+optimize_model over the first pool_size rows (ppo_steps passes of unshuffled minibatches: clipped
+surrogate incl. the reference's [b, b] ratio broadcast, entropy bonus with the linear 1e-2 -> 5e-4
+schedule, 0.5 * value MSE, clip_grad_norm 0.5), and the rest moves to the front of the pool.
+1-step episodes (NaN returns: torch.std of one element) never reach the pool; any other row with a
+non-finite advantage or return is dropped at update time (the reference would train on NaN).
 """
 import time
 
@@ -22,159 +31,196 @@ from .. import _native as N
 from ..agents.ppo import ActorCriticNet, PPOMinibatchGraph, make_optimizer, optimize_model
 
 
+def pool_update(net, opt, cols, coef, batch_size, ppo_steps, allreduce=None, graph=None):
+    """optimize_model on one pool's rows `cols` = (obs6, window bits or f32 window, action,
+    log-prob, advantage, return). Rows with a non-finite advantage / return are dropped; with a
+    gradient all-reduce every rank keeps the smallest kept count over the ranks, so all ranks run
+    the same minibatch schedule (the same collective count and graph-replay / eager split).
+    Returns the number of rows trained on."""
+    s6, w, a, lp, adv, ret = cols
+    P = s6.shape[0]
+    keep = torch.isfinite(adv) & torch.isfinite(ret)
+    n_keep = keep.sum().reshape(1)
+    if allreduce is not None:
+        import torch.distributed as dist
+        dist.all_reduce(n_keep, op=dist.ReduceOp.MIN)
+    n_keep = int(n_keep.item())
+    if n_keep < P or not bool(keep[:n_keep].all()):
+        rows = torch.nonzero(keep).flatten()[:n_keep]
+        s6, w, a, lp, adv, ret = (x.index_select(0, rows) for x in (s6, w, a, lp, adv, ret))
+    optimize_model(net, opt, (s6, w), a[:, None], lp[:, None], adv, ret, coef, batch_size,
+                   ppo_steps, allreduce=allreduce, graph=graph)
+    return n_keep
+
+
 class VectorPPOTrainer:
     def __init__(self, env, device, actor_lr=3e-4, critic_lr=1e-4, gamma=0.9, batch_size=2048,
                  ppo_steps=4, pool_size=65536, hidden_dim=1024, h_channels=32, seed=0,
-                 allreduce=None, act_bf16=True, use_graph=True, bit_stem=True, bank=True):
+                 allreduce=None, use_graph=True, bank=True, pool_capacity=None):
         self.env = env
-        if bank and env.device.type == "cuda":
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("VectorPPOTrainer runs on the GPU (libmazerl HIP kernels)")
+        if env.window_bits is None or env.reward64 is None:
+            raise ValueError("VectorPPOTrainer needs an env with window_bits=True, reward64=True")
+        if bank:
             # winners' new mazes (update_maze) copied from a bank built ahead of time on a side
             # stream, one per grid size of the variable-size env, instead of built inline
             env.enable_bank(dims=getattr(env, "dims_in_use", None))
-        self.device = torch.device(device)
         torch.manual_seed(seed)
         self.net = ActorCriticNet(3, 6, 4, h_channels, hidden_dim).to(self.device)
-        # on the GPU the update reads the pool's packed windows through the HIP stem and replays
-        # a captured minibatch step (PPOMinibatchGraph)
-        self.on_gpu = self.device.type == "cuda"
-        self.bit_stem = self.on_gpu and bit_stem
-        self.opt = make_optimizer(self.net, actor_lr, critic_lr, capturable=self.on_gpu and use_graph)
-        self.graph = (PPOMinibatchGraph(self.net, self.opt, batch_size, allreduce)
-                      if self.on_gpu and use_graph else None)
+        # the update reads the pool's packed windows through the HIP stem and replays a captured
+        # minibatch step (PPOMinibatchGraph)
+        self.opt = make_optimizer(self.net, actor_lr, critic_lr, capturable=use_graph)
+        self.graph = PPOMinibatchGraph(self.net, self.opt, batch_size, allreduce) if use_graph else None
         self.gamma, self.batch_size, self.ppo_steps = gamma, batch_size, ppo_steps
-        self.pool_size = pool_size
+        self.pool_size = int(pool_size)
         self.allreduce = allreduce
-        self.act_bf16 = act_bf16
+        self.seed = int(seed)
+        self.counter = 0
         B = env.num_envs
-        self.L = (env.max_dim - 1) ** 2 + 2
+        self.L = L = (env.max_dim - 1) ** 2 + 2
         kw = dict(device=self.device)
-        self.b_s6 = torch.zeros(B, self.L, 6, dtype=torch.float32, **kw)
-        self.b_w = torch.zeros(B, self.L, 22, dtype=torch.int32, **kw)
-        self.b_a = torch.zeros(B, self.L, dtype=torch.int64, **kw)
-        self.b_lp = torch.zeros(B, self.L, dtype=torch.float32, **kw)
-        self.b_v = torch.zeros(B, self.L, dtype=torch.float32, **kw)
-        self.b_r = torch.zeros(B, self.L, dtype=torch.float64, **kw)
-        self.t = torch.zeros(B, dtype=torch.int64, **kw)
-        self.ar = torch.arange(B, **kw)
-        self.pool = []
-        self.pool_n = 0
-        self.episodes = 0
-        self.wins = 0
+        # per-instance episode records [B, L]
+        self.b_s6 = torch.zeros(B, L, 6, dtype=torch.float32, **kw)
+        self.b_w = torch.zeros(B, L, 22, dtype=torch.int32, **kw)
+        self.b_a = torch.zeros(B, L, dtype=torch.int64, **kw)
+        self.b_lp = torch.zeros(B, L, dtype=torch.float32, **kw)
+        self.b_v = torch.zeros(B, L, dtype=torch.float32, **kw)
+        self.b_r = torch.zeros(B, L, dtype=torch.float64, **kw)
+        self.t = torch.zeros(B, dtype=torch.int32, **kw)
+        self.act_out = torch.zeros(B, dtype=torch.int32, **kw)
+        # the update pool. Fill bound at an update: < pool_size + the rows two vector steps can
+        # append (an instance appends <= L rows over two steps: an episode that ends at step t-1
+        # leaves a 1-step one at step t); 2 B L leaves room for ranks that fill at different rates
+        self.cap = int(pool_capacity or self.pool_size + 2 * B * L)
+        C = self.cap
+        self.p_s6 = torch.zeros(C, 6, dtype=torch.float32, **kw)
+        self.p_w = torch.zeros(C, 22, dtype=torch.int32, **kw)
+        self.p_a = torch.zeros(C, dtype=torch.int64, **kw)
+        self.p_lp = torch.zeros(C, dtype=torch.float32, **kw)
+        self.p_adv = torch.zeros(C, dtype=torch.float32, **kw)
+        self.p_ret = torch.zeros(C, dtype=torch.float32, **kw)
+        self.fin_id = torch.zeros(B, dtype=torch.int32, **kw)
+        self.fin_off = torch.zeros(B, dtype=torch.int64, **kw)
+        self.fin_len = torch.zeros(B, dtype=torch.int32, **kw)
+        self.fin_count = torch.zeros(1, dtype=torch.int32, **kw)
+        self.pool_fill = torch.zeros(1, dtype=torch.int64, **kw)
+        self.pool_total = torch.zeros(1, dtype=torch.int64, **kw)
+        self.stats = torch.zeros(3, dtype=torch.int64, **kw)  # episodes, wins, dropped 1-step
+        self._total_host = torch.zeros(1, dtype=torch.int64, pin_memory=True)
+        self._total_ev = None
+        self.consumed = 0
         self.updates = 0
-        self.gen = torch.Generator(device=self.device)
-        self.gen.manual_seed(seed)
-        self.fused = None
-        if self.device.type == "cuda" and act_bf16:
-            from ..agents.fused import FusedActorCritic
-            self.fused = FusedActorCritic(self.net, seed=seed)
+        self.rows_trained = 0
+        self.lib = N.load()
 
     @property
     def supports_bits(self):
-        return self.fused is not None
+        return True
+
+    @property
+    def episodes(self):
+        return int(self.stats[0])
+
+    @property
+    def wins(self):
+        return int(self.stats[1])
+
+    def _stream(self):
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def _cols(self, lo, hi):
+        return (self.p_s6[lo:hi], self.p_w[lo:hi], self.p_a[lo:hi], self.p_lp[lo:hi],
+                self.p_adv[lo:hi], self.p_ret[lo:hi])
 
     @torch.no_grad()
     def _act(self):
+        """ActorCriticNet.act in f32 for every instance + the record at t[i] (mz_ppo_act)."""
         env = self.env
-        state = (env.obs6, env.window)
-        if self.fused is not None and env.window_bits is not None:
-            logits, value = self.fused(env.obs6, env.window_bits)
-        elif self.act_bf16 and self.device.type == "cuda":
-            with torch.autocast("cuda", dtype=torch.bfloat16):
-                logits, value = self.net(state)
-        else:
-            logits, value = self.net(state)
-        prob = F.softmax(logits.float(), dim=-1)
-        a = torch.multinomial(prob, 1, generator=self.gen)
-        lp = torch.log(prob.gather(1, a).squeeze(1))
-        return a.squeeze(1), lp, value.float().squeeze(1)
+        logits, value = self.net((env.obs6, env.window_bits))
+        logits, value = logits.contiguous(), value.contiguous()
+        B = env.num_envs
+        N.check(self.lib.mz_ppo_act(
+            logits.data_ptr(), logits.stride(0), value.data_ptr(), value.stride(0),
+            env.obs6.data_ptr(), env.window_bits.data_ptr(), B, self.L,
+            self.seed & 0xFFFFFFFFFFFFFFFF, self.counter & 0xFFFFFFFFFFFFFFFF, self.t.data_ptr(),
+            self.b_s6.data_ptr(), self.b_w.data_ptr(), self.b_a.data_ptr(), self.b_lp.data_ptr(),
+            self.b_v.data_ptr(), self.act_out.data_ptr(), self._stream()))
+        self.counter += 1
+        return logits, value
 
-    def _finish(self, rows):
-        """do_episode's tail for the finished instances `rows` (device int64)."""
-        n = int(rows.numel())
-        if n == 0:
-            return
-        lens = self.t.index_select(0, rows)
-        T = int(lens.max())
-        ret = torch.zeros(n, self.L, dtype=torch.float32, device=self.device)
-        rows32, lens32 = rows.to(torch.int32), lens.to(torch.int32)
-        N.check(N.load().mz_discounted_returns(
-            self.b_r.data_ptr(), self.L, rows32.data_ptr(), lens32.data_ptr(), n, float(self.gamma),
-            ret.data_ptr(), self.L, torch.cuda.current_stream(self.device).cuda_stream))
-        ret = ret[:, :T]
-        mask = torch.arange(T, device=self.device)[None, :] < lens[:, None]
-        cnt = lens.to(torch.float32)[:, None]
+    def _scan_finish(self, reward64=None, terminated=None, truncated=None):
+        """The step's outcome (default: the env's output tensors) -> records, finished episodes
+        -> pool."""
+        env, B, L, st = self.env, self.env.num_envs, self.L, self._stream()
+        r64 = env.reward64 if reward64 is None else reward64
+        term = env.terminated if terminated is None else terminated
+        trunc = env.truncated if truncated is None else truncated
+        N.check(self.lib.mz_ppo_scan(
+            r64.data_ptr(), term.data_ptr(), trunc.data_ptr(), B, L,
+            self.t.data_ptr(), self.b_r.data_ptr(), self.fin_id.data_ptr(), self.fin_off.data_ptr(),
+            self.fin_len.data_ptr(), self.fin_count.data_ptr(), self.pool_fill.data_ptr(),
+            self.pool_total.data_ptr(), self.stats.data_ptr(), st))
+        N.check(self.lib.mz_ppo_finish(
+            self.b_r.data_ptr(), self.b_s6.data_ptr(), self.b_w.data_ptr(), self.b_a.data_ptr(),
+            self.b_lp.data_ptr(), self.b_v.data_ptr(), B, L, self.fin_id.data_ptr(),
+            self.fin_off.data_ptr(), self.fin_len.data_ptr(), self.fin_count.data_ptr(),
+            float(self.gamma), self.cap, self.p_s6.data_ptr(), self.p_w.data_ptr(),
+            self.p_a.data_ptr(), self.p_lp.data_ptr(), self.p_adv.data_ptr(),
+            self.p_ret.data_ptr(), st))
 
-        def norm(x, eps):  # (x - mean) / (std + eps), unbiased std per episode (torch.std)
-            m = (x * mask).sum(1, keepdim=True) / cnt
-            var = (((x - m) * mask) ** 2).sum(1, keepdim=True) / (cnt - 1)
-            return (x - m) / (var.sqrt() + eps)
-        ret = norm(ret, 0.0)
-        val = self.b_v.index_select(0, rows)[:, :T]
-        adv = norm(ret - val, 1e-8)
-        sel = mask.flatten()
-        ri = rows[:, None].expand(n, T).flatten()[sel]
-        ti = torch.arange(T, device=self.device)[None, :].expand(n, T).flatten()[sel]
-        chunk = (self.b_s6[ri, ti], self.b_w[ri, ti], self.b_a[ri, ti], self.b_lp[ri, ti],
-                 adv.flatten()[sel], ret.flatten()[sel])
-        self.pool.append(chunk)
-        self.pool_n += int(sel.sum())
-
-    def _ready(self):
-        """All ranks update together, each on exactly pool_size rows (equal collective counts)."""
-        n = torch.tensor([self.pool_n], dtype=torch.int64, device=self.device)
+    def _due(self):
+        """True when the pool held >= pool_size rows after the PREVIOUS vector step (the host copy
+        of the appended total lands while this step runs; it only grows, so a late look never
+        overshoots). Then issues this step's copy (MIN over the ranks with an all-reduce, so all
+        ranks decide alike)."""
+        due = False
+        if self._total_ev is not None:
+            self._total_ev.synchronize()
+            due = int(self._total_host[0]) - self.consumed >= self.pool_size
+        src = self.pool_total
         if self.allreduce is not None:
             import torch.distributed as dist
-            dist.all_reduce(n, op=dist.ReduceOp.MIN)
-        return int(n.item()) >= self.pool_size
+            src = self.pool_total.clone()
+            dist.all_reduce(src, op=dist.ReduceOp.MIN)
+        self._total_host.copy_(src, non_blocking=True)
+        if self._total_ev is None:
+            self._total_ev = torch.cuda.Event()
+        self._total_ev.record()
+        return due
 
     def _update(self, frac):
-        cat = [torch.cat(x) for x in zip(*self.pool)]
+        fill = int(self.pool_fill.item())  # one synchronisation per update
+        if fill > self.cap:
+            raise RuntimeError(f"PPO pool overflow: {fill} rows > capacity {self.cap} "
+                               "(raise pool_capacity)")
         P = self.pool_size
-        rest = [x[P:] for x in cat]
-        self.pool = [tuple(rest)] if rest[0].shape[0] else []
-        self.pool_n = int(rest[0].shape[0])
-        s6, w, a, lp, adv, ret = (x[:P] for x in cat)
-        win = w if self.bit_stem else self.env.expand_window(w)  # packed bits -> HIP stem
-        coef = 1e-2 - (1e-2 - 5e-4) * frac  # ppo_trainer.py:73
-        keep = (adv == adv) & (ret == ret)  # a 1-step episode has an undefined std (NaN): drop
-        rows = torch.nonzero(keep).flatten()
-        n_keep = torch.tensor([rows.numel()], dtype=torch.int64, device=self.device)
+        k = torch.tensor([fill // P], dtype=torch.int64, device=self.device)
         if self.allreduce is not None:
-            # every rank must run the same minibatch schedule (same collective count and the
-            # same graph-replay / eager split): all keep the smallest kept count
             import torch.distributed as dist
-            dist.all_reduce(n_keep, op=dist.ReduceOp.MIN)
-        n_keep = int(n_keep.item())
-        if n_keep < P:
-            rows = rows[:n_keep]
-            s6, win, a, lp, adv, ret = (x.index_select(0, rows) for x in (s6, win, a, lp, adv, ret))
-        optimize_model(self.net, self.opt, (s6, win), a[:, None], lp[:, None], adv, ret, coef,
-                       self.batch_size, self.ppo_steps, allreduce=self.allreduce, graph=self.graph)
-        if self.fused is not None:
-            self.fused.invalidate()  # graph replays leave the params' _version as is
-        self.updates += 1
+            dist.all_reduce(k, op=dist.ReduceOp.MIN)
+        k = int(k.item())
+        coef = 1e-2 - (1e-2 - 5e-4) * frac  # ppo_trainer.py:73
+        for j in range(k):
+            self.rows_trained += pool_update(self.net, self.opt, self._cols(j * P, (j + 1) * P),
+                                             coef, self.batch_size, self.ppo_steps,
+                                             allreduce=self.allreduce, graph=self.graph)
+            self.updates += 1
+        rest = fill - k * P
+        if k and rest:
+            for col in self._cols(0, self.cap):
+                col[:rest].copy_(col[k * P:fill].clone() if rest > k * P else col[k * P:fill])
+        self.pool_fill.fill_(rest)
+        self.consumed += k * P
 
     def vector_step(self, frac=0.0):
         env = self.env
-        a, lp, v = self._act()
-        t = self.t
-        self.b_s6[self.ar, t] = env.obs6
-        self.b_w[self.ar, t] = env.window_bits
-        self.b_a[self.ar, t] = a
-        self.b_lp[self.ar, t] = lp
-        self.b_v[self.ar, t] = v
-        env.step(a.to(torch.int32))
-        self.b_r[self.ar, t] = env.reward64
-        self.t += 1
-        term = env.terminated.bool()
-        done = term | env.truncated.bool()
-        rows = torch.nonzero(done).flatten()
-        self._finish(rows)
-        self.t.masked_fill_(done, 0)
-        self.episodes += int(rows.numel())
-        self.wins += int(term.sum())
+        self._act()
+        env.step(self.act_out)
+        self._scan_finish()
         env.reset_done(regen_won=True)
-        if self._ready():
+        if self._due():
             self._update(frac)
 
     def train(self, vector_steps, log_every=0, log=print):
@@ -189,8 +235,6 @@ class VectorPPOTrainer:
 
     @torch.no_grad()
     def greedy(self, obs6, window, bits=None):
-        if bits is not None and self.fused is not None:
-            logits, _ = self.fused(obs6, bits)
-        else:
-            logits, _ = self.net((obs6, window))
-        return torch.argmax(F.softmax(logits.float(), dim=-1), dim=-1)
+        """PPOAgent.evaluate's action (ppo_agent.py:239-252): argmax of softmax(logits), f32."""
+        logits, _ = self.net((obs6, bits if bits is not None else window))
+        return torch.argmax(F.softmax(logits, dim=-1), dim=-1)

@@ -115,6 +115,12 @@ class VectorOffPolicyTrainer:
         return secs
 
     def _train(self, vector_steps, log_every, log, t0):
+        # the next step's epsilon and its issued greedy-row list are recomputed on entry: the
+        # caller may have changed steps_done (a reload, a reset) since the last train() call
+        self._eps = None
+        rows = getattr(self.learner, "_rows", None)
+        if rows is not None:
+            rows._issued = None
         for k in range(vector_steps):
             loss = self.vector_step()
             if log_every and (k + 1) % log_every == 0:

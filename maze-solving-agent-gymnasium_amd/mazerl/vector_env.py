@@ -201,8 +201,15 @@ class VectorMazeEnv:
             self.algos_in_use = set(ALGOS.values())
 
     # ---------------------------------------------------------------------------------------
+    def _host_sync(self):
+        """host_scalars: the scalar outputs are CPU tensors over mapped memory the kernels write
+        asynchronously — wait for the launch before handing them back."""
+        if self._host is not None:
+            torch.cuda.current_stream(self.device).synchronize()
+
     def reset(self):
         N.check(self.lib.mz_reset_all(self._h, N.C.byref(self._out), self._stream()))
+        self._host_sync()
         return self.obs(), {}
 
     def reset_list(self, idx, count=None, regen_won=False, seed=None):
@@ -217,6 +224,7 @@ class VectorMazeEnv:
                                        self._stream()))
         if count is not None and count.data_ptr() == self.done_count.data_ptr():
             self._count_zero = True  # the reset kernel consumed it
+        self._host_sync()
 
     def reset_done(self, regen_won=False, seed=None):
         """Auto-reset every instance whose last step ended terminated|truncated (flag scan, no
@@ -230,6 +238,7 @@ class VectorMazeEnv:
                                        self._stream()))
         if regen_won and self._bank is not None:
             self._bank_tick()
+        self._host_sync()
 
     # ---------------------------------------------------------------------------------------
     # Maze bank: winners' new mazes are generated ahead of time, in bulk, on a side stream.
@@ -319,6 +328,7 @@ class VectorMazeEnv:
         N.check(self.lib.mz_step_ex(self._h, self._dev_ptr(a), N.C.byref(self._out), flags,
                                     self._stream()))
         self._count_zero = False
+        self._host_sync()
         return self.obs(), self.reward, self.truncated, self.terminated, {}
 
     def step_act(self, eps=1.0, greedy=None, seed=0, counter=0, actions_out=None, autoreset=False):
@@ -336,6 +346,7 @@ class VectorMazeEnv:
                                      counter & 0xFFFFFFFFFFFFFFFF, out_p,
                                      N.C.byref(self._out), flags, self._stream()))
         self._count_zero = False
+        self._host_sync()
         return self.obs(), self.reward, self.truncated, self.terminated, {}
 
     def obs(self):
@@ -361,6 +372,8 @@ class VectorMazeEnv:
         N.check(self.lib.mz_act(self._h, _ptr(eps_t), float(eps) if eps_t is None else 0.0,
                                 _ptr(g), seed & 0xFFFFFFFFFFFFFFFF, counter & 0xFFFFFFFFFFFFFFFF,
                                 self._dev_ptr(out), self._stream()))
+        if out is self.actions:
+            self._host_sync()
         return out
 
     def expand_window(self, bits, out=None):

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Where a config-5 PPO vector step goes (synchronised phase timers; not the production path):
-act (fused actor-critic forward + sampling), buffer writes, env step, episode finishing,
+act (f32 actor-critic forward + draw + record), env step, episode finishing into the pool,
 auto-reset (+ regeneration of winners), and the update when the pool is full."""
 import collections
 import json
@@ -33,30 +33,15 @@ def main(B=4096, steps=300):
 
     t = time.perf_counter()
     for k in range(steps):
-        a, lp, v = tr._act()
+        tr._act()  # f32 forward + mz_ppo_act (draw + record)
         t = tick("act", t)
-        tt = tr.t
-        tr.b_s6[tr.ar, tt] = env.obs6
-        tr.b_w[tr.ar, tt] = env.window_bits
-        tr.b_a[tr.ar, tt] = a
-        tr.b_lp[tr.ar, tt] = lp
-        tr.b_v[tr.ar, tt] = v
-        t = tick("buffers", t)
-        env.step(a.to(torch.int32))
-        tr.b_r[tr.ar, tt] = env.reward64
-        tr.t += 1
+        env.step(tr.act_out)
         t = tick("env_step", t)
-        term = env.terminated.bool()
-        done = term | env.truncated.bool()
-        rows = torch.nonzero(done).flatten()
-        tr._finish(rows)
-        tr.t.masked_fill_(done, 0)
-        tr.episodes += int(rows.numel())
-        tr.wins += int(term.sum())
+        tr._scan_finish()  # mz_ppo_scan + mz_ppo_finish (returns / advantages -> pool)
         t = tick("finish", t)
         env.reset_done(regen_won=True)
         t = tick("reset_regen", t)
-        if tr._ready():
+        if tr._due():
             tr._update(k / steps)
         t = tick("update", t)
     tot = sum(acc.values())

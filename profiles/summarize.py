@@ -2,9 +2,11 @@
 """Turn rocprofv3 outputs under gpurun_out/ into the committed summaries under profiles/.
 
   python profiles/summarize.py <round_tag> <kernel-trace dir> <FETCH_SIZE dir> <WRITE_SIZE dir> \
-      --envs 65536 --dim 81
+      --envs 65536 --dim 81 --mode window|bits
 
-Writes profiles/<tag>_kernel_stats.csv (copy of rocprofv3 --stats) and profiles/pmc_k_step.json:
+Writes profiles/<tag>_kernel_stats.csv (copy of rocprofv3 --stats) and the <mode> record of
+profiles/pmc_k_step.json (stamped with the hash of k_step's sources: bench.py uses a record only
+while the sources are unchanged):
 per-launch HBM bytes of k_step = (2 x FETCH_SIZE + WRITE_SIZE) x 1024, the gfx950 correction of
 MI355X_MICROARCH.md §HBM (FETCH_SIZE reads half of the bytes of wide streaming reads; the
 gathers of k_step are uncalibrated, so the doubled figure is an upper bound on its read side).
@@ -16,8 +18,10 @@ import json
 import os
 import shutil
 import statistics
+import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
 
 
 def counter(d, name, kernel_sub):
@@ -36,14 +40,17 @@ def main():
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--dim", type=int, default=81)
     ap.add_argument("--kernel", default="k_step<16, false, true, true, true>")
+    ap.add_argument("--mode", default="window", choices=["window", "bits"])
     a = ap.parse_args()
+    from bench import kstep_source_sha
     stats = glob.glob(os.path.join(a.kt, "**", "*kernel_stats.csv"), recursive=True)[0]
     shutil.copy(stats, os.path.join(HERE, f"{a.tag}_kernel_stats.csv"))
     avg_ns = [float(r["AverageNs"]) for r in csv.DictReader(open(stats)) if a.kernel in r["Name"]][0]
     fetch_kb, nf = counter(a.fetch, "FETCH_SIZE", a.kernel)
     write_kb, nw = counter(a.write, "WRITE_SIZE", a.kernel)
     out = {
-        "kernel": a.kernel, "envs": a.envs, "dim": a.dim,
+        "kernel": a.kernel, "envs": a.envs, "dim": a.dim, "mode": a.mode, "tag": a.tag,
+        "source_sha": kstep_source_sha(),
         "rocprof_avg_ns": avg_ns,
         "FETCH_SIZE_kb_per_launch": fetch_kb, "WRITE_SIZE_kb_per_launch": write_kb,
         "launches_sampled": [nf, nw],
@@ -52,8 +59,16 @@ def main():
         "note": "traffic = (2*FETCH_SIZE + WRITE_SIZE)*1024 per MI355X_MICROARCH.md §HBM; "
                 "separate --pmc passes for FETCH_SIZE and WRITE_SIZE",
     }
-    with open(os.path.join(HERE, "pmc_k_step.json"), "w") as f:
-        json.dump(out, f, indent=1)
+    path = os.path.join(HERE, "pmc_k_step.json")
+    allrec = {}
+    if os.path.exists(path):
+        with open(path) as f:
+            allrec = json.load(f)
+        if "kernel" in allrec:  # the round-2 single-record layout
+            allrec = {}
+    allrec[a.mode] = out
+    with open(path, "w") as f:
+        json.dump(allrec, f, indent=1)
     print(json.dumps(out, indent=1))
 
 

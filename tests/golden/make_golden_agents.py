@@ -34,6 +34,41 @@ def ppo_inputs():
     return s6, w, a, lp, adv, ret, vals
 
 
+# a pool of whole episodes for the vectorised trainer's on-device finishing (mz_ppo_scan /
+# mz_ppo_finish): lengths incl. 1-step episodes (NaN returns in the reference: torch.std of one
+# element) and one longer than the kernel's 2,048-reward LDS chunk
+POOL_LENS = [1, 2, 3, 7, 1, 40, 12, 2, 150, 5, 2600, 9]
+
+
+def pool_episodes():
+    """Rewards from the env's reward set (base_maze_env.py:183-208: new cell 0.45 / -0.55 /
+    toroidal -0.05, revisit -(1 - exp(-0.2 k)), invalid move -(1 - exp(-0.15 k)), win 1,
+    truncation -1) and critic values per episode."""
+    import math
+    rng = np.random.default_rng(2024)
+    eps = []
+    for n in POOL_LENS:
+        r = []
+        for t in range(n):
+            c = rng.integers(0, 6)
+            if c == 0:
+                r.append(0.45)
+            elif c == 1:
+                r.append(-0.55)
+            elif c == 2:
+                r.append(-0.05)
+            elif c == 3:
+                r.append(0.0 - (1 - math.exp(-0.2 * int(rng.integers(1, 300)))))
+            elif c == 4:
+                r.append(0.0 - (1 - math.exp(-0.15 * int(rng.integers(1, 300)))))
+            else:
+                r.append(0.45)
+        r[-1] = 1 if rng.random() < 0.5 else -1  # the last step: a win or a truncation
+        v = rng.standard_normal(n).astype(np.float32)
+        eps.append((r, v))
+    return eps
+
+
 def main(ref="/root/reference"):
     sys.path.insert(0, HERE)
     import _refstubs
@@ -101,6 +136,19 @@ def main(ref="/root/reference"):
                          torch.from_numpy(ret), PPO_COEF)
     for k, p in sorted(net.named_parameters()):
         out[f"ppo.param.{k}"] = p.data.numpy().copy()
+    # per-episode returns / advantages of the pool episodes (do_episode's tail, :166-167)
+    rew, val, rets, advs = [], [], [], []
+    for r, v in pool_episodes():
+        R = P.calculate_returns(h, r)
+        A = P.calculate_advantages(h, R, torch.from_numpy(v))
+        rew.append(np.array(r, np.float64)); val.append(v)
+        rets.append(R.numpy().astype(np.float32)); advs.append(A.numpy().astype(np.float32))
+    out["ppo.pool.lens"] = np.array(POOL_LENS, np.int64)
+    out["ppo.pool.rewards"] = np.concatenate(rew)
+    out["ppo.pool.values"] = np.concatenate(val)
+    out["ppo.pool.returns"] = np.concatenate(rets)
+    out["ppo.pool.advantages"] = np.concatenate(advs)
+    out["ppo.pool.gamma"] = np.float64(h.gamma)
     np.savez_compressed(os.path.join(HERE, "agents.npz"), **out)
     print("q keys", len(keys), "ppo returns", out["ppo.returns"][:3])
 

@@ -68,3 +68,20 @@ def test_ppo_optimize_model_matches_reference(fx):
                    PPO_BATCH, PPO_STEPS)
     for k, p in sorted(net.named_parameters()):
         np.testing.assert_allclose(p.data.numpy(), fx[f"ppo.param.{k}"], rtol=1e-5, atol=1e-7, err_msg=k)
+
+
+def test_ppo_pool_episode_returns_advantages(fx):
+    """The pool fixture (per-episode calculate_returns / calculate_advantages of the reference,
+    ppo_agent.py:171-186, incl. 1-step episodes whose unbiased std is NaN) against this package's
+    CPU restatement, exactly — the fixture the GPU finishing kernel is checked against."""
+    from mazerl.agents.ppo import calculate_advantages, calculate_returns
+    lens = fx["ppo.pool.lens"]
+    off = np.concatenate([[0], np.cumsum(lens)])
+    for k, n in enumerate(lens):
+        sl = slice(off[k], off[k + 1])
+        R = calculate_returns([float(x) for x in fx["ppo.pool.rewards"][sl]],
+                              float(fx["ppo.pool.gamma"]))  # Python floats, as the reference
+        A = calculate_advantages(R, torch.from_numpy(fx["ppo.pool.values"][sl]))
+        np.testing.assert_array_equal(R.numpy(), fx["ppo.pool.returns"][sl])
+        np.testing.assert_array_equal(A.numpy(), fx["ppo.pool.advantages"][sl])
+        assert np.isnan(R.numpy()).all() == (n == 1)

@@ -79,3 +79,46 @@ def test_ddp_update_equals_single_process_union_batch():
         torch.testing.assert_close(r0[k], v, rtol=1e-5, atol=1e-7)
         torch.testing.assert_close(r1[k], v, rtol=1e-5, atol=1e-7)
     assert r0["stats"].tolist() == [3.0, 30.0] == r1["stats"].tolist()
+
+
+def _ppo_worker(rank, world, port, outdir):
+    """Config 5's update on two ranks whose pools hold different numbers of non-finite rows
+    (trainers/ppo_trainer.py pool_update): both keep the smaller kept count, run the same
+    minibatch schedule with the flat-bucket gradient all-reduce, and end with identical weights."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from mazerl.agents.ppo import ActorCriticNet, make_optimizer
+    from mazerl.distributed import GradAllReduce, broadcast_params, init_from_env
+    from mazerl.trainers.ppo_trainer import pool_update
+    init_from_env("gloo")
+    net = ActorCriticNet(3, 6, 4, 4, hidden_dim=16)
+    U.fill_params(net, 7 if rank == 0 else 8)
+    broadcast_params(net)
+    opt = make_optimizer(net, 3e-4, 1e-4)
+    g = torch.Generator().manual_seed(100 + rank)  # each rank its own pool
+    P = 40
+    s6 = torch.rand(P, 6, generator=g)
+    win = (torch.rand(P, 3, 15, 15, generator=g) < 0.5).float()
+    a = torch.randint(0, 4, (P,), generator=g)
+    lp = -torch.rand(P, generator=g)
+    adv, ret = torch.randn(P, generator=g), torch.randn(P, generator=g)
+    bad = [3, 17, 30] if rank == 0 else [0, 5, 6, 11, 22, 23, 39]  # NaN / inf rows
+    adv[bad[::2]] = float("nan")
+    ret[bad[1::2]] = float("inf")
+    kept = pool_update(net, opt, (s6, win, a, lp, adv, ret), 1e-2, 8, 2,
+                       allreduce=GradAllReduce())
+    torch.save({"kept": kept, **{k: v.clone() for k, v in net.state_dict().items()}},
+               os.path.join(outdir, f"p{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_ppo_pool_update_two_ranks_agree_on_rows_and_weights():
+    torch.set_num_threads(1)
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_ppo_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        r0 = torch.load(os.path.join(d, "p0.pt"), weights_only=True)
+        r1 = torch.load(os.path.join(d, "p1.pt"), weights_only=True)
+    assert r0.pop("kept") == r1.pop("kept") == 40 - 7  # the smaller kept count on both ranks
+    for k in r0:
+        assert torch.equal(r0[k], r1[k]), k  # same schedule, same averaged gradients

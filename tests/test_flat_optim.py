@@ -70,3 +70,39 @@ def test_flat_params_survive_state_dict_and_copy():
     fc = flatten_params(C)
     assert fc.data_ptr() != fa.data_ptr()
     assert all(torch.equal(x, y) for x, y in zip(C.parameters(), A.parameters()))
+
+
+def test_flat_adamw_step_counts_are_independent_and_graph_safe():
+    """The step count is a plain f32 [1] (include/mazerl.h mz_adamw_flat); the launch's
+    last-workgroup ticket is library-owned, one slot per counter. Two optimizers interleaved on
+    two streams, eagerly and as captured-graph replays, each advance their own count by exactly
+    one per step."""
+    from mazerl.agents.flat import FlatAdamW
+    from mazerl.agents.nets import QNet
+    torch.manual_seed(3)
+    A, B = QNet(variant="dqn").cuda(), QNet(variant="ddqn").cuda()
+    oa, ob = FlatAdamW(A, lr=1e-3), FlatAdamW(B, lr=1e-3)
+    assert oa._step_buf.numel() == 1 and ob._step_buf.numel() == 1
+    for p in list(A.parameters()) + list(B.parameters()):
+        p.grad = torch.randn_like(p) * 1e-3
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    for k in range(7):
+        with torch.cuda.stream(s1):
+            oa.step()
+        with torch.cuda.stream(s2):
+            ob.step()
+            ob.step()
+    torch.cuda.synchronize()
+    assert float(oa.step_t) == 7.0 and float(ob.step_t) == 14.0
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            oa.step()
+    torch.cuda.current_stream().wait_stream(s)
+    for _ in range(5):
+        g.replay()
+    ob.step()
+    torch.cuda.synchronize()
+    assert float(oa.step_t) == 12.0 and float(ob.step_t) == 15.0

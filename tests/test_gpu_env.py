@@ -488,3 +488,129 @@ def test_large_batch_fused_autoreset_every_lane_vs_oracle(mazerl, B):
             was_done[i] = o["terminated"] or o["truncated"]
     assert resets > 0
     env.close()
+
+
+def test_headline_config_every_lane_autoreset_vs_oracle(mazerl):
+    """The bench's kernel instantiation (k_step<16, euclidean, Enrich, fused act, autoreset) at
+    the headline config, 65,536 x 81x81 r-prim: every lane of 9 whole 16-instance groups — one
+    in each XCD's slice of the group map (mz_env.hip k_step: workgroup b steps group
+    (b & 7) * grid/8 + (b >> 3)) plus the last group — replayed through the oracle for 400 vector
+    steps, rewards as float64 ==, flags, positions, best dirs and f32 windows exactly. Actions:
+    epsilon-mixed best-dir following (eps 0.3: episodes end in wins across multi-strip windows);
+    two groups play loaded copies of their mazes with the start two cells from the goal
+    (max_steps 7) at eps 1.0, so truncation resets come often too. >= 100 resets must occur in
+    the sampled lanes, of both kinds."""
+    import pyoracle as O
+    B, dim, K = 65536, 81, 400
+    env = mazerl.VectorMazeEnv(B, dim, enrich=True, reward64=True, seed=0x5EED0000)
+    per_xcd = (B // 16) // 8
+    groups = [x * per_xcd + (61 * x) % per_xcd for x in range(8)] + [B // 16 - 1]
+    sample = [i for g in groups for i in range(16 * g, 16 * g + 16)]
+    short = [i for g in (groups[3], groups[8]) for i in range(16 * g, 16 * g + 16)]
+    grids, sg = [], []
+    for i in short:
+        g = env.grid(i)
+        q = env.query(i)
+        gr, gc = q["goal_r"], q["goal_c"]
+        for dr, dc in ((1, 0), (-1, 0), (0, 1), (0, -1)):
+            if 0 < gr + 2 * dr < dim - 1 and 0 < gc + 2 * dc < dim - 1 and g[gr + dr, gc + dc]:
+                sg.append((gr + 2 * dr, gc + 2 * dc, gr, gc))
+                break
+        grids.append(g)
+    env.load_mazes(np.stack(grids), np.array(sg), env_ids=short)
+    env.reset()
+    eps = torch.full((B,), 0.3, device="cuda")
+    eps[torch.tensor(short, device="cuda")] = 1.0
+    ors = {}
+    for i in sample:
+        q = env.query(i)
+        ors[i] = O.Env(env.grid(i), (q["start_r"], q["start_c"]), (q["goal_r"], q["goal_c"]), False, True)
+        ors[i].reset()
+        if i in short:
+            assert q["max_steps"] == ors[i].max_steps == 7
+    idx = torch.tensor(sample, device="cuda")
+    was_done = {i: False for i in sample}
+    short_set = set(short)
+    wins = truncs = resets = long_wins = 0
+    for k in range(K):
+        bd = env.best_dir.long()
+        dr, dc = -bd[:, 0], -bd[:, 1]
+        greedy = torch.where(dr == 1, 0, torch.where(dr == -1, 1, torch.where(dc == 1, 2, 3)))
+        env.step_act(eps=eps, greedy=greedy, seed=0xB16, counter=k, autoreset=True)
+        a = env.actions[idx].cpu().numpy()
+        r64 = env.reward64[idx].cpu().numpy()
+        te, tr = env.terminated[idx].cpu().numpy(), env.truncated[idx].cpu().numpy()
+        pos, bdir = env.pos[idx].cpu().numpy(), env.best_dir[idx].cpu().numpy()
+        win = env.window[idx].cpu().numpy()
+        bits = env.expand_window(env.window_bits[idx].contiguous()).cpu().numpy()
+        for j, i in enumerate(sample):
+            if was_done[i]:
+                assert a[j] == -1, (k, i)
+                o = ors[i].reset()
+                resets += 1
+            else:
+                assert 0 <= a[j] < 4, (k, i)
+                o = ors[i].step(int(a[j]))
+            assert r64[j] == o["reward"], (k, i)
+            assert bool(te[j]) == o["terminated"] and bool(tr[j]) == o["truncated"], (k, i)
+            assert tuple(pos[j]) == o["pos"] and tuple(bdir[j]) == o["best_dir"], (k, i)
+            np.testing.assert_array_equal(win[j], o["window"].astype(np.float32), err_msg=f"{k} {i}")
+            np.testing.assert_array_equal(bits[j], win[j])
+            wins += bool(te[j])
+            long_wins += bool(te[j]) and i not in short_set
+            truncs += bool(tr[j]) and not bool(te[j])
+            was_done[i] = o["terminated"] or o["truncated"]
+    assert resets >= 100 and wins >= 20 and truncs >= 20, (resets, wins, truncs)
+    assert long_wins >= 8, long_wins  # wins on the generated 81x81 mazes too (long paths)
+    env.close()
+
+
+@pytest.mark.parametrize("tor,dim", [(False, 21), (True, 17), (False, 81), (True, 29)])
+def test_act_draw_follows_reference_exploration_distribution(mazerl, tor, dim):
+    """The fused act's exploration draw (act_draw, csrc/mz_env.hip) against the reference's
+    np.random.choice(4, p=mask / mask.sum()) (dqn_agent.py:109-112) with the 0.25 weight on the
+    step back after >= 2 moves — on the torus on the transposed direction (Q6,
+    toroidal_maze_env.py:64-68); the masks themselves are pinned bit-exactly to the reference
+    by the traces (get_mask_direction(probs=True)). 4,096 instances in mid-episode states x 256
+    draws each, pooled per distinct mask row: chi-square p-value > 1e-6, zero-probability
+    directions never drawn. Then epsilon: with a greedy action the mask forbids, the greedy
+    fraction is binomial(1 - eps)."""
+    from scipy.stats import chi2, norm
+    B, K = 4096, 256
+    env = mazerl.VectorMazeEnv(B, dim, toroidal=tor, enrich=True, seed=99)
+    for k in range(12):  # most instances now have >= 2 moves: the 0.25 weight is live
+        env.step_act(eps=1.0, seed=5, counter=k)
+        env.reset_done()
+    m = env.direction_mask(True).clone()
+    assert int(((m == 0.25).sum(1) == 1).sum()) > B // 4
+    assert bool(((m == 0) | (m == 0.25) | (m == 1)).all())
+    counts = torch.zeros(B, 4, dtype=torch.int64, device="cuda")
+    ar = torch.arange(B, device="cuda")
+    for c in range(K):
+        a = env.act(eps=1.0, seed=123, counter=c).long()
+        counts[ar, a] += 1
+    key = (m * 4).round().long()
+    key = key[:, 0] + 5 * key[:, 1] + 25 * key[:, 2] + 125 * key[:, 3]
+    stat, dof = 0.0, 0
+    for kv in torch.unique(key).tolist():
+        sel = key == kv
+        row = m[sel][0].double()
+        p = (row / row.sum()).cpu().numpy()
+        n = counts[sel].sum(0).cpu().numpy().astype(np.float64)
+        live = p > 0
+        assert n[~live].sum() == 0, (row, n)
+        exp = p[live] * n.sum()
+        stat += float(((n[live] - exp) ** 2 / exp).sum())
+        dof += int(live.sum()) - 1
+    assert dof > 0 and chi2.sf(stat, dof) > 1e-6, (stat, dof)
+    # epsilon-greedy: sample < eps explores, else the greedy action (dqn_agent.py:104-116)
+    blocked = (m == 0).any(1)
+    g = torch.argmin(m, 1)  # a direction the exploration never draws where blocked
+    eps, hits, tot = 0.37, 0, 0
+    for c in range(64):
+        a = env.act(eps=eps, greedy=g, seed=321, counter=c).long()
+        hits += int((a[blocked] == g[blocked]).sum())
+        tot += int(blocked.sum())
+    z = (hits - tot * (1 - eps)) / np.sqrt(tot * eps * (1 - eps))
+    assert 2 * norm.sf(abs(z)) > 1e-6, (hits, tot)
+    env.close()

@@ -191,3 +191,40 @@ def test_fused_q_loss_matches_torch_loss(variant):
     torch.testing.assert_close(l0, l1, rtol=1e-6, atol=0)
     for x, y in zip(g0, g1):
         torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("ddqn", [True, False])
+def test_fused_q_loss_propagates_nan_like_torch(ddqn):
+    """mz_q_loss on rows holding NaN: torch's argmax takes the first NaN as the maximum
+    (DDQN's target column) and max(1)[0] propagates NaN (DQN), so the per-row diff — and the
+    loss — are NaN exactly where the torch expression's are (a diverging net must not report a
+    finite loss)."""
+    from mazerl.agents.dqn import _QLossFn
+    nan = float("nan")
+    q = torch.tensor([[1., 2., 3., 4.], [0.5, nan, 0.1, 0.2], [1., 1., 1., 1.], [2., 0., 0., 0.]],
+                     device=DEV)
+    qn = torch.tensor([[0., nan, 5., nan], [1., 2., 3., 4.], [nan, 0., 0., 0.], [3., 1., 9., 2.]],
+                      device=DEV)
+    qt = torch.tensor([[1., nan, 3., 4.], [1., nan, 0., 0.], [5., 6., 7., 8.], [1., 2., 3., nan]],
+                      device=DEV)
+    a = torch.tensor([0, 2, 1, 3], device=DEV)
+    r = torch.tensor([0.5, -0.05, 1.0, 0.45], device=DEV)
+    diff_ref = []
+    for i in range(4):
+        v = qt[i, torch.argmax(qn[i])] if ddqn else qt[i].max()
+        diff_ref.append(q[i, a[i]] - (v * 0.7 + r[i]))
+    diff_ref = torch.stack(diff_ref)
+    loss = _QLossFn.apply(q, qn if ddqn else None, qt, a, r, 0.7, 4)
+    torch.cuda.synchronize()
+    assert torch.isnan(loss) and torch.isnan((diff_ref ** 2).mean())
+    # row by row: the kernel's diff has NaN in the rows torch's has
+    from mazerl import _native as N
+    diff = torch.empty(4, device=DEV)
+    out = torch.empty((), device=DEV)
+    N.check(N.load().mz_q_loss(q.data_ptr(), 4, qn.data_ptr() if ddqn else None, 4 if ddqn else 0,
+                               qt.data_ptr(), 4, a.data_ptr(), r.data_ptr(), 0.7, 4, out.data_ptr(),
+                               diff.data_ptr(), torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    assert torch.equal(torch.isnan(diff), torch.isnan(diff_ref)), (diff, diff_ref)
+    fin = ~torch.isnan(diff_ref)
+    assert torch.equal(diff[fin], diff_ref[fin])
