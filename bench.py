@@ -95,6 +95,9 @@ def parse():
     ap.add_argument("--fused-bookkeeping", type=int, default=1,
                     help="1: per-step trainer bookkeeping + replay push as HIP launches "
                          "(mz_trainer_tick, mz_replay_push); 0: torch ops")
+    ap.add_argument("--acting", default="x3", choices=["x3", "bf16"],
+                    help="acting head: x3 = f32-accurate bf16x3 MFMA (QAct, sized on the device); "
+                         "bf16 = bf16 stem + hipBLASLt bf16 GEMMs (FusedQ, count read on the host)")
     ap.add_argument("--overlap", type=int, default=1,
                     help="1: learner updates on a side HIP stream, overlapped with acting + env "
                          "step (acting weights one update behind); 0: sequential")
@@ -121,7 +124,7 @@ def win_rate(a, dev, rank=0, world=1):
                          eps_decay=decay, gamma=0.7, batch_size=a.batch, capacity=2_000_000,
                          updates_per_step=a.updates_per_step, target_every=a.target_every,
                          allreduce=GradAllReduce() if world > 1 else None, overlap=bool(a.overlap),
-                         greedy_rows=bool(a.greedy_rows))
+                         greedy_rows=bool(a.greedy_rows), acting=a.acting)
     if world > 1:
         broadcast_params(L.source)
         L.target.load_state_dict(L.source.state_dict())
@@ -155,6 +158,7 @@ def win_rate(a, dev, rank=0, world=1):
                                 if L.overlap else "sequential",
             "acting_rows": "greedy rows only (epsilon draw first, dqn_agent.py:104-116)"
                            if L.greedy_rows else "every instance",
+            "acting_head": a.acting,
             "grad_allreduce": (f"{dist.get_backend()} ({'RCCL' if dist.get_backend() == 'nccl' else 'rehearsal'}), "
                                "one 8.56 MB fp32 bucket per update between two graph replays")
                               if world > 1 else None,
@@ -198,22 +202,39 @@ def acting_agreement(L, n=65536):
 BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X bf16 MFMA, dense (MI355X_MICROARCH.md)
 
 
+# issued MFMA FLOP per row of QAct (csrc/mz_qact.hip): conv 49 chunks x 32 tiles x 4 MFMAs x 16,384
+# per 128-row workgroup x 4 output tiles, fc1 3 x 2 x 1,600 x 1,024, fc2 3 x 2 x 1,024 x 512
+QACT_ISSUED_FLOP = 49 * 32 * 4 * 16384 * 4 / 128 + 3 * 2 * 1600 * 1024 + 3 * 2 * 1024 * 512
+REF_FWD_FLOP = 4665024  # the reference net's forward per sample
+
+
 def q_head(dev, n, iters=50):
     """The acting Q-network forward of the DDQN learner on n instances (north_star: MFMA for the
-    dense Q-head GEMMs): fused conv stem from window bits (k_qfront, bf16 MFMA) + fc1 1574->1024,
-    fc2 1024->512, fc3 512->4 bf16 GEMMs (hipBLASLt). HIP events on the launch stream; FLOPs are
-    algorithmic (conv 388,800 / sample, fc1 K = 1,574)."""
+    dense Q-head GEMMs), both heads, HIP events on the launch stream:
+      x3   (the trainer's head) QAct: conv stem inside fc1's K loop + fc2 + fc3 + argmax, every
+           GEMM operand split into bf16 hi + lo (three MFMAs per tile) — f32-accurate; all rows,
+           and the greedy-row list at the training leg's typical size (0.43 n rows, count on
+           the device);
+      bf16 FusedQ: bf16 stem (k_qfront, features to HBM) + hipBLASLt bf16 GEMMs.
+    algorithmic TFLOP/s = the reference's 4,665,024 FLOP per row / time; issued = the MFMA FLOP
+    the kernels execute (QAct: x3 products + the conv recomputed per output tile)."""
     import torch
     import torch.nn.functional as F
     from mazerl.agents.fused import FusedQ
     from mazerl.agents.nets import QNet
+    from mazerl.agents.qact import QAct
     torch.manual_seed(0)
     net = QNet(variant="ddqn").to(dev)
     fq = FusedQ(net, seed=1)
+    qa = QAct(net, seed=1)
     g = torch.Generator(device=dev).manual_seed(0)
     bits = torch.randint(0, 2**31 - 1, (n, 22), generator=g, device=dev, dtype=torch.int32)
     obs6 = torch.rand(n, 6, generator=g, device=dev)
     st = torch.cuda.current_stream(dev)
+    m = int(0.43 * n)
+    rows = torch.randperm(n, generator=g, device=dev)[:m].to(torch.int32).contiguous()
+    count = torch.tensor([m], dtype=torch.int32, device=dev)
+    greedy = torch.zeros(n, dtype=torch.int64, device=dev)
 
     def timed(fn):
         for _ in range(5):
@@ -227,18 +248,30 @@ def q_head(dev, n, iters=50):
         return e0.elapsed_time(e1) / iters
 
     with torch.no_grad():
+        t_x3 = timed(lambda: qa.greedy(obs6, bits, out=greedy))
+        t_x3r = timed(lambda: qa.rows_greedy(obs6, bits, rows, count, greedy))
         t_all = timed(lambda: fq(obs6, bits))
         feat = fq.stem(obs6, bits)
         w0, b0 = fq.head._w[0]
         t_fc1 = timed(lambda: F.linear(feat, w0, b0))
     f_fc1 = 2.0 * n * 1574 * 1024
     f_all = n * (388800 + 2.0 * (1574 * 1024 + 1024 * 512 + 512 * 4))
-    return {"instances": n, "forward_ms": t_all, "fc1_ms": t_fc1,
-            "fc1_tflops": f_fc1 / (t_fc1 * 1e-3) / 1e12,
-            "fc1_mfma_frac": f_fc1 / (t_fc1 * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS,
-            "forward_tflops": f_all / (t_all * 1e-3) / 1e12,
-            "forward_mfma_frac": f_all / (t_all * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS,
-            "dtype": "bf16 (f32 accumulate)", "peak_tflops": BF16_DENSE_PEAK_TFLOPS}
+
+    def x3(t, rows_):
+        return {"rows": rows_, "ms": t, "alg_tflops": rows_ * REF_FWD_FLOP / (t * 1e-3) / 1e12,
+                "issued_tflops": rows_ * QACT_ISSUED_FLOP / (t * 1e-3) / 1e12,
+                "mfma_frac": rows_ * QACT_ISSUED_FLOP / (t * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS}
+    return {"instances": n,
+            "x3": {"all_rows": x3(t_x3, n), "greedy_rows": x3(t_x3r, m),
+                   "issued_flop_per_row": QACT_ISSUED_FLOP,
+                   "dtype": "bf16x3 (hi*hi + hi*lo + lo*hi, f32 accumulate)"},
+            "bf16": {"forward_ms": t_all, "fc1_ms": t_fc1,
+                     "fc1_tflops": f_fc1 / (t_fc1 * 1e-3) / 1e12,
+                     "fc1_mfma_frac": f_fc1 / (t_fc1 * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS,
+                     "forward_tflops": f_all / (t_all * 1e-3) / 1e12,
+                     "forward_mfma_frac": f_all / (t_all * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS,
+                     "dtype": "bf16 (f32 accumulate)"},
+            "peak_tflops": BF16_DENSE_PEAK_TFLOPS}
 
 
 def host_threads():

@@ -486,6 +486,32 @@ int mz_ppo_finish(const double* rec_r_dev, const float* rec_s6_dev, const uint32
                   int64_t capacity, float* pool_s6_dev, uint32_t* pool_w_dev, int64_t* pool_a_dev,
                   float* pool_lp_dev, float* pool_adv_dev, float* pool_ret_dev, void* stream);
 
+/* ---- The DQN / DDQN acting forward, f32-accurate on the bf16 MFMA (mz_qact.hip) -------------
+ * Replaces, per acting row, source_net(state).max(1)[1] (dqn_agent.py:113-116; the nets of
+ * dqn_agent.py:19-57 / ddqn_agent.py:18-52 at the reference's sizes: Conv2d(3, 32, 3, p 1),
+ * 1,574 -> 1,024 -> 512 -> 4). Every GEMM operand is split into bf16 hi + lo and each product
+ * summed as hi*hi + hi*lo + lo*hi in f32 (~2^-16 relative): the f32 argmax at bf16-MFMA speed. */
+
+/* fc1's weight [1024][1574] (torch layout) and fc2's [512][1024] f32 -> the hi / lo bf16 images
+ * mz_qact reads, in MFMA fragment order (a wave's operand for one K chunk contiguous): w1 1024 x 1600
+ * elements (features in the kernel's order, zero pad), w2 512 x 1024 (16-B aligned). */
+int mz_qact_prepare(const float* fc1_w_dev, const float* fc2_w_dev, uint16_t* w1_hi_dev,
+                    uint16_t* w1_lo_dev, uint16_t* w2_hi_dev, uint16_t* w2_lo_dev, void* stream);
+
+/* Q values and greedy actions of min(n, *count_dev) rows (count_dev NULL: n): row i is instance
+ * rows_dev[i] (rows_dev NULL: instance i) of bits_dev [B][22] / obs6_dev [B][6]. Conv weight
+ * [32][3][3][3] / bias, fc1 bias [1024], fc2 bias [512], fc3 weight [4][512] / bias [4] f32;
+ * relu: 1 for DDQN's second activation (ReLU), 0 for DQN's LeakyReLU; drop_p > 0: DDQN's
+ * train-mode Dropout after the conv activation (counter hash of seed / counter, row, feature).
+ * h1_dev: workspace [n][1024] f32. Outputs: greedy_dev[instance] = first argmax (int64; NaN as
+ * torch.argmax), q_out_dev [n][4] f32 (either may be NULL). No host synchronisation. */
+int mz_qact(const uint32_t* bits_dev, const float* obs6_dev, const int32_t* rows_dev,
+            const int32_t* count_dev, int32_t n, const float* conv_w_dev, const float* conv_b_dev,
+            const uint16_t* w1_hi_dev, const uint16_t* w1_lo_dev, const float* b1_dev,
+            const uint16_t* w2_hi_dev, const uint16_t* w2_lo_dev, const float* b2_dev,
+            const float* w3_dev, const float* b3_dev, int32_t relu, float drop_p, uint64_t seed,
+            uint64_t counter, float* h1_dev, int64_t* greedy_dev, float* q_out_dev, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

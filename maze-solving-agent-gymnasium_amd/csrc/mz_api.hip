@@ -901,3 +901,40 @@ int mz_ppo_finish(const double* rec_r_dev, const float* rec_s6_dev, const uint32
   return MZ_OK;
 }
 
+int mz_qact_prepare(const float* fc1_w_dev, const float* fc2_w_dev, uint16_t* w1_hi_dev,
+                    uint16_t* w1_lo_dev, uint16_t* w2_hi_dev, uint16_t* w2_lo_dev, void* stream) {
+  if (!fc1_w_dev || !fc2_w_dev || !w1_hi_dev || !w1_lo_dev || !w2_hi_dev || !w2_lo_dev)
+    return fail(MZ_EINVAL, "bad arguments");
+  StreamGuard g(stream);
+  MZ_HIP(mz_launch_qact_prepare(fc1_w_dev, fc2_w_dev, w1_hi_dev, w1_lo_dev, w2_hi_dev, w2_lo_dev,
+                                static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
+int mz_qact(const uint32_t* bits_dev, const float* obs6_dev, const int32_t* rows_dev,
+            const int32_t* count_dev, int32_t n, const float* conv_w_dev, const float* conv_b_dev,
+            const uint16_t* w1_hi_dev, const uint16_t* w1_lo_dev, const float* b1_dev,
+            const uint16_t* w2_hi_dev, const uint16_t* w2_lo_dev, const float* b2_dev,
+            const float* w3_dev, const float* b3_dev, int32_t relu, float drop_p, uint64_t seed,
+            uint64_t counter, float* h1_dev, int64_t* greedy_dev, float* q_out_dev, void* stream) {
+  if (!bits_dev || !obs6_dev || !conv_w_dev || !conv_b_dev || !w1_hi_dev || !w1_lo_dev ||
+      !b1_dev || !w2_hi_dev || !w2_lo_dev || !b2_dev || !w3_dev || !b3_dev || !h1_dev || n < 0 ||
+      (!greedy_dev && !q_out_dev))
+    return fail(MZ_EINVAL, "bad arguments");
+  if (count_dev && !rows_dev) return fail(MZ_EINVAL, "a device count needs a row list");
+  if (!(drop_p >= 0.0f && drop_p < 1.0f)) return fail(MZ_EINVAL, "dropout p %g", (double)drop_p);
+  const uintptr_t al = reinterpret_cast<uintptr_t>(w1_hi_dev) | reinterpret_cast<uintptr_t>(w1_lo_dev) |
+                       reinterpret_cast<uintptr_t>(w2_hi_dev) | reinterpret_cast<uintptr_t>(w2_lo_dev) |
+                       reinterpret_cast<uintptr_t>(h1_dev) | reinterpret_cast<uintptr_t>(q_out_dev);
+  if (al & 15) return fail(MZ_EALIGN, "weight images, h1 and q_out must be 16-byte aligned");
+  StreamGuard g(stream);
+  const uint64_t k = seed * 0x9E3779B97F4A7C15ull + counter * 0xD1B54A32D192ED03ull + 1;
+  MzQAct q{bits_dev, obs6_dev, rows_dev, count_dev, n, conv_w_dev, conv_b_dev, w1_hi_dev,
+           w1_lo_dev, b1_dev, w2_hi_dev, w2_lo_dev, b2_dev, w3_dev, b3_dev,
+           drop_p > 0.0f ? (uint32_t)(drop_p * 65536.0f + 0.5f) : 0u,
+           drop_p > 0.0f ? 1.0f / (1.0f - drop_p) : 1.0f, (uint32_t)(k ^ (k >> 32)), h1_dev,
+           greedy_dev, q_out_dev};
+  MZ_HIP(mz_launch_qact(q, relu, static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+

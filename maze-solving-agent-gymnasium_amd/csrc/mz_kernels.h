@@ -126,3 +126,21 @@ struct MzPpoFinish {
 hipError_t mz_launch_ppo_act(const MzPpoAct& q, hipStream_t s);
 hipError_t mz_launch_ppo_scan(const MzPpoScan& q, hipStream_t s);
 hipError_t mz_launch_ppo_finish(const MzPpoFinish& q, int max_episodes, hipStream_t s);
+
+// ---- f32-accurate acting forward on the bf16 MFMA (mz_qact.hip) ------------------------------
+struct MzQAct {
+  const uint32_t* bits; const float* obs6;   // [B][22], [B][6] (instance rows)
+  const int32_t* rows; const int32_t* count; int n;  // rows[i] (i < min(n, *count)) or row i
+  const float* conv_w; const float* conv_b;  // [32][27], [32]
+  const uint16_t* w1h; const uint16_t* w1l; const float* b1;  // prepared [1024][1600] bf16, [1024]
+  const uint16_t* w2h; const uint16_t* w2l; const float* b2;  // prepared [512][1024] bf16, [512]
+  const float* w3; const float* b3;          // [4][512], [4]
+  uint32_t drop_thresh; float drop_scale; uint32_t key;
+  float* h1;                                 // workspace [n][1024] f32
+  int64_t* greedy; float* q_out;             // greedy[inst] = argmax; q_out [n][4] (nullable)
+};
+int mz_qact_row_tiles(int n);
+hipError_t mz_launch_qact(const MzQAct& q, int relu, hipStream_t s);
+hipError_t mz_launch_qact_prepare(const float* w1, const float* w2, uint16_t* w1h, uint16_t* w1l,
+                                  uint16_t* w2h, uint16_t* w2l, hipStream_t s);
+

@@ -1,0 +1,624 @@
+// mz_qact.hip — the DQN / DDQN acting forward (argmax_a Q_source(s), dqn_agent.py:113-116,
+// ddqn_agent.py:98-110) from packed window bits, in two launches, f32-accurate on the bf16 MFMA.
+//
+// Precision. The reference acts in f32. A plain bf16 acting head agreed with the f32 argmax on
+// 99.4 % of real trainer states (profiles/r03c_acting_precision.json: every miss a near-tie);
+// emulated variants put the error in every layer. Here each GEMM operand x is split into
+// x_hi = bf16(x), x_lo = bf16(x - x_hi), and a product is hi*hi + hi*lo + lo*hi with f32
+// accumulation ("bf16x3", three v_mfma_f32_16x16x32_bf16 per tile): ~2^-16 relative per
+// product, the f32 argmax on 100 % of those states, at ~5x the f32 MFMA's rate (gfx950 has no
+// xf32; f32 MFMA runs at 1/16 of bf16). The conv's input is a binary window (exact in bf16), so
+// only its weights are split.
+//
+//   k_qact1  conv stem + fc1: per workgroup 64 rows x 256 fc1 outputs, 4 waves (column quarters,
+//            64 x 64 each). The K loop runs over the 49 pooled positions (32
+//            channels each, the feature order q * 32 + c) and one chunk for obs6: the chunk's A
+//            tile is produced in LDS by the conv (MFMA over 27 patch bits x 32 channels, pool by
+//            register max, LeakyReLU, DDQN's dropout) while the previous chunk's fc1 MFMAs run —
+//            the 1,574-wide feature row never leaves the chip. fc1's weights stream from L2:
+//            workgroups are dealt round-robin over the 8 XCDs, and XCD x works on output tile
+//            x / 2, so each XCD's L2 holds one 1.6 MB hi/lo weight slice. Output: the LeakyReLU
+//            of fc1 as f32 rows.
+//   k_qact2  fc2 + ReLU (DDQN) / LeakyReLU (DQN) + fc3 (f32) + argmax (first maximum, NaN as
+//            torch.argmax) + the scatter of the action to the listed instance.
+// Both read the row count from the device (the greedy-row list's length, mz_greedy_rows):
+// workgroups past it exit, so no host round trip sizes the work.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "mz_kernels.h"
+
+namespace {
+
+constexpr int WAVE = 64;
+constexpr int CONV_OUT = 1568;     // 32 channels x 7 x 7 pooled positions
+constexpr int K1 = 1600;           // fc1 input row as prepared: features | obs6 | zero pad
+constexpr int N1 = 1024, N2 = 512;
+constexpr int NCH = K1 / 32;       // 50 K chunks: 49 pooled positions + obs6
+// k_qact1: QW1 waves per workgroup (4 column quarters x QW1 / 4 row halves of 64 rows); 4-wave
+// workgroups let two independent workgroups share a CU (their barrier phases drift apart, so one
+// runs MFMAs while the other waits on LDS / VALU work)
+#ifndef MZ_QACT_WAVES
+#define MZ_QACT_WAVES 4
+#endif
+constexpr int QW1 = MZ_QACT_WAVES;
+constexpr int T1 = 64 * QW1;       // k_qact1 threads
+constexpr int RT1 = 16 * QW1;      // k_qact1 rows per workgroup (4 conv tiles of 4 rows per wave)
+constexpr int NT1 = 256;           // k_qact1 fc1 outputs per workgroup
+constexpr int PR = 17;             // padded window rows per instance
+constexpr int AST = 40;            // LDS A-tile row stride in bf16 (32 + 8: conflict-free b128)
+constexpr int RT2 = 64;            // k_qact2 rows per workgroup
+
+typedef __attribute__((ext_vector_type(8))) __bf16 frag_ab;
+typedef __attribute__((ext_vector_type(4))) float frag_cd;
+
+__device__ inline uint32_t bf16x2(float lo, float hi) {  // round to nearest even, packed
+  uint32_t r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+  return r;
+}
+__device__ inline float bf16_round(float x) {  // x rounded to bf16, as f32 (RNE)
+  return __uint_as_float(bf16x2(x, 0.0f) << 16);
+}
+// x = hi + lo + O(2^-17 x): the two bf16 halves, packed for a pair of adjacent elements
+__device__ inline void split2(float x0, float x1, uint32_t& hi, uint32_t& lo) {
+  const float h0 = bf16_round(x0), h1 = bf16_round(x1);
+  hi = bf16x2(h0, h1);
+  lo = bf16x2(x0 - h0, x1 - h1);
+}
+
+__device__ inline uint32_t lowbias32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+// DDQN's acting dropout (nn.Dropout(0.2) in train mode): the conv output (row, channel
+// c, pooled position q, 2x2 position p) is kept iff a 16-bit uniform >= thresh, P(drop) = thresh /
+// 65536; the uniforms come from one xorshift32 stream per (row, channel pair) seeded from the
+// key and the row (k_qact1), so tests rebuild the masks (tests/test_qact.py).
+
+__device__ inline float leaky(float x) { return x > 0.0f ? x : x * 0.01f; }
+
+// acc[i][j] += A_i B_j over one 32-deep K chunk, split precision: hi*hi, then hi*lo, then lo*hi
+// over all 16 tiles (product-major: consecutive MFMAs never share an accumulator)
+__device__ inline void mfma_x3(const frag_ab (&ah)[4], const frag_ab (&al)[4], const uint4 (&bh)[4],
+                               const uint4 (&bl)[4], frag_cd (&acc)[4][4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], __builtin_bit_cast(frag_ab, bh[j]),
+                                                          acc[i][j], 0, 0, 0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], __builtin_bit_cast(frag_ab, bl[j]),
+                                                          acc[i][j], 0, 0, 0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], __builtin_bit_cast(frag_ab, bh[j]),
+                                                          acc[i][j], 0, 0, 0);
+}
+
+// ---- k_qact1 -------------------------------------------------------------------------------
+template <bool DROP>
+__global__ __launch_bounds__(T1) __attribute__((amdgpu_waves_per_eu(8 / QW1, 8 / QW1)))
+void k_qact1(MzQAct q, int row_tiles) {
+  __shared__ uint4 lut[256];                   // 8 patch bits -> 8 bf16 (0 / 1.0)
+  __shared__ uint32_t spread[256];             // 8 bits -> bits at 3i
+  __shared__ uint64_t crow[RT1 * PR];          // column-interleaved padded window rows
+  __shared__ uint32_t wb[RT1 * 22];            // the rows' window bits
+  __shared__ __align__(16) uint16_t A[2][2][RT1 * AST];  // [buffer][hi, lo][row][k]
+
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1);
+  const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);
+  const int g4 = lane >> 4, c16 = lane & 15;
+  // XCD-aware tile map: workgroup b runs on XCD b % 8 (round-robin dispatch); XCD x computes
+  // output tile x / 2, so one XCD's L2 serves one weight slice
+  const int b = blockIdx.x, x = b & 7;
+  const int nt = x >> 1, rt = ((b >> 3) << 1) | (x & 1);
+  if (rt >= row_tiles) return;
+  const int m = q.count ? min(q.n, *q.count) : q.n;
+  const int r0 = rt * RT1;
+  if (r0 >= m) return;
+  const int nr = min(RT1, m - r0);
+
+  for (int i = tid; i < 256; i += T1) {
+    uint32_t v[4], sp = 0;
+    for (int p = 0; p < 4; ++p)
+      v[p] = (((i >> (2 * p)) & 1) ? 0x3F80u : 0u) | (((i >> (2 * p + 1)) & 1) ? 0x3F800000u : 0u);
+    lut[i] = make_uint4(v[0], v[1], v[2], v[3]);
+    for (int k = 0; k < 8; ++k) sp |= ((uint32_t)(i >> k) & 1u) << (3 * k);
+    spread[i] = sp;
+  }
+  for (int i = tid; i < RT1 * 22; i += T1) {
+    const int r = i / 22, k = i - r * 22;
+    uint32_t v = 0;
+    if (r < nr) {
+      const int inst = q.rows ? q.rows[r0 + r] : r0 + r;
+      v = q.bits[(size_t)inst * 22 + k];
+    }
+    wb[i] = v;
+  }
+  for (int r = tid; r < RT1; r += T1) {
+    crow[r * PR] = 0ull;
+    crow[r * PR + 16] = 0ull;
+  }
+  __syncthreads();
+  // window row y of every channel -> one column-interleaved row (col c at bits 3(c+1) + ch)
+  for (int i = tid; i < RT1 * 15; i += T1) {
+    const int r = i / 15, y = i - r * 15;
+    uint64_t cr = 0;
+    for (int ch = 0; ch < 3; ++ch) {
+      const int f0 = ch * 225 + y * 15, j = f0 >> 5;
+      const uint64_t v = ((uint64_t)wb[r * 22 + j + 1] << 32) | wb[r * 22 + j];
+      const uint32_t row = (uint32_t)(v >> (f0 & 31)) & 0x7FFFu;
+      const uint64_t sp = (uint64_t)spread[row & 0xFF] | ((uint64_t)spread[row >> 8] << 24);
+      cr |= sp << (3 + ch);
+    }
+    crow[r * PR + y + 1] = cr;
+  }
+
+  // conv B operands, hi and lo: lane holds W[c][k] for k = 8 g4 + j, c = 2 c16 (even) and
+  // 2 c16 + 1 (odd); K order 9 ky + 3 kx + ch (the interleaved rows), torch's [c][ch][ky][kx]
+  frag_ab be_h, be_l, bo_h, bo_l;
+  for (int j = 0; j < 8; ++j) {
+    const int k = 8 * g4 + j;
+    const int ky = k / 9, kx = (k % 9) / 3, ch = k % 3;
+    const int wi = ch * 9 + ky * 3 + kx;
+    const float we = k < 27 ? q.conv_w[(2 * c16) * 27 + wi] : 0.0f;
+    const float wo = k < 27 ? q.conv_w[(2 * c16 + 1) * 27 + wi] : 0.0f;
+    const float weh = bf16_round(we), woh = bf16_round(wo);
+    be_h[j] = static_cast<__bf16>(weh);
+    be_l[j] = static_cast<__bf16>(we - weh);
+    bo_h[j] = static_cast<__bf16>(woh);
+    bo_l[j] = static_cast<__bf16>(wo - woh);
+  }
+  const float bias_e = q.conv_b[2 * c16], bias_o = q.conv_b[2 * c16 + 1];
+  // dropout streams (DDQN): one xorshift32 stream per (row, channel pair) — this lane's rows
+  // 4 (4w + tt) + g4, pair c16 — seeded lowbias32(lowbias32(key ^ lowbias32(row)) ^ pair) | 1,
+  // four draws per pooled position in chunk order
+  uint32_t rs[4] = {0u, 0u, 0u, 0u};
+  if (DROP) {
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      const uint32_t row = (uint32_t)(r0 + 4 * (4 * w + tt) + g4);
+      rs[tt] = lowbias32(lowbias32(q.key ^ lowbias32(row)) ^ (uint32_t)c16) | 1u;
+    }
+  }
+
+  // fc1 tile of this wave: rows 64 rh + 16 i, columns nt * 256 + 64 cq + 16 j
+  const int rh = w >> 2, cq = w & 3;
+  const int col0 = nt * NT1 + cq * 64;
+  frag_cd acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = frag_cd{0.0f, 0.0f, 0.0f, 0.0f};
+  // B fragments of chunk c: lane reads W1[col][32 c + 8 g4 .. +8] (16 B, hi and lo images)
+  uint4 bh[4], bl[4], nbh[4], nbl[4];
+  // B fragments: the fragment-ordered image (k_qact_prepare) — this wave's 4 KB per chunk and
+  // image are contiguous, lane-linear 16-B loads through buffer descriptors (32-bit offsets)
+  const auto rs_h = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(q.w1h) + (size_t)nt * NT1 * K1,
+                                                      0, NT1 * K1 * 2, 0x00020000);
+  const auto rs_l = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(q.w1l) + (size_t)nt * NT1 * K1,
+                                                      0, NT1 * K1 * 2, 0x00020000);
+  const int boff = (cq * 4 * 64 + lane) * 16;  // bytes within a chunk's 16 KB
+  auto load_b = [&](int c, uint4* dh, uint4* dl) {
+#ifdef MZ_QPROBE_NO_BLOAD
+    if (c > 0) return;
+#endif
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int off = boff + c * (4 * 4 * 64 * 16) + j * (64 * 16);
+      dh[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs_h, off, 0, 0));
+      dl[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs_l, off, 0, 0));
+    }
+  };
+  __syncthreads();  // crow complete
+
+  // stage 1 — the A tile of conv chunk c (pooled position c) into A[c & 1]: conv tiles 4w .. 4w + 3
+  // (tile t: instances 4t .. 4t + 3); A row of this lane = c16: instance 4t + c16 / 4, position
+  // c16 % 4 of its 2x2 pooling window
+  auto conv_chunk = [&](int c) {
+    const int py = c / 7, px = c - py * 7;
+    uint16_t* Ah = A[c & 1][0];
+    uint16_t* Al = A[c & 1][1];
+    frag_ab a[4];
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      const int inst = 4 * (4 * w + tt) + (c16 >> 2), pos = c16 & 3;
+      const int y = 2 * py + (pos >> 1), xx = 2 * px + (pos & 1);
+      const uint64_t* cr = crow + inst * PR + y;
+      const uint32_t p = ((uint32_t)(cr[0] >> (3 * xx)) & 0x1FFu) |
+                         (((uint32_t)(cr[1] >> (3 * xx)) & 0x1FFu) << 9) |
+                         (((uint32_t)(cr[2] >> (3 * xx)) & 0x1FFu) << 18);
+#ifdef MZ_QACT_VALU_LUT
+      // the 8 patch bits of this lane's K slice -> 8 bf16 (0 / 1.0) in registers
+      const uint32_t by = (p >> (8 * g4)) & 0xFFu;
+      uint4 v;
+      v.x = __umul24((by & 1u) | (((by >> 1) & 1u) << 16), 0x3F80u);
+      v.y = __umul24(((by >> 2) & 1u) | (((by >> 3) & 1u) << 16), 0x3F80u);
+      v.z = __umul24(((by >> 4) & 1u) | (((by >> 5) & 1u) << 16), 0x3F80u);
+      v.w = __umul24(((by >> 6) & 1u) | (((by >> 7) & 1u) << 16), 0x3F80u);
+      a[tt] = __builtin_bit_cast(frag_ab, v);
+#else
+      a[tt] = __builtin_bit_cast(frag_ab, lut[(p >> (8 * g4)) & 0xFFu]);
+#endif
+    }
+    frag_cd e[4], o[4];
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      e[tt] = frag_cd{bias_e, bias_e, bias_e, bias_e};
+      o[tt] = frag_cd{bias_o, bias_o, bias_o, bias_o};
+    }
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      e[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tt], be_h, e[tt], 0, 0, 0);
+      o[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tt], bo_h, o[tt], 0, 0, 0);
+    }
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      e[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tt], be_l, e[tt], 0, 0, 0);
+      o[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tt], bo_l, o[tt], 0, 0, 0);
+    }
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      // lane: pooled output of instance 4t + g4, channels 2 c16 (e) and 2 c16 + 1 (o);
+      // registers = the 4 positions of its 2x2 window
+      const int il = 4 * (4 * w + tt) + g4;
+      float ve, vo;
+      if (DROP) {
+        // MaxPool(Dropout(LeakyReLU(x))) = scale * leaky(max_r x'_r), x'_r = x_r kept, 0
+        // dropped (leaky(0) = 0; leaky and the scale are monotonic): the 4 draws of this chunk
+        // from the lane's stream, low half -> even channel, high half -> odd
+        float me = 0.0f, mo = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          uint32_t x = rs[tt];
+          x ^= x << 13;
+          x ^= x >> 17;
+          x ^= x << 5;
+          rs[tt] = x;
+          const float xe = (x & 0xFFFFu) >= q.drop_thresh ? e[tt][r] : 0.0f;
+          const float xo = (x >> 16) >= q.drop_thresh ? o[tt][r] : 0.0f;
+          me = r ? fmaxf(me, xe) : xe;
+          mo = r ? fmaxf(mo, xo) : xo;
+        }
+        ve = leaky(me) * q.drop_scale;
+        vo = leaky(mo) * q.drop_scale;
+      } else {
+        ve = leaky(fmaxf(fmaxf(e[tt][0], e[tt][1]), fmaxf(e[tt][2], e[tt][3])));
+        vo = leaky(fmaxf(fmaxf(o[tt][0], o[tt][1]), fmaxf(o[tt][2], o[tt][3])));
+      }
+      uint32_t hi, lo;
+      split2(ve, vo, hi, lo);
+      reinterpret_cast<uint32_t*>(Ah + il * AST)[c16] = hi;
+      reinterpret_cast<uint32_t*>(Al + il * AST)[c16] = lo;
+    }
+  };
+  // stage 1 of the last chunk: features 1568..1573 = obs6, then zeros
+  auto obs_chunk = [&]() {
+    uint16_t* Ah = A[(NCH - 1) & 1][0];
+    uint16_t* Al = A[(NCH - 1) & 1][1];
+    for (int i = tid; i < RT1 * 16; i += T1) {
+      const int r = i >> 4, k2 = (i & 15) * 2;
+      float v0 = 0.0f, v1 = 0.0f;
+      if (r < nr && k2 < 6) {
+        const int inst = q.rows ? q.rows[r0 + r] : r0 + r;
+        v0 = q.obs6[(size_t)inst * 6 + k2];
+        v1 = q.obs6[(size_t)inst * 6 + k2 + 1];
+      }
+      uint32_t hi, lo;
+      split2(v0, v1, hi, lo);
+      reinterpret_cast<uint32_t*>(Ah + r * AST)[k2 >> 1] = hi;
+      reinterpret_cast<uint32_t*>(Al + r * AST)[k2 >> 1] = lo;
+    }
+  };
+  // stage 2 — the fc1 MFMAs of chunk c from A[c & 1] and the B fragments in bh / bl. The A
+  // fragments are read before stage 1 writes the other buffer (program order: the compiler
+  // keeps LDS reads after earlier LDS writes), so the MFMAs can run beside stage 1's VALU work
+  frag_ab ah[4], al[4];
+  auto fc1_read = [&](int c) {
+    const uint16_t* Ah = A[c & 1][0];
+    const uint16_t* Al = A[c & 1][1];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 64 * rh + 16 * i + c16;
+      ah[i] = __builtin_bit_cast(frag_ab, *reinterpret_cast<const uint4*>(Ah + r * AST + 8 * g4));
+      al[i] = __builtin_bit_cast(frag_ab, *reinterpret_cast<const uint4*>(Al + r * AST + 8 * g4));
+    }
+  };
+  auto fc1_mfma = [&](const uint4 (&xh)[4], const uint4 (&xl)[4]) {
+#ifndef MZ_QPROBE_NO_FC1
+    mfma_x3(ah, al, xh, xl, acc);
+#endif
+  };
+
+  // iteration c: the A tile of chunk c and the fc1 MFMAs of chunk c - 1, one barrier; the B
+  // fragments of chunk c are loaded in iteration c and used in c + 1. The main loop body is one
+  // basic block, so the scheduler can run the conv's LDS / VALU work between the fc1 MFMAs.
+  // the scheduler's order for one half-iteration: the conv MFMAs as their inputs arrive, then
+  // fc1's 48 MFMAs each with a few of the stage-1 VALU instructions (pool / dropout / split)
+  // between them — the MFMA holds the SIMD's VALU issue for only 8 of its 16 cycles
+  auto interleave = [&]() {
+#ifdef MZ_QACT_INTERLEAVE
+#pragma unroll
+    for (int k = 0; k < 64; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, MZ_QACT_INTERLEAVE, 0);
+    }
+#endif
+  };
+  // B registers ping-pong between (bh, bl) and (nbh, nbl): the loop body is unrolled by two (conv
+  // chunks 1 .. 48 and the fc1 steps of chunks 0 .. 47)
+  load_b(0, bh, bl);
+#ifndef MZ_QPROBE_NO_CONV
+  conv_chunk(0);
+#endif
+  __syncthreads();
+  static_assert((NCH - 2) % 2 == 0, "main loop unrolled by two");
+  for (int c = 1; c < NCH - 1; c += 2) {
+    fc1_read(c - 1);
+    load_b(c, nbh, nbl);
+#ifndef MZ_QPROBE_NO_CONV
+    conv_chunk(c);
+#endif
+    fc1_mfma(bh, bl);
+    interleave();
+    __syncthreads();
+    fc1_read(c);
+    load_b(c + 1, bh, bl);
+#ifndef MZ_QPROBE_NO_CONV
+    conv_chunk(c + 1);
+#endif
+    fc1_mfma(nbh, nbl);
+    interleave();
+    __syncthreads();
+  }
+  // the obs6 chunk, then the last two fc1 steps
+  fc1_read(NCH - 2);
+  load_b(NCH - 1, nbh, nbl);
+  obs_chunk();
+  fc1_mfma(bh, bl);
+  __syncthreads();
+  fc1_read(NCH - 1);
+  fc1_mfma(nbh, nbl);
+
+  // epilogue: h1 = LeakyReLU(acc + b1) as f32 rows (list order); lane: column 16 j + c16 of the
+  // wave's tile, rows 16 i + 4 g4 + reg
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = col0 + 16 * j + c16;
+    const float bb = q.b1[col];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 64 * rh + 16 * i + 4 * g4 + r;
+        if (row < nr) q.h1[(size_t)(r0 + row) * N1 + col] = leaky(acc[i][j][r] + bb);
+      }
+  }
+}
+
+// ---- k_qact2 -------------------------------------------------------------------------------
+template <bool RELU>
+__global__ __launch_bounds__(512) void k_qact2(MzQAct q) {
+  __shared__ __align__(16) uint16_t A[2][2][RT2 * AST];
+  __shared__ float part[8][RT2][4];
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1);
+  const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);
+  const int g4 = lane >> 4, c16 = lane & 15;
+  const int m = q.count ? min(q.n, *q.count) : q.n;
+  const int r0 = blockIdx.x * RT2;
+  if (r0 >= m) return;
+  const int nr = min(RT2, m - r0);
+  const int col0 = 64 * w;  // this wave's 64 fc2 outputs
+
+  // A chunk c (32 columns of h1 for the 64 rows): thread -> (row tid / 8, 4 columns)
+  const int ar = tid >> 3, ak = (tid & 7) * 4;
+  auto load_a = [&](int c) -> float4 {
+    if (ar >= nr) return make_float4(0.f, 0.f, 0.f, 0.f);
+    return *reinterpret_cast<const float4*>(q.h1 + (size_t)(r0 + ar) * N1 + 32 * c + ak);
+  };
+  auto store_a = [&](int buf, float4 v) {
+    uint32_t h0, l0, h1, l1;
+    split2(v.x, v.y, h0, l0);
+    split2(v.z, v.w, h1, l1);
+    uint32_t* ph = reinterpret_cast<uint32_t*>(A[buf][0] + ar * AST + ak);
+    uint32_t* pl = reinterpret_cast<uint32_t*>(A[buf][1] + ar * AST + ak);
+    ph[0] = h0; ph[1] = h1;
+    pl[0] = l0; pl[1] = l1;
+  };
+  uint4 bh[4], bl[4], nbh[4], nbl[4];
+  // B fragments from the fragment-ordered fc2 image: [chunk][wave][j][lane][8]
+  const auto rs_h = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(q.w2h), 0, N2 * N1 * 2,
+                                                      0x00020000);
+  const auto rs_l = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(q.w2l), 0, N2 * N1 * 2,
+                                                      0x00020000);
+  const int boff = (w * 4 * 64 + lane) * 16;
+  auto load_b = [&](int c, uint4* dh, uint4* dl) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int off = boff + c * (8 * 4 * 64 * 16) + j * (64 * 16);
+      dh[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs_h, off, 0, 0));
+      dl[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs_l, off, 0, 0));
+    }
+  };
+  frag_cd acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = frag_cd{0.0f, 0.0f, 0.0f, 0.0f};
+  constexpr int NC2 = N1 / 32;
+  store_a(0, load_a(0));
+  load_b(0, bh, bl);
+  float4 na = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  for (int c = 0; c < NC2; ++c) {
+    if (c + 1 < NC2) {
+      na = load_a(c + 1);
+      load_b(c + 1, nbh, nbl);
+    }
+    const uint16_t* Ah = A[c & 1][0];
+    const uint16_t* Al = A[c & 1][1];
+    frag_ab ah[4], al[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 16 * i + c16;
+      ah[i] = __builtin_bit_cast(frag_ab, *reinterpret_cast<const uint4*>(Ah + r * AST + 8 * g4));
+      al[i] = __builtin_bit_cast(frag_ab, *reinterpret_cast<const uint4*>(Al + r * AST + 8 * g4));
+    }
+    mfma_x3(ah, al, bh, bl, acc);
+    if (c + 1 < NC2) {
+      store_a((c + 1) & 1, na);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bh[j] = nbh[j];
+        bl[j] = nbl[j];
+      }
+    }
+    __syncthreads();
+  }
+
+  // h2 = act(acc + b2) in f32; fc3 partial sums over this wave's 64 columns, per row and action
+  float s[4][4][4];  // [i][reg][action]
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int a = 0; a < 4; ++a) s[i][r][a] = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = col0 + 16 * j + c16;
+    const float bb = q.b2[col];
+    float w3[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) w3[a] = q.w3[a * N2 + col];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float h = acc[i][j][r] + bb;
+        const float hv = RELU ? fmaxf(h, 0.0f) : leaky(h);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) s[i][r][a] += hv * w3[a];
+      }
+  }
+  // sum over the 16 lanes of a row group (columns), fixed butterfly order
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        float v = s[i][r][a];
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 4);
+        v += __shfl_xor(v, 8);
+        s[i][r][a] = v;
+      }
+  if (c16 == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) part[w][16 * i + 4 * g4 + r][a] = s[i][r][a];
+  }
+  __syncthreads();
+  if (tid < nr) {
+    float qv[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      float v = 0.0f;
+      for (int k = 0; k < 8; ++k) v += part[k][tid][a];
+      qv[a] = v + q.b3[a];
+    }
+    int best = 0;  // torch.argmax: the first maximum, a NaN counts as the maximum
+    for (int a = 1; a < 4; ++a)
+      if (!isnan(qv[best]) && (isnan(qv[a]) || qv[a] > qv[best])) best = a;
+    const int row = r0 + tid;
+    const int inst = q.rows ? q.rows[row] : row;
+    if (q.greedy) q.greedy[inst] = best;
+    if (q.q_out) *reinterpret_cast<float4*>(q.q_out + (size_t)row * 4) =
+        make_float4(qv[0], qv[1], qv[2], qv[3]);
+  }
+}
+
+// ---- weight preparation ----------------------------------------------------------------------
+// fc1 [1024][1574] (torch order: feature c * 49 + q, then obs6) and fc2 [512][1024] -> hi / lo bf16
+// images in MFMA fragment order: element ((((tile * NCH + chunk) * 4 + wave) * 4 + j) * 64 + lane)
+// * 8 + e of the fc1 image is W1[output tile * 256 + 64 wave + 16 j + lane % 16][feature 32 chunk +
+// 8 (lane / 16) + e] (kernel feature order q * 32 + c, obs6 at 1568, zero pad to 1600); the fc2 image
+// is [chunk 32][wave 8][j][lane][8]. A wave's B fragments for one chunk are then 4 KB contiguous
+// per image: one fully coalesced 1 KB load per 16-column tile instead of 16 rows x 64 B.
+__global__ void k_qact_prepare(const float* __restrict__ w1, const float* __restrict__ w2,
+                               uint16_t* __restrict__ w1h, uint16_t* __restrict__ w1l,
+                               uint16_t* __restrict__ w2h, uint16_t* __restrict__ w2l) {
+  const int64_t n1 = (int64_t)N1 * K1, n2 = (int64_t)N2 * N1;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n1 + n2;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    // element e of the fragment-ordered image: [tile][chunk][wave][j][lane][8] (see w1_frag)
+    const int64_t o = e < n1 ? e : e - n1;
+    const int el = (int)(o & 7), lane = (int)((o >> 3) & 63), j = (int)((o >> 9) & 3);
+    const int64_t rest = o >> 11;
+    float v;
+    uint16_t *ph, *pl;
+    if (e < n1) {
+      const int cq = (int)(rest & 3), c = (int)((rest >> 2) % NCH), nt = (int)((rest >> 2) / NCH);
+      const int r = nt * NT1 + cq * 64 + 16 * j + (lane & 15);  // fc1 output
+      const int f = 32 * c + 8 * (lane >> 4) + el;                // kernel feature order
+      int src = -1;
+      if (f < CONV_OUT) src = (f & 31) * 49 + (f >> 5);
+      else if (f < CONV_OUT + 6) src = f;
+      v = src >= 0 ? w1[(size_t)r * (CONV_OUT + 6) + src] : 0.0f;
+      ph = w1h; pl = w1l;
+    } else {
+      const int wv = (int)(rest & 7), c = (int)(rest >> 3);
+      const int r = 64 * wv + 16 * j + (lane & 15);            // fc2 output
+      const int k = 32 * c + 8 * (lane >> 4) + el;
+      v = w2[(size_t)r * N1 + k];
+      ph = w2h; pl = w2l;
+    }
+    const float h = bf16_round(v);
+    ph[o] = (uint16_t)(bf16x2(h, 0.0f) & 0xFFFFu);
+    pl[o] = (uint16_t)(bf16x2(v - h, 0.0f) & 0xFFFFu);
+  }
+}
+
+}  // namespace
+
+int mz_qact_row_tiles(int n) { return (n + RT1 - 1) / RT1; }
+
+hipError_t mz_launch_qact(const MzQAct& q, int relu, hipStream_t s) {
+  if (q.n <= 0) return hipSuccess;
+  const int rt = (q.n + RT1 - 1) / RT1;
+  // 8 workgroups per pair of row tiles: XCD x takes output tile x / 2 of row tile 2 k + (x & 1)
+  const int blocks1 = 8 * ((rt + 1) / 2);
+  if (q.drop_thresh)
+    hipLaunchKernelGGL(k_qact1<true>, dim3(blocks1), dim3(T1), 0, s, q, rt);
+  else
+    hipLaunchKernelGGL(k_qact1<false>, dim3(blocks1), dim3(T1), 0, s, q, rt);
+  const int blocks2 = (q.n + RT2 - 1) / RT2;
+  if (relu)
+    hipLaunchKernelGGL(k_qact2<true>, dim3(blocks2), dim3(512), 0, s, q);
+  else
+    hipLaunchKernelGGL(k_qact2<false>, dim3(blocks2), dim3(512), 0, s, q);
+  return hipGetLastError();
+}
+
+hipError_t mz_launch_qact_prepare(const float* w1, const float* w2, uint16_t* w1h, uint16_t* w1l,
+                                  uint16_t* w2h, uint16_t* w2l, hipStream_t s) {
+  hipLaunchKernelGGL(k_qact_prepare, dim3(1024), dim3(256), 0, s, w1, w2, w1h, w1l, w2h, w2l);
+  return hipGetLastError();
+}

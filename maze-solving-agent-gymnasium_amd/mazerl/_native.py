@@ -45,7 +45,7 @@ EXPORTS = ["mz_last_error", "mz_device_count", "mz_create", "mz_destroy", "mz_lo
            "mz_replay_gather", "mz_host_alloc", "mz_host_free", "mz_q_front_rows", "mz_greedy_rows",
            "mz_trainer_tick", "mz_greedy_scatter", "mz_head_bf16", "mz_replay_push",
            "mz_replay_sample_idx", "mz_q_loss", "mz_q_loss_backward", "mz_adamw_groups",
-           "mz_ppo_act", "mz_ppo_scan", "mz_ppo_finish"]
+           "mz_ppo_act", "mz_ppo_scan", "mz_ppo_finish", "mz_qact_prepare", "mz_qact"]
 
 _lib = None
 
@@ -134,6 +134,9 @@ def load(build_if_missing=True):
     L.mz_ppo_scan.argtypes = [vp, vp, vp, C.c_int32, C.c_int32] + [vp] * 10
     L.mz_ppo_finish.argtypes = [vp] * 6 + [C.c_int32, C.c_int32] + [vp] * 4 + \
         [C.c_double, C.c_int64] + [vp] * 7
+    L.mz_qact_prepare.argtypes = [vp] * 7
+    L.mz_qact.argtypes = [vp, vp, vp, vp, C.c_int32] + [vp] * 10 + [C.c_int32, C.c_float,
+                                                                   C.c_uint64, C.c_uint64] + [vp] * 4
     L.mz_host_alloc.argtypes = [C.c_uint64, C.c_int32, C.POINTER(vp), C.POINTER(vp)]
     L.mz_host_free.argtypes = [vp]
     for f in EXPORTS:

@@ -268,7 +268,7 @@ class VectorDQNLearner:
                  eps_decay=8000.0, gamma=0.7, batch_size=128, capacity=1_000_000,
                  updates_per_step=1, target_every=100, hidden_dim=1024, h_channels=32,
                  act_bf16=True, t_max=150, updates_per_epoch=100, allreduce=None, seed=0,
-                 use_graph=True, bit_stem=True, overlap=False, greedy_rows=True):
+                 use_graph=True, bit_stem=True, overlap=False, greedy_rows=True, acting="x3"):
         self.device = torch.device(device)
         torch.manual_seed(seed)
         self.variant = variant
@@ -310,15 +310,18 @@ class VectorDQNLearner:
         # acting forward over the rows that act greedily only (agents/fused.py GreedyRows)
         self.greedy_rows = bool(greedy_rows)
         self._rows = None
+        # the acting head on the GPU: "x3" = QAct (f32-accurate bf16x3 MFMA, sized on the device:
+        # no host round trip per vector step); "bf16" = FusedQ (bf16 stem + hipBLASLt bf16 GEMMs)
+        if acting not in ("x3", "bf16"):
+            raise ValueError(f"acting {acting!r}: 'x3' or 'bf16'")
+        self.acting = acting
         if self.device.type == "cuda" and act_bf16:
-            from .fused import FusedQ
-            self.fused = FusedQ(self.source, seed=seed)
+            self.fused = self._head(self.source, seed)
         # env -> learner handoff on a side HIP stream (north_star): the updates of vector step t
         # run on `side` while the main stream acts and steps the env for t + 1 (see update()).
         self.overlap = bool(overlap) and self.use_graph and self.fused is not None
         self._async = False
         if self.overlap:
-            from .fused import FusedQ
             self.side = torch.cuda.Stream(self.device)
             # two actor snapshots of the source net (ping-pong) with their own fused heads and
             # dropout streams; the source net itself is only touched on `side`
@@ -326,13 +329,20 @@ class VectorDQNLearner:
             self.actors = [copy.deepcopy(self.source) for _ in range(2)]
             for a in self.actors:
                 flatten_params(a)
-            self.actor_fused = [FusedQ(a, seed=seed * 2 + 101 + k) for k, a in enumerate(self.actors)]
+            self.actor_fused = [self._head(a, seed * 2 + 101 + k) for k, a in enumerate(self.actors)]
             self._published = collections.deque()  # (slot, event) of issued snapshots, oldest first
             self._acting = None  # slot greedy() reads
             self._idx = None     # [2][K, batch] sample indices, written on the main stream
             self._par = 0
             self._sample_seed = 0x5A3B1E + 7919 * int(seed)
             self._sample_counter = 0
+
+    def _head(self, net, seed):
+        if self.acting == "x3":
+            from .qact import QAct
+            return QAct(net, seed=seed)
+        from .fused import FusedQ
+        return FusedQ(net, seed=seed)
 
     @property
     def supports_bits(self):
@@ -354,7 +364,9 @@ class VectorDQNLearner:
                 if self._rows is None:
                     from .fused import GreedyRows
                     self._rows = GreedyRows(bits.shape[0], self.device)
-                return self._rows(f, obs6, bits, *act)  # (waits for the list's count)
+                return self._rows(f, obs6, bits, *act)
+            if hasattr(f, "greedy"):
+                return f.greedy(obs6, bits)
             return f(obs6, bits).float().argmax(1)
         if window is None:
             raise ValueError("greedy() needs the f32 window or window bits on the GPU")

@@ -201,7 +201,8 @@ class FusedQ:
 class GreedyRows:
     """The greedy-row list of the next fused act (mz_greedy_rows: the instances that will act
     greedily with this eps / seed / counter, dqn_agent.py:104-116) and the acting forward over
-    those rows only; its count comes back to the host (one stream sync) to size the GEMMs.
+    those rows only. With QAct (agents/qact.py) the forward reads the list's length on the
+    device; with FusedQ the count comes back to the host (one stream sync) to size the GEMMs.
     `greedy` [n] int64 holds the argmax of the listed rows; the other entries are stale — the
     fused act never reads them (it explores there)."""
 
@@ -252,6 +253,11 @@ class GreedyRows:
         key = (eps.data_ptr() if torch.is_tensor(eps) else float(eps), seed, counter)
         if getattr(self, "_issued", None) != key:
             self.issue(eps, seed, counter)
+        if hasattr(fused, "rows_greedy"):
+            # QAct: the forward reads the list's length on the device — no host wait
+            self._issued = None
+            fused.rows_greedy(obs6, bits, self.rows, self.count, self.greedy)
+            return self.greedy
         if self.feat is None:
             self.feat = torch.zeros(self.n, LD, dtype=torch.bfloat16, device=self.rows.device)
         # the stem reads the list's length on the device: it runs while the host waits for it

@@ -9,6 +9,7 @@
 # records of profiles/pmc_k_step.json.
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+export PYTHONPATH="$GRAFT_REPO_ROOT/maze-solving-agent-gymnasium_amd:$PYTHONPATH"
 O=gpurun_out/prof
 mkdir -p $O
 ARGS="--steps 300 --warmup 30 --train-steps 0 --no-cpu-baseline"

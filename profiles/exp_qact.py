@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Time the f32-accurate acting forward (mz_qact: k_qact1 + k_qact2) alone: the greedy-row list at
+the training leg's size (0.43 x 65,536 rows, count on the device) and all 65,536 rows, DDQN with
+and without the acting dropout. MZ_LIB_OVERRIDE selects a probe build
+(profiles/build_qact_variant.sh). One JSON line."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "maze-solving-agent-gymnasium_amd"))
+import torch  # noqa: E402
+
+
+def main(tag=""):
+    from mazerl.agents.nets import QNet
+    from mazerl.agents.qact import QAct
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    net = QNet(variant="ddqn").to(dev)
+    qa = QAct(net, seed=1)
+    n = 65536
+    g = torch.Generator(device=dev).manual_seed(0)
+    bits = torch.randint(0, 2**31 - 1, (n, 22), generator=g, device=dev, dtype=torch.int32)
+    obs6 = torch.rand(n, 6, generator=g, device=dev)
+    m = int(0.43 * n)
+    rows = torch.randperm(n, generator=g, device=dev)[:m].to(torch.int32).contiguous()
+    count = torch.tensor([m], dtype=torch.int32, device=dev)
+    greedy = torch.zeros(n, dtype=torch.int64, device=dev)
+    st = torch.cuda.current_stream(dev)
+
+    def timed(fn, iters=30):
+        for _ in range(5):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(iters):
+            fn()
+        e1.record(st)
+        torch.cuda.synchronize()
+        return round(e0.elapsed_time(e1) / iters * 1e3, 1)
+
+    out = {"tag": tag}
+    for drop in (True, False):
+        net.train(drop)
+        out[f"rows_{m}_drop{int(drop)}_us"] = timed(lambda: qa.rows_greedy(obs6, bits, rows, count, greedy))
+        out[f"all_{n}_drop{int(drop)}_us"] = timed(lambda: qa.greedy(obs6, bits, out=greedy))
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])

@@ -113,7 +113,7 @@ def test_trainer_step_uses_greedy_rows():
     for _ in range(3):
         tr.vector_step()
     torch.cuda.synchronize()
-    assert L._rows is not None and 0 < L._rows.last_count <= B
+    assert L._rows is not None and 0 < int(L._rows.count[0]) <= B
     assert int((env.actions < 0).sum()) == 0 and int((env.actions > 3).sum()) == 0
     env.close()
 
