@@ -345,6 +345,20 @@ int mz_difficulty(const uint8_t* grid_host, int32_t h, int32_t w, int32_t sr, in
 int mz_maze_complexity(const uint8_t* grid_host, int32_t h, int32_t w, int32_t sr, int32_t sc,
                        int32_t gr, int32_t gc, double* difficulty_out, double* complexity_out);
 
+/* McClendon difficulty of resident mazes on the GPU, one workgroup per maze (replaces the
+ * per-maze host ComplexityEvaluation(...).difficulty_of_maze() calls of best-of-6 generation,
+ * base_maze_env.py:84-95, maze_complexity_evaluation.py:38-329). For the listed instances
+ * (env_ids_dev NULL = all B): out_dev [n][2] float64 = {prod, sum}, the reference's product
+ * prod_b (C_b + 1) * C_0 and sum sum_b C_b + C_0 BEFORE math.log (the caller takes the log with
+ * the C library, as the reference: difficulty = log(prod), complexity = log(sum)); status_dev
+ * [n] int32: 0 ok, 1 not a perfect maze (cycles / unreachable squares), 2 outside the kernel's
+ * cases (open border squares, straight goal square, all solution points junctions, more points
+ * than the LDS plan holds), 3 invalid (start == goal, bad id, log domain), 4 toroidal — the caller
+ * computes every nonzero-status maze with mz_difficulty. Asynchronous on `stream`.
+ * Returns MZ_EINVAL_SHAPE when the handle's pitch exceeds the kernel's LDS plan (P > 92). */
+int mz_difficulty_batch(mz_handle* h, const int32_t* env_ids_dev, int32_t n, double* out_dev,
+                        int32_t* status_dev, void* stream);
+
 /* The reference's maze-metric suite (MetricsCalculator, metrics_calculator.py:11-133, as used by
  * generation_algos_metrics_evaluations.py:33-45) for the listed euclidean instances (NULL = all B),
  * computed on the GPU from the instances' mazes: out_dev [n][6] float64 = L, DE, D, AC, FDE, BDE

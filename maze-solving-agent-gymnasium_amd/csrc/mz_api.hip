@@ -15,7 +15,8 @@
 
 #include "../../include/mazerl.h"
 #include "mz_common.h"
-#include "mz_kernels.h"
+#include "mz_learner.h"
+#include "mz_mcclendon.h"
 
 struct MzBankStore {  // two banks x the enabled algorithms x sizes x K slots (mz_bank_*)
   int K = 0, nA = 0, nD = 0;
@@ -632,6 +633,20 @@ int mz_maze_metrics(mz_handle* h, const int32_t* env_ids_dev, int32_t n, double*
   if (n < 0 || n > h->d.B) return fail(MZ_EINVAL, "n out of range");
   DeviceGuard g(h->cfg.device);
   MZ_HIP(mz_launch_metrics(h->d, env_ids_dev, n, out_dev, static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
+int mz_difficulty_batch(mz_handle* h, const int32_t* env_ids_dev, int32_t n, double* out_dev,
+                        int32_t* status_dev, void* stream) {
+  if (!h || !out_dev || !status_dev) return fail(MZ_EINVAL, "bad arguments");
+  if (!env_ids_dev) n = h->d.B;
+  if (n < 0 || (!env_ids_dev && n > h->d.B)) return fail(MZ_EINVAL, "n out of range");
+  int mm = 0;
+  if (mz_mcclendon_lds(h->d.P, &mm) > 160 * 1024)
+    return fail(MZ_EINVAL_SHAPE, "maze pitch beyond the difficulty kernel's LDS plan");
+  DeviceGuard g(h->cfg.device);
+  MZ_HIP(mz_launch_mcclendon(h->d, env_ids_dev, n, out_dev, status_dev,
+                             static_cast<hipStream_t>(stream)));
   return MZ_OK;
 }
 

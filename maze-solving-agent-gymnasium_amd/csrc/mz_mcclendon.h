@@ -1,0 +1,15 @@
+// mz_mcclendon.h — McClendon difficulty of resident mazes (mz_mcclendon.hip).
+// Kept out of mz_kernels.h: that header is part of k_step's source hash (bench.py
+// KSTEP_SOURCES), which decides whether the committed PMC traffic record still applies.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "mz_common.h"
+
+// out[i] = {prod, sum} of instance ids[i] (ids null: i); status[i] 0 ok, 1 not a tree, 2 outside
+// the kernel's cases (host restatement), 3 invalid, 4 toroidal
+size_t mz_mcclendon_lds(int P, int* mm);
+hipError_t mz_launch_mcclendon(const MzDev& d, const int32_t* ids, int n, double* out,
+                               int32_t* status, hipStream_t s);

@@ -28,7 +28,7 @@
 #include <mutex>
 #include <unordered_map>
 
-#include "mz_kernels.h"
+#include "mz_learner.h"
 
 // k_adamw's grid: every workgroup takes one same-address ticket (publish_step), and those atomics
 // serialise at ~30 ns each — 2,048 workgroups of 256 made the launch 78 us alone (106 us per

@@ -27,7 +27,7 @@
 #include <math.h>
 #include <stdint.h>
 
-#include "mz_kernels.h"
+#include "mz_learner.h"
 
 namespace {
 
@@ -36,16 +36,20 @@ constexpr int CONV_OUT = 1568;     // 32 channels x 7 x 7 pooled positions
 constexpr int K1 = 1600;           // fc1 input row as prepared: features | obs6 | zero pad
 constexpr int N1 = 1024, N2 = 512;
 constexpr int NCH = K1 / 32;       // 50 K chunks: 49 pooled positions + obs6
-// k_qact1: QW1 waves per workgroup (4 column quarters x QW1 / 4 row halves of 64 rows); 4-wave
-// workgroups let two independent workgroups share a CU (their barrier phases drift apart, so one
-// runs MFMAs while the other waits on LDS / VALU work)
+// k_qact1: 64 rows per workgroup, QW1 waves of 64 fc1 outputs each (64 QW1 outputs per
+// workgroup); the 16 conv tiles of the 64 rows are spread over the waves. 4-wave workgroups let
+// two independent workgroups share a CU (their barrier phases drift apart, so one runs MFMAs
+// while the other waits on LDS / VALU work); 8 waves halve each wave's conv work instead
 #ifndef MZ_QACT_WAVES
-#define MZ_QACT_WAVES 4
+#define MZ_QACT_WAVES 8
 #endif
 constexpr int QW1 = MZ_QACT_WAVES;
 constexpr int T1 = 64 * QW1;       // k_qact1 threads
-constexpr int RT1 = 16 * QW1;      // k_qact1 rows per workgroup (4 conv tiles of 4 rows per wave)
-constexpr int NT1 = 256;           // k_qact1 fc1 outputs per workgroup
+constexpr int RT1 = 64;            // k_qact1 rows per workgroup
+constexpr int NT1 = 64 * QW1;      // k_qact1 fc1 outputs per workgroup
+constexpr int TPW = 16 / QW1;      // conv tiles (4 rows each) per wave
+constexpr int NTL1 = N1 / NT1;     // fc1 output tiles
+constexpr int XPT = 8 / NTL1;      // XCDs per output tile
 constexpr int PR = 17;             // padded window rows per instance
 constexpr int AST = 40;            // LDS A-tile row stride in bf16 (32 + 8: conflict-free b128)
 constexpr int RT2 = 64;            // k_qact2 rows per workgroup
@@ -109,7 +113,7 @@ __device__ inline void mfma_x3(const frag_ab (&ah)[4], const frag_ab (&al)[4], c
 
 // ---- k_qact1 -------------------------------------------------------------------------------
 template <bool DROP>
-__global__ __launch_bounds__(T1) __attribute__((amdgpu_waves_per_eu(8 / QW1, 8 / QW1)))
+__global__ __launch_bounds__(T1) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void k_qact1(MzQAct q, int row_tiles) {
   __shared__ uint4 lut[256];                   // 8 patch bits -> 8 bf16 (0 / 1.0)
   __shared__ uint32_t spread[256];             // 8 bits -> bits at 3i
@@ -121,9 +125,9 @@ void k_qact1(MzQAct q, int row_tiles) {
   const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);
   const int g4 = lane >> 4, c16 = lane & 15;
   // XCD-aware tile map: workgroup b runs on XCD b % 8 (round-robin dispatch); XCD x computes
-  // output tile x / 2, so one XCD's L2 serves one weight slice
+  // output tile x / XPT, so one XCD's L2 serves one weight slice
   const int b = blockIdx.x, x = b & 7;
-  const int nt = x >> 1, rt = ((b >> 3) << 1) | (x & 1);
+  const int nt = x / XPT, rt = (b >> 3) * XPT + (x % XPT);
   if (rt >= row_tiles) return;
   const int m = q.count ? min(q.n, *q.count) : q.n;
   const int r0 = rt * RT1;
@@ -188,14 +192,14 @@ void k_qact1(MzQAct q, int row_tiles) {
   uint32_t rs[4] = {0u, 0u, 0u, 0u};
   if (DROP) {
 #pragma unroll
-    for (int tt = 0; tt < 4; ++tt) {
-      const uint32_t row = (uint32_t)(r0 + 4 * (4 * w + tt) + g4);
+    for (int tt = 0; tt < TPW; ++tt) {
+      const uint32_t row = (uint32_t)(r0 + 4 * (TPW * w + tt) + g4);
       rs[tt] = lowbias32(lowbias32(q.key ^ lowbias32(row)) ^ (uint32_t)c16) | 1u;
     }
   }
 
-  // fc1 tile of this wave: rows 64 rh + 16 i, columns nt * 256 + 64 cq + 16 j
-  const int rh = w >> 2, cq = w & 3;
+  // fc1 tile of this wave: rows 16 i, columns nt * NT1 + 64 cq + 16 j
+  const int cq = w;
   const int col0 = nt * NT1 + cq * 64;
   frag_cd acc[4][4];
 #pragma unroll
@@ -210,14 +214,14 @@ void k_qact1(MzQAct q, int row_tiles) {
                                                       0, NT1 * K1 * 2, 0x00020000);
   const auto rs_l = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(q.w1l) + (size_t)nt * NT1 * K1,
                                                       0, NT1 * K1 * 2, 0x00020000);
-  const int boff = (cq * 4 * 64 + lane) * 16;  // bytes within a chunk's 16 KB
+  const int boff = (cq * 4 * 64 + lane) * 16;  // bytes within a chunk's QW1 x 4 KB
   auto load_b = [&](int c, uint4* dh, uint4* dl) {
 #ifdef MZ_QPROBE_NO_BLOAD
     if (c > 0) return;
 #endif
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int off = boff + c * (4 * 4 * 64 * 16) + j * (64 * 16);
+      const int off = boff + c * (QW1 * 4 * 64 * 16) + j * (64 * 16);
       dh[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs_h, off, 0, 0));
       dl[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs_l, off, 0, 0));
     }
@@ -231,10 +235,10 @@ void k_qact1(MzQAct q, int row_tiles) {
     const int py = c / 7, px = c - py * 7;
     uint16_t* Ah = A[c & 1][0];
     uint16_t* Al = A[c & 1][1];
-    frag_ab a[4];
+    frag_ab a[TPW];
 #pragma unroll
-    for (int tt = 0; tt < 4; ++tt) {
-      const int inst = 4 * (4 * w + tt) + (c16 >> 2), pos = c16 & 3;
+    for (int tt = 0; tt < TPW; ++tt) {
+      const int inst = 4 * (TPW * w + tt) + (c16 >> 2), pos = c16 & 3;
       const int y = 2 * py + (pos >> 1), xx = 2 * px + (pos & 1);
       const uint64_t* cr = crow + inst * PR + y;
       const uint32_t p = ((uint32_t)(cr[0] >> (3 * xx)) & 0x1FFu) |
@@ -253,27 +257,27 @@ void k_qact1(MzQAct q, int row_tiles) {
       a[tt] = __builtin_bit_cast(frag_ab, lut[(p >> (8 * g4)) & 0xFFu]);
 #endif
     }
-    frag_cd e[4], o[4];
+    frag_cd e[TPW], o[TPW];
 #pragma unroll
-    for (int tt = 0; tt < 4; ++tt) {
+    for (int tt = 0; tt < TPW; ++tt) {
       e[tt] = frag_cd{bias_e, bias_e, bias_e, bias_e};
       o[tt] = frag_cd{bias_o, bias_o, bias_o, bias_o};
     }
 #pragma unroll
-    for (int tt = 0; tt < 4; ++tt) {
+    for (int tt = 0; tt < TPW; ++tt) {
       e[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tt], be_h, e[tt], 0, 0, 0);
       o[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tt], bo_h, o[tt], 0, 0, 0);
     }
 #pragma unroll
-    for (int tt = 0; tt < 4; ++tt) {
+    for (int tt = 0; tt < TPW; ++tt) {
       e[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tt], be_l, e[tt], 0, 0, 0);
       o[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tt], bo_l, o[tt], 0, 0, 0);
     }
 #pragma unroll
-    for (int tt = 0; tt < 4; ++tt) {
+    for (int tt = 0; tt < TPW; ++tt) {
       // lane: pooled output of instance 4t + g4, channels 2 c16 (e) and 2 c16 + 1 (o);
       // registers = the 4 positions of its 2x2 window
-      const int il = 4 * (4 * w + tt) + g4;
+      const int il = 4 * (TPW * w + tt) + g4;
       float ve, vo;
       if (DROP) {
         // MaxPool(Dropout(LeakyReLU(x))) = scale * leaky(max_r x'_r), x'_r = x_r kept, 0
@@ -331,7 +335,7 @@ void k_qact1(MzQAct q, int row_tiles) {
     const uint16_t* Al = A[c & 1][1];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int r = 64 * rh + 16 * i + c16;
+      const int r = 16 * i + c16;
       ah[i] = __builtin_bit_cast(frag_ab, *reinterpret_cast<const uint4*>(Ah + r * AST + 8 * g4));
       al[i] = __builtin_bit_cast(frag_ab, *reinterpret_cast<const uint4*>(Al + r * AST + 8 * g4));
     }
@@ -402,7 +406,7 @@ void k_qact1(MzQAct q, int row_tiles) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = 64 * rh + 16 * i + 4 * g4 + r;
+        const int row = 16 * i + 4 * g4 + r;
         if (row < nr) q.h1[(size_t)(r0 + row) * N1 + col] = leaky(acc[i][j][r] + bb);
       }
   }
@@ -575,7 +579,7 @@ __global__ void k_qact_prepare(const float* __restrict__ w1, const float* __rest
     float v;
     uint16_t *ph, *pl;
     if (e < n1) {
-      const int cq = (int)(rest & 3), c = (int)((rest >> 2) % NCH), nt = (int)((rest >> 2) / NCH);
+      const int cq = (int)(rest % QW1), c = (int)((rest / QW1) % NCH), nt = (int)((rest / QW1) / NCH);
       const int r = nt * NT1 + cq * 64 + 16 * j + (lane & 15);  // fc1 output
       const int f = 32 * c + 8 * (lane >> 4) + el;                // kernel feature order
       int src = -1;
@@ -603,8 +607,8 @@ int mz_qact_row_tiles(int n) { return (n + RT1 - 1) / RT1; }
 hipError_t mz_launch_qact(const MzQAct& q, int relu, hipStream_t s) {
   if (q.n <= 0) return hipSuccess;
   const int rt = (q.n + RT1 - 1) / RT1;
-  // 8 workgroups per pair of row tiles: XCD x takes output tile x / 2 of row tile 2 k + (x & 1)
-  const int blocks1 = 8 * ((rt + 1) / 2);
+  // 8 workgroups per XPT row tiles: XCD x takes output tile x / XPT of row tile XPT k + x % XPT
+  const int blocks1 = 8 * ((rt + XPT - 1) / XPT);
   if (q.drop_thresh)
     hipLaunchKernelGGL(k_qact1<true>, dim3(blocks1), dim3(T1), 0, s, q, rt);
   else

@@ -29,7 +29,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "mz_kernels.h"
+#include "mz_learner.h"
 
 namespace {
 

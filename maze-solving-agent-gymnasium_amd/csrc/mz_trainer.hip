@@ -24,7 +24,7 @@
 #include <stdint.h>
 
 #include "mz_common.h"
-#include "mz_kernels.h"
+#include "mz_learner.h"
 
 namespace {
 

@@ -161,27 +161,24 @@ def make_env(num_envs, dims, toroidal=False, algorithm="r-prim", seed=0x5EED0000
 def best_of_mazes(num_mazes, dim, algorithm="r-prim", seed=0x7E57, device=None, candidates=6):
     """The reference's maze selection for new mazes (BaseMazeEnv.generate_maze,
     base_maze_env.py:78-97): per maze, `candidates` generated mazes, keep the one with the
-    smallest McClendon difficulty (strict <: the first minimum; native mz_difficulty). The
-    candidates are GPU-generated (Philox); returns (grids uint8 [n, dim, dim], start_goal [n, 4])
-    for VectorMazeEnv.load_mazes."""
+    smallest McClendon difficulty (strict <: the first minimum). The candidates are GPU-generated
+    (Philox) and scored on the GPU in one launch (mz_difficulty_batch, one workgroup per maze;
+    host mz_difficulty for the mazes it declines); returns (grids uint8 [n, dim, dim],
+    start_goal [n, 4]) for VectorMazeEnv.load_mazes."""
     import numpy as np
-    from ..difficulty import maze_difficulty
+    from ..difficulty import difficulty_batch
     cand = VectorMazeEnv(num_mazes * candidates, dim, enrich=True, device=device,
                          algorithm=algorithm, seed=seed, done_list=False, pos=False, window=False,
                          window_bits=False)
+    d = difficulty_batch(cand).reshape(num_mazes, candidates)
+    pick = d.argmin(axis=1)  # first minimum (NaN-free: a log domain error raises on the host)
     grids = np.zeros((num_mazes, dim, dim), np.uint8)
     sg = np.zeros((num_mazes, 4), np.int32)
     for k in range(num_mazes):
-        best = None
-        for c in range(candidates):
-            i = k * candidates + c
-            q = cand.query(i)
-            g = cand.grid(i)
-            s, t = (q["start_r"], q["start_c"]), (q["goal_r"], q["goal_c"])
-            d = maze_difficulty(g, s, t)
-            if best is None or d < best[0]:
-                best = (d, g, s + t)
-        grids[k], sg[k] = best[1], best[2]
+        i = k * candidates + int(pick[k])
+        q = cand.query(i)
+        grids[k] = cand.grid(i)
+        sg[k] = (q["start_r"], q["start_c"], q["goal_r"], q["goal_c"])
     cand.close()
     return grids, sg
 

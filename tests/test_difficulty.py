@@ -45,3 +45,20 @@ def test_complexity_evaluation_dropin_matches_reference(diff):
         assert math.isfinite(ce.complexity_of_maze())
         n += 1
     assert n >= 90  # the euclidean fixtures with a reference difficulty (N <= 41)
+
+
+def test_difficulty_81x81_matches_reference(diff):
+    """The headline size: the 24 reference 81x81 mazes of gen_euclid.npz against the values the
+    reference's ComplexityEvaluation computed for them (tests/golden/difficulty81.npz, made by
+    tests/golden/make_golden_difficulty81.py) — difficulty and complexity, same tolerance."""
+    z = G.load("difficulty81.npz")
+    allm = G.mazes("gen_euclid.npz")
+    exact = 0
+    for k, i in enumerate(z["index"]):
+        m = allm[int(i)]
+        assert m["n"] == 81
+        d, c = diff.maze_complexity(m["grid"], m["start"], m["goal"])
+        assert d == pytest.approx(float(z["difficulty"][k]), rel=1e-15, abs=0), k
+        assert c == pytest.approx(float(z["complexity"][k]), rel=1e-15, abs=0), k
+        exact += int(d == z["difficulty"][k]) + int(c == z["complexity"][k])
+    assert len(z["index"]) == 24 and exact >= 40
