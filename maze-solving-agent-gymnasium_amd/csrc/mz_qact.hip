@@ -39,9 +39,12 @@ constexpr int NCH = K1 / 32;       // 50 K chunks: 49 pooled positions + obs6
 // k_qact1: 64 rows per workgroup, QW1 waves of 64 fc1 outputs each (64 QW1 outputs per
 // workgroup); the 16 conv tiles of the 64 rows are spread over the waves. 4-wave workgroups let
 // two independent workgroups share a CU (their barrier phases drift apart, so one runs MFMAs
-// while the other waits on LDS / VALU work); 8 waves halve each wave's conv work instead
+// while the other waits on LDS / VALU work); 8 waves halve each wave's conv work instead: faster
+// alone (all 65,536 rows 899 vs 1,053 us) but slower inside training, where the update stream's
+// kernels share the CUs (53.0 / 53.2 vs 55.3 / 55.7 M env steps/s, same box interleaved,
+// profiles/r03n_qact_waves_ab.json)
 #ifndef MZ_QACT_WAVES
-#define MZ_QACT_WAVES 8
+#define MZ_QACT_WAVES 4
 #endif
 constexpr int QW1 = MZ_QACT_WAVES;
 constexpr int T1 = 64 * QW1;       // k_qact1 threads

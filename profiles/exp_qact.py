@@ -41,6 +41,11 @@ def main(tag=""):
         return round(e0.elapsed_time(e1) / iters * 1e3, 1)
 
     out = {"tag": tag}
+    if tag == "prof":  # profiler runs: all 65,536 rows with the acting dropout (DDQN) only
+        net.train(True)
+        out[f"all_{n}_drop1_us"] = timed(lambda: qa.greedy(obs6, bits, out=greedy))
+        print(json.dumps(out), flush=True)
+        return
     for drop in (True, False):
         net.train(drop)
         out[f"rows_{m}_drop{int(drop)}_us"] = timed(lambda: qa.rows_greedy(obs6, bits, rows, count, greedy))
