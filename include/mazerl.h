@@ -345,20 +345,6 @@ int mz_difficulty(const uint8_t* grid_host, int32_t h, int32_t w, int32_t sr, in
 int mz_maze_complexity(const uint8_t* grid_host, int32_t h, int32_t w, int32_t sr, int32_t sc,
                        int32_t gr, int32_t gc, double* difficulty_out, double* complexity_out);
 
-/* The learners' f32 GEMM in split precision (bf16x3 on the bf16 MFMA): C[m][n] =
- * act(sum_k A(m,k) B(n,k) + bias[n]) with A(m,k) = a[m*a_rs + k*a_ks] and B(n,k) =
- * b[n*b_rs + k*b_ks] (one unit stride per operand, any alignment), act 0 none / 1 LeakyReLU(0.01)
- * / 2 ReLU, bias f32 [n] or NULL, C rows ldc apart. Each product is Ah Bh + Ah Bl + Al Bh of the
- * operands' bf16 hi / lo halves, accumulated in f32 (relative error ~2^-16 per product; replaces
- * the f32 GEMMs of the Linear layers' forward / dX / dW in optimize_model, dqn_agent.py:121-157,
- * ppo_agent.py:206-237). ws: 16-B aligned device workspace of mz_gemm_x3_workspace(m, n, k)
- * floats (the operands' bf16 images and split-K partial sums, summed in split order).
- * Asynchronous on `stream`; deterministic. */
-int mz_gemm_x3_workspace(int32_t m, int32_t n, int32_t k, int64_t* floats_out);
-int mz_gemm_x3(const float* a, int64_t a_rs, int64_t a_ks, const float* b, int64_t b_rs,
-               int64_t b_ks, float* c, int64_t ldc, const float* bias, int32_t m, int32_t n,
-               int32_t k, int32_t act, float* ws, void* stream);
-
 /* McClendon difficulty of resident mazes on the GPU, one workgroup per maze (replaces the
  * per-maze host ComplexityEvaluation(...).difficulty_of_maze() calls of best-of-6 generation,
  * base_maze_env.py:84-95, maze_complexity_evaluation.py:38-329). For the listed instances

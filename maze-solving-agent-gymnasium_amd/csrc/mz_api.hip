@@ -17,7 +17,6 @@
 #include "mz_common.h"
 #include "mz_learner.h"
 #include "mz_mcclendon.h"
-#include "mz_gemm.h"
 
 struct MzBankStore {  // two banks x the enabled algorithms x sizes x K slots (mz_bank_*)
   int K = 0, nA = 0, nD = 0;
@@ -634,29 +633,6 @@ int mz_maze_metrics(mz_handle* h, const int32_t* env_ids_dev, int32_t n, double*
   if (n < 0 || n > h->d.B) return fail(MZ_EINVAL, "n out of range");
   DeviceGuard g(h->cfg.device);
   MZ_HIP(mz_launch_metrics(h->d, env_ids_dev, n, out_dev, static_cast<hipStream_t>(stream)));
-  return MZ_OK;
-}
-
-int mz_gemm_x3_workspace(int32_t m, int32_t n, int32_t k, int64_t* floats_out) {
-  if (!floats_out || m <= 0 || n <= 0 || k <= 0) return fail(MZ_EINVAL, "bad arguments");
-  *floats_out = (int64_t)mz_gemm_ws_floats(m, n, k);
-  return MZ_OK;
-}
-
-int mz_gemm_x3(const float* a, int64_t a_rs, int64_t a_ks, const float* b, int64_t b_rs,
-               int64_t b_ks, float* c, int64_t ldc, const float* bias, int32_t m, int32_t n,
-               int32_t k, int32_t act, float* ws, void* stream) {
-  if (!a || !b || !c || !ws || m <= 0 || n <= 0 || k <= 0 || act < 0 || act > 2)
-    return fail(MZ_EINVAL, "bad arguments");
-  if ((a_rs != 1 && a_ks != 1) || (b_rs != 1 && b_ks != 1))
-    return fail(MZ_EINVAL, "each operand needs a unit stride (rows or k)");
-  if ((uintptr_t)ws & 15) return fail(MZ_EALIGN, "mz_gemm_x3: workspace must be 16-B aligned");
-  MzGemm g{};
-  g.a = a; g.a_rs = a_rs; g.a_ks = a_ks;
-  g.b = b; g.b_rs = b_rs; g.b_ks = b_ks;
-  g.c = c; g.ldc = ldc; g.bias = bias; g.ws_img = ws; g.M = m; g.N = n; g.K = k; g.act = act;
-  StreamGuard sg(stream);
-  MZ_HIP(mz_launch_gemm_x3(g, static_cast<hipStream_t>(stream)));
   return MZ_OK;
 }
 

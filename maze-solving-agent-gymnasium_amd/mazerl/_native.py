@@ -37,7 +37,7 @@ MZ_ERRORS = {-1: ValueError, -2: ValueError, -3: RuntimeError, -4: MemoryError, 
 EXPORTS = ["mz_last_error", "mz_device_count", "mz_create", "mz_destroy", "mz_load_mazes",
            "mz_generate", "mz_generate_ex", "mz_generate_state", "mz_reset_all", "mz_reset_list", "mz_reset_done", "mz_step", "mz_step_ex", "mz_direction_mask",
            "mz_act", "mz_step_act", "mz_expand_window", "mz_set_algorithm", "mz_query", "mz_get_grid",
-           "mz_difficulty", "mz_maze_complexity", "mz_maze_metrics", "mz_difficulty_batch", "mz_gemm_x3", "mz_gemm_x3_workspace", "mz_get_meta", "mz_discounted_returns", "mz_q_front",
+           "mz_difficulty", "mz_maze_complexity", "mz_maze_metrics", "mz_difficulty_batch", "mz_get_meta", "mz_discounted_returns", "mz_q_front",
            "mz_bank_create", "mz_bank_create_dims", "mz_bank_fill", "mz_bank_use",
            "mz_bank_consumed",
            "mz_stem_forward", "mz_stem_backward", "mz_stem_workspace_floats", "mz_adamw_flat",
@@ -96,9 +96,6 @@ def load(build_if_missing=True):
     L.mz_maze_complexity.argtypes = [vp] + [C.c_int32] * 6 + [C.POINTER(C.c_double)] * 2
     L.mz_maze_metrics.argtypes = [vp, vp, C.c_int32, vp, vp]
     L.mz_difficulty_batch.argtypes = [vp, vp, C.c_int32, vp, vp, vp]
-    L.mz_gemm_x3_workspace.argtypes = [C.c_int32] * 3 + [C.POINTER(C.c_int64)]
-    L.mz_gemm_x3.argtypes = [vp, C.c_int64, C.c_int64, vp, C.c_int64, C.c_int64, vp, C.c_int64, vp,
-                             C.c_int32, C.c_int32, C.c_int32, C.c_int32, vp, vp]
     L.mz_bank_create.argtypes = [vp, C.c_int32, C.c_int32, C.c_uint32]
     L.mz_bank_create_dims.argtypes = [vp, C.c_int32, vp, C.c_int32, C.c_uint32]
     L.mz_bank_fill.argtypes = [vp, C.c_int32, C.c_uint64, vp]

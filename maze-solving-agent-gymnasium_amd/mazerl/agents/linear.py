@@ -20,42 +20,12 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 
-_WS = {}
-
-
-def mm_x3(a, b, bias=None, act=0, out=None):
-    """a @ b.T (+ bias, act 0 / 1 LeakyReLU(0.01) / 2 ReLU) for f32 2-D views a [M, K], b [N, K]
-    with one unit stride each, on the bf16 MFMA in split precision (mz_gemm_x3: hi*hi + hi*lo +
-    lo*hi, f32 accumulate). out: [M, N] with unit column stride (default: a new tensor)."""
-    from .. import _native as N
-    M, K = a.shape
-    Nn = b.shape[0]
-    if out is None:
-        out = torch.empty(M, Nn, dtype=torch.float32, device=a.device)
-    lib = N.load()
-    key = (M, Nn, K)
-    if key not in _WS:
-        f = N.C.c_int64()
-        N.check(lib.mz_gemm_x3_workspace(M, Nn, K, N.C.byref(f)))
-        _WS[key] = f.value
-    ws = torch.empty(_WS[key], dtype=torch.float32, device=a.device)
-    N.check(lib.mz_gemm_x3(a.data_ptr(), a.stride(0), a.stride(1), b.data_ptr(), b.stride(0),
-                           b.stride(1), out.data_ptr(), out.stride(0),
-                           bias.data_ptr() if bias is not None else None, M, Nn, K, int(act),
-                           ws.data_ptr(),
-                           torch.cuda.current_stream(a.device).cuda_stream))
-    return out
-
-
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, n_grad=None, x3=False):
+    def forward(ctx, x, w, b, n_grad=None):
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
         ctx.n_grad = n_grad
-        ctx.x3 = x3
-        if x3:
-            return mm_x3(x, w, b.detach() if b is not None else None)
         return F.linear(x, w, b)
 
     @staticmethod
@@ -64,26 +34,20 @@ class _LinearFn(torch.autograd.Function):
         n = ctx.n_grad
         part = n is not None and n < gy.shape[0]
         gy_n, x_n = (gy[:n], x[:n]) if part else (gy, x)
-        x3 = ctx.x3
         gx = None
         if ctx.needs_input_grad[0]:
             if part:
                 # rows >= n are left unwritten: every consumer below a forward_rows pass (the
                 # activation, this class and the stem with the same n_grad) reads rows < n only
                 gx = torch.empty(x.shape, dtype=gy.dtype, device=gy.device)
-                if x3:
-                    mm_x3(gy_n, w.t(), out=gx[:n])
-                else:
-                    torch.mm(gy_n, w, out=gx[:n])
+                torch.mm(gy_n, w, out=gx[:n])
             else:
-                gx = mm_x3(gy, w.t()) if x3 else gy @ w
-        gw = None
-        if ctx.needs_input_grad[1]:
-            gw = mm_x3(gy_n.t(), x_n.t()) if x3 else gy_n.t() @ x_n
+                gx = gy @ w
+        gw = gy_n.t() @ x_n if ctx.needs_input_grad[1] else None
         gb = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
             gb = _bias_grad(gy_n)
-        return gx, gw, gb, None, None
+        return gx, gw, gb, None
 
 
 def _bias_grad(gy):
@@ -101,28 +65,7 @@ def _bias_grad(gy):
 
 
 class GraphSafeLinear(nn.Linear):
-    """`gemm = "x3"` (set by the learners on their large layers, LEARNER_GEMM): forward, dX and dW
-    through mz_gemm_x3 (bf16x3 split precision) instead of f32 hipBLASLt GEMMs."""
-    gemm = "f32"
-
-    def _x3(self, x):
-        return self.gemm == "x3" and x.is_cuda and x.dtype == torch.float32 and \
-            self.in_features % 2 == 0 and self.out_features % 2 == 0
-
     def forward(self, x, n_grad=None):
         if x.is_cuda and x.dim() == 2 and torch.is_grad_enabled() and self.weight.requires_grad:
-            return _LinearFn.apply(x, self.weight, self.bias, n_grad, self._x3(x))
-        if x.dim() == 2 and self._x3(x):
-            return mm_x3(x, self.weight.detach(), self.bias.detach() if self.bias is not None else None)
+            return _LinearFn.apply(x, self.weight, self.bias, n_grad)
         return F.linear(x, self.weight, self.bias)
-
-
-def set_learner_gemm(net, mode, min_features=64):
-    """Route the GEMMs of `net`'s GraphSafeLinear layers with both dimensions >= min_features
-    (fc1 / fc2 of the reference's heads; the 4- and 1-wide output layers stay f32) through
-    mode "x3" (mz_gemm_x3) or "f32" (torch / hipBLASLt)."""
-    for m in net.modules():
-        if isinstance(m, GraphSafeLinear):
-            big = m.in_features >= min_features and m.out_features >= min_features
-            m.gemm = mode if big else "f32"
-    return net

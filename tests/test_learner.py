@@ -20,7 +20,7 @@ def fx():
     return G.load("learner.npz")
 
 
-def run_ours(case, device, gemm="f32"):
+def run_ours(case, device):
     variant, h, hid, n, gamma, lr, train = U.CASES[case]
     src = QNet(3, 6, 4, h, hid, variant)
     tgt = QNet(3, 6, 4, h, hid, variant)
@@ -28,10 +28,6 @@ def run_ours(case, device, gemm="f32"):
     U.fill_params(tgt, 22)
     src.to(device)
     tgt.to(device)
-    if gemm != "f32":
-        from mazerl.agents.linear import set_learner_gemm
-        set_learner_gemm(src, gemm, min_features=2)
-        set_learner_gemm(tgt, gemm, min_features=2)
     if not train:
         src.eval()
         tgt.eval()
@@ -83,16 +79,6 @@ def test_q_loss_matches_reference_gpu(fx, case):
     torch.backends.cuda.matmul.allow_tf32 = False
     torch.backends.cudnn.allow_tf32 = False
     src, loss = run_ours(case, "cuda")
-    _compare(fx, case, src, loss, "cuda")
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("case", [c for c in U.CASES if not U.CASES[c][6]])
-def test_q_loss_matches_reference_gpu_x3(fx, case):
-    """The same reference fixtures with every even-sized Linear GEMM (forward, dX, dW) in bf16x3
-    split precision (mz_gemm_x3) — the same tolerances as the f32 GPU path."""
-    src, loss = run_ours(case, "cuda", gemm="x3")
-    assert any(getattr(m, "gemm", "f32") == "x3" for m in src.modules())
     _compare(fx, case, src, loss, "cuda")
 
 
