@@ -36,6 +36,9 @@ def parse(argv=None):
     ap.add_argument("--target-every", type=int, default=13)
     ap.add_argument("--eval-mazes", type=int, default=1000)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--curriculum", action="store_true",
+                    help="change_algorithm per instance (off_policy_trainer.py:302-310): prim&kill "
+                         "from the 5th win, dfs from the 10th, epsilon_decay *3 / *4")
     ap.add_argument("--log-every", type=int, default=50)
     ap.add_argument("--overlap", type=int, default=1,
                     help="1: updates on a side HIP stream (acting one update behind); 0: sequential")
@@ -66,7 +69,7 @@ def main(argv=None):
     if world > 1:
         broadcast_params(learner.source)
         learner.target.load_state_dict(learner.source.state_dict())
-    trainer = VectorOffPolicyTrainer(env, learner, seed=a.seed + 7919 * rank)
+    trainer = VectorOffPolicyTrainer(env, learner, seed=a.seed + 7919 * rank, curriculum=a.curriculum)
     secs = trainer.train(a.steps, log_every=a.log_every if rank == 0 else 0,
                          log=(lambda r: print(json.dumps(r), flush=True)) if rank == 0 else None)
     stats = torch.stack([trainer.wins, trainer.episodes]).to(torch.float64)

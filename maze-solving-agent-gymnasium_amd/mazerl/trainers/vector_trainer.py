@@ -48,6 +48,23 @@ class VectorOffPolicyTrainer:
         self._eps = None  # the next step's epsilon, computed at the end of the previous step
         self.history = []
 
+    def _change_algorithm(self, term):
+        """NeuralOffPolicyTrainer.change_algorithm (off_policy_trainer.py:302-310, called on every
+        win, :201) per instance: at the 5th win epsilon_decay *= 3 and the maze algorithm becomes
+        prim&kill, at the 10th epsilon_decay *= 4 and dfs (steps_done = 0 on every win is the
+        common bookkeeping); the winner's new maze (update_maze, :202) is then drawn with the new
+        algorithm by the reset that follows. The learner's eps_decay becomes a per-instance
+        tensor."""
+        L, dev = self.learner, self.env.device
+        self.inst_wins += term.to(torch.int32)
+        if not torch.is_tensor(L.eps_decay):
+            L.eps_decay = torch.full((self.env.num_envs,), float(L.eps_decay), device=dev)
+        w = self.inst_wins
+        L.eps_decay.mul_(torch.where(term & (w == 5), 3.0, torch.where(term & (w == 10), 4.0, 1.0)))
+        self.algo = torch.where(w >= 10, ALGOS["dfs"],
+                                torch.where(w >= 5, ALGOS["prim&kill"], ALGOS["r-prim"])).to(torch.uint8)
+        self.env.set_algorithm(self.algo)
+
     def _expand(self, bits):
         return self.env.expand_window(bits)
 
@@ -84,10 +101,7 @@ class VectorOffPolicyTrainer:
             self.wins += term.sum()
             self.episodes += (term | env.truncated.bool()).sum()
             if self.curriculum:  # change_algorithm (off_policy_trainer.py:302-310), per instance
-                self.inst_wins += term.to(torch.int32)
-                algo = torch.where(self.inst_wins >= 10, ALGOS["dfs"],
-                                   torch.where(self.inst_wins >= 5, ALGOS["prim&kill"], ALGOS["r-prim"]))
-                env.set_algorithm(algo.to(torch.uint8))
+                self._change_algorithm(term)
         if ring:
             rp.push_rest(env.actions, env.reward, env.obs6, env.window_bits)
         else:
