@@ -44,6 +44,16 @@ def main():
         torch.cuda.synchronize()
         rec = {"gpu_kernel_ms": e0.elapsed_time(e1) / reps,
                "status_nonzero": int((st != 0).sum())}
+        # near ties: relative gap between the smallest and the second smallest difficulty of
+        # each group of 6 candidates (a 1-ulp difference could flip the choice only below ~2e-16)
+        import math
+        import numpy as np
+        d = np.array([math.log(x) for x in res[:, 0].cpu().tolist()]).reshape(1000, 6)
+        srt = np.sort(d, axis=1)
+        gap = (srt[:, 1] - srt[:, 0]) / np.abs(srt[:, 0])
+        rec["best_of_6_min_rel_gap"] = float(gap.min())
+        rec["groups_gap_below_1e-12"] = int((gap < 1e-12).sum())
+        rec["groups_exact_tie"] = int((gap == 0).sum())
         t0 = time.perf_counter()
         for i in range(300):
             q = env.query(i)
