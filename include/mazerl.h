@@ -500,6 +500,20 @@ int mz_ppo_finish(const double* rec_r_dev, const float* rec_s6_dev, const uint32
                   int64_t capacity, float* pool_s6_dev, uint32_t* pool_w_dev, int64_t* pool_a_dev,
                   float* pool_lp_dev, float* pool_adv_dev, float* pool_ret_dev, void* stream);
 
+/* The PPO minibatch loss in three launches (ppo_agent.py:188-203 through ActorCriticNet.evaluate,
+ * :55-66, and optimize_model's total = policy + 0.5 value, :222-224): for b rows of 4 action
+ * logits (row stride ldl), value (stride ldv), action, old log-prob, advantage, return and the
+ * entropy coefficient (device scalar): softmax, the action's log_softmax, entropy
+ * -sum p log(p + 1e-8), the clipped surrogate over the reference's [b, b] ratio broadcast
+ * (mz_pair_surrogate), total = -(surrogate + coef * mean entropy) + 0.5 * mean((v - ret)^2) into
+ * loss_dev[0], and d total / d logits (dlogits_dev, row stride ldg) and d total / d value
+ * (dvalue_dev, stride ldvg). scratch_dev: 12 b floats. Sums in a fixed order (deterministic). */
+int mz_ppo_head_loss(const float* logits_dev, int32_t ldl, const float* value_dev, int32_t ldv,
+                     const int64_t* action_dev, const float* lp_old_dev, const float* adv_dev,
+                     const float* ret_dev, const float* coef_dev, int32_t b, float clip,
+                     float* scratch_dev, float* loss_dev, float* dlogits_dev, int32_t ldg,
+                     float* dvalue_dev, int32_t ldvg, void* stream);
+
 /* ---- The DQN / DDQN acting forward, f32-accurate on the bf16 MFMA (mz_qact.hip) -------------
  * Replaces, per acting row, source_net(state).max(1)[1] (dqn_agent.py:113-116; the nets of
  * dqn_agent.py:19-57 / ddqn_agent.py:18-52 at the reference's sizes: Conv2d(3, 32, 3, p 1),

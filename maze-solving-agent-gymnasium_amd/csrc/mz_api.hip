@@ -916,6 +916,24 @@ int mz_ppo_finish(const double* rec_r_dev, const float* rec_s6_dev, const uint32
   return MZ_OK;
 }
 
+int mz_ppo_head_loss(const float* logits_dev, int32_t ldl, const float* value_dev, int32_t ldv,
+                     const int64_t* action_dev, const float* lp_old_dev, const float* adv_dev,
+                     const float* ret_dev, const float* coef_dev, int32_t b, float clip,
+                     float* scratch_dev, float* loss_dev, float* dlogits_dev, int32_t ldg,
+                     float* dvalue_dev, int32_t ldvg, void* stream) {
+  if (!logits_dev || !value_dev || !action_dev || !lp_old_dev || !adv_dev || !ret_dev ||
+      !coef_dev || !scratch_dev || !loss_dev || !dlogits_dev || !dvalue_dev || b < 0 || ldl < 4 ||
+      ldg < 4 || ldv < 1 || ldvg < 1)
+    return fail(MZ_EINVAL, "bad arguments");
+  StreamGuard g(stream);
+  float* w = scratch_dev;
+  MzPpoHead q{logits_dev, ldl, value_dev, ldv, action_dev, lp_old_dev, adv_dev, ret_dev, coef_dev,
+              b, w, w + b, w + 2 * (size_t)b, w + 6 * (size_t)b, w + 10 * (size_t)b,
+              w + 11 * (size_t)b, loss_dev, dlogits_dev, ldg, dvalue_dev, ldvg};
+  MZ_HIP(mz_launch_ppo_head(q, clip, static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
 int mz_qact_prepare(const float* fc1_w_dev, const float* fc2_w_dev, uint16_t* w1_hi_dev,
                     uint16_t* w1_lo_dev, uint16_t* w2_hi_dev, uint16_t* w2_lo_dev, void* stream) {
   if (!fc1_w_dev || !fc2_w_dev || !w1_hi_dev || !w1_lo_dev || !w2_hi_dev || !w2_lo_dev)

@@ -92,6 +92,14 @@ struct MzPpoFinish {
 hipError_t mz_launch_ppo_act(const MzPpoAct& q, hipStream_t s);
 hipError_t mz_launch_ppo_scan(const MzPpoScan& q, hipStream_t s);
 hipError_t mz_launch_ppo_finish(const MzPpoFinish& q, int max_episodes, hipStream_t s);
+struct MzPpoHead {  // fused loss of one minibatch (4 actions)
+  const float* logits; int ldl; const float* value; int ldv;
+  const int64_t* action; const float* lp_old; const float* adv; const float* ret;
+  const float* coef; int b;
+  float* lp_new; float* ent; float* p; float* dent; float* part; float* dsum;  // scratch
+  float* loss; float* dlogits; int ldg; float* dvalue; int ldvg;
+};
+hipError_t mz_launch_ppo_head(const MzPpoHead& q, float clip, hipStream_t s);
 
 // ---- f32-accurate acting forward on the bf16 MFMA (mz_qact.hip) ------------------------------
 struct MzQAct {

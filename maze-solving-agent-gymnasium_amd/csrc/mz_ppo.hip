@@ -263,6 +263,90 @@ __global__ __launch_bounds__(FIN_T) void k_ppo_finish(MzPpoFinish q) {
   }
 }
 
+// ---- fused PPO head loss (optimize_model's loss, ppo_agent.py:188-203 via ActorCriticNet.evaluate
+// :55-66): per row softmax / log_softmax / the action's log-prob / entropy and their gradients
+// (k_ppo_head1), the [b, b] clipped surrogate (k_pair_surrogate, mz_optim.hip), then the total
+// loss and d total / d logits, d value in one workgroup (k_ppo_head2, fixed-order sums).
+constexpr float ENT_EPS = 1e-8f;
+
+__global__ __launch_bounds__(256) void k_ppo_head1(MzPpoHead q) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= q.b) return;
+  const float* z = q.logits + (size_t)i * q.ldl;
+  float zz[4], mx = z[0];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    zz[k] = z[k];
+    mx = fmaxf(mx, zz[k]);
+  }
+  float e[4], S = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    e[k] = expf(zz[k] - mx);
+    S += e[k];
+  }
+  const float lS = logf(S);
+  float p[4], g[4], pg = 0.0f, ent = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    p[k] = e[k] / S;
+    const float lp = logf(p[k] + ENT_EPS);
+    ent -= p[k] * lp;
+    g[k] = -(lp + p[k] / (p[k] + ENT_EPS));  // d entropy / d p_k
+    pg += p[k] * g[k];
+  }
+  const int a = (int)q.action[i];
+  q.lp_new[i] = zz[a] - mx - lS;  // log_softmax(z)[a]
+  q.ent[i] = ent;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    q.p[(size_t)i * 4 + k] = p[k];
+    q.dent[(size_t)i * 4 + k] = p[k] * (g[k] - pg);  // d entropy / d z_k through the softmax
+  }
+}
+
+// one workgroup of 1,024: total = -(sum(part) / b^2 + coef * mean(ent)) + 0.5 * mean((v - ret)^2)
+// and its gradients (d total / d lp_new_i = -adv_i dsum_i / b^2)
+__global__ __launch_bounds__(1024) void k_ppo_head2(MzPpoHead q) {
+  __shared__ double red[3][1024];
+  const int tid = threadIdx.x, b = q.b;
+  const float coef = *q.coef;
+  const float inv_b = 1.0f / (float)b, inv_b2 = inv_b * inv_b;
+  double sp = 0.0, se = 0.0, sv = 0.0;
+  for (int i = tid; i < b; i += 1024) {
+    const float v = q.value[(size_t)i * q.ldv], r = q.ret[i];
+    const float dv = v - r;
+    sp += q.part[i];
+    se += q.ent[i];
+    sv += (double)dv * dv;
+    const float dlp = -q.adv[i] * q.dsum[i] * inv_b2;
+    const int a = (int)q.action[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float pk = q.p[(size_t)i * 4 + k];
+      q.dlogits[(size_t)i * q.ldg + k] =
+          dlp * ((k == a ? 1.0f : 0.0f) - pk) - coef * inv_b * q.dent[(size_t)i * 4 + k];
+    }
+    q.dvalue[(size_t)i * q.ldvg] = dv * inv_b;  // 0.5 * d mean((v - r)^2) / dv
+  }
+  red[0][tid] = sp;
+  red[1][tid] = se;
+  red[2][tid] = sv;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if (tid < o) {
+      red[0][tid] += red[0][tid + o];
+      red[1][tid] += red[1][tid + o];
+      red[2][tid] += red[2][tid + o];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const double n = (double)b;
+    *q.loss = (float)(-(red[0][0] / (n * n) + (double)coef * red[1][0] / n) + 0.5 * red[2][0] / n);
+  }
+}
+
 }  // namespace
 
 hipError_t mz_launch_ppo_act(const MzPpoAct& q, hipStream_t s) {
@@ -281,5 +365,14 @@ hipError_t mz_launch_ppo_finish(const MzPpoFinish& q, int max_episodes, hipStrea
   if (max_episodes <= 0) return hipSuccess;
   const int blocks = max_episodes < 2048 ? max_episodes : 2048;
   hipLaunchKernelGGL(k_ppo_finish, dim3(blocks), dim3(FIN_T), 0, s, q);
+  return hipGetLastError();
+}
+
+hipError_t mz_launch_ppo_head(const MzPpoHead& q, float clip, hipStream_t s) {
+  if (q.b <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ppo_head1, dim3((q.b + 255) / 256), dim3(256), 0, s, q);
+  const hipError_t e = mz_launch_pair_surrogate(q.lp_new, q.lp_old, q.adv, q.b, clip, q.part, q.dsum, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_ppo_head2, dim3(1), dim3(1024), 0, s, q);
   return hipGetLastError();
 }

@@ -45,7 +45,7 @@ EXPORTS = ["mz_last_error", "mz_device_count", "mz_create", "mz_destroy", "mz_lo
            "mz_replay_gather", "mz_host_alloc", "mz_host_free", "mz_q_front_rows", "mz_greedy_rows",
            "mz_trainer_tick", "mz_greedy_scatter", "mz_head_bf16", "mz_replay_push",
            "mz_replay_sample_idx", "mz_q_loss", "mz_q_loss_backward", "mz_adamw_groups",
-           "mz_ppo_act", "mz_ppo_scan", "mz_ppo_finish", "mz_qact_prepare", "mz_qact"]
+           "mz_ppo_act", "mz_ppo_scan", "mz_ppo_finish", "mz_ppo_head_loss", "mz_qact_prepare", "mz_qact"]
 
 _lib = None
 
@@ -133,6 +133,8 @@ def load(build_if_missing=True):
     L.mz_ppo_act.argtypes = [vp, C.c_int32, vp, C.c_int32, vp, vp, C.c_int32, C.c_int32,
                              C.c_uint64, C.c_uint64] + [vp] * 8
     L.mz_ppo_scan.argtypes = [vp, vp, vp, C.c_int32, C.c_int32] + [vp] * 10
+    L.mz_ppo_head_loss.argtypes = [vp, C.c_int32, vp, C.c_int32, vp, vp, vp, vp, vp, C.c_int32,
+                                   C.c_float, vp, vp, vp, C.c_int32, vp, C.c_int32, vp]
     L.mz_ppo_finish.argtypes = [vp] * 6 + [C.c_int32, C.c_int32] + [vp] * 4 + \
         [C.c_double, C.c_int64] + [vp] * 7
     L.mz_qact_prepare.argtypes = [vp] * 7

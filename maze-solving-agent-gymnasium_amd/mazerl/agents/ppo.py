@@ -145,14 +145,63 @@ def ppo_losses(logp_old, logp_new, advantages, entropy, returns, value_pred, ent
     return policy_loss, value_loss
 
 
+class _PPOHeadLoss(torch.autograd.Function):
+    """evaluate() + ppo_losses() + total = policy + 0.5 value (ppo_agent.py:55-66, 188-203,
+    222-224) from the heads' outputs in three HIP launches (mz_ppo_head_loss: softmax, the
+    action's log_softmax, entropy, the [b, b] clipped surrogate, value MSE, and d total / d logits,
+    d total / d value computed in the same pass) instead of ~25 small torch kernels forward and
+    backward. Same arithmetic in f32 (the loss sums in float64, fixed order)."""
+
+    @staticmethod
+    def forward(ctx, logits, value, action, lp_old, adv, ret, coef, clip):
+        from .. import _native as N
+        b = logits.shape[0]
+        dev = logits.device
+        logits = logits.contiguous()
+        value = value.contiguous()
+        action = action.reshape(-1).contiguous()
+        lp_old = lp_old.reshape(-1).contiguous().float()
+        adv, ret = adv.contiguous().float(), ret.contiguous().float()
+        if not torch.is_tensor(coef):
+            coef = torch.full((), float(coef), dtype=torch.float32, device=dev)
+        scratch = torch.empty(12 * b, dtype=torch.float32, device=dev)
+        loss = torch.empty(1, dtype=torch.float32, device=dev)
+        dlogits = torch.empty(b, 4, dtype=torch.float32, device=dev)
+        dvalue = torch.empty(b, 1, dtype=torch.float32, device=dev)
+        N.check(N.load().mz_ppo_head_loss(
+            logits.data_ptr(), logits.stride(0), value.data_ptr(), value.stride(0),
+            action.data_ptr(), lp_old.data_ptr(), adv.data_ptr(), ret.data_ptr(), coef.data_ptr(),
+            b, float(clip), scratch.data_ptr(), loss.data_ptr(), dlogits.data_ptr(), 4,
+            dvalue.data_ptr(), 1, torch.cuda.current_stream(dev).cuda_stream))
+        ctx.save_for_backward(dlogits, dvalue)
+        return loss[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        dlogits, dvalue = ctx.saved_tensors
+        return dlogits * g, dvalue * g, None, None, None, None, None, None
+
+
+FUSED_LOSS = os.environ.get("MZ_PPO_FUSED_LOSS", "1") != "0"
+
+
 def ppo_minibatch(net, optimizer, pos, win, act, lp_old, adv, ret, entropy_coef, allreduce=None,
                   phase=None):
     """One minibatch step of optimize_model (ppo_agent.py:217-236). phase "a" / "b" split it
-    around the gradient all-reduce (backward + pack / unpack + clip + step) for graph capture."""
+    around the gradient all-reduce (backward + pack / unpack + clip + step) for graph capture.
+    On the GPU the loss and its gradient w.r.t. the heads' outputs come from the fused
+    _PPOHeadLoss (MZ_PPO_FUSED_LOSS=0: the torch expressions)."""
     if phase != "b":
-        lp_new, value, ent = net.evaluate((pos, win), act)
-        pl, vl = ppo_losses(lp_old, lp_new, adv, ent, ret, value, entropy_coef)
-        total = pl + 0.5 * vl
+        logits, value = net((pos, win))
+        if FUSED_LOSS and logits.is_cuda and logits.shape[1] == 4 and lp_old.dim() == 2:
+            total = _PPOHeadLoss.apply(logits, value, act, lp_old, adv.detach(), ret,
+                                       entropy_coef, 0.3)
+        else:
+            prob = F.softmax(logits, dim=-1)
+            lp_new = F.log_softmax(logits, dim=-1).gather(1, act).squeeze(1)
+            ent = -torch.sum(prob * torch.log(prob + 1e-8), dim=1)
+            pl, vl = ppo_losses(lp_old, lp_new, adv, ent, ret, value, entropy_coef)
+            total = pl + 0.5 * vl
         optimizer.zero_grad()
         total.backward()
         if phase == "a":
@@ -193,60 +242,86 @@ def optimize_model(net, optimizer, states, actions, logp, advantages, returns, e
 class PPOMinibatchGraph:
     """optimize_model's full-size minibatch step (forward of both heads from packed windows,
     the clipped-surrogate / entropy / value losses, backward, clip_grad_norm_(0.5), AdamW) captured
-    once into a HIP graph and replayed: ~250 small kernels per minibatch are launch-bound when
-    issued eagerly. Inputs are copied into static buffers before each replay; the entropy
-    coefficient lives on the device. With a gradient all-reduce it is two graphs with the one
-    RCCL all-reduce between the replays (as the DQN learner, agents/dqn.py). The optimizer must
-    be capturable (make_optimizer(..., capturable=True))."""
+    into HIP graphs and replayed: ~250 small kernels per minibatch are launch-bound when issued
+    eagerly. One graph per minibatch location: the minibatches are fixed slices of the update
+    pool's columns, so each graph reads its slice in place (no copies into static inputs); other
+    inputs (rows re-gathered after a drop) go through one graph with static input buffers. All
+    graphs share one memory pool (they never run concurrently). The entropy coefficient lives on
+    the device. With a gradient all-reduce each location is two graphs with the one RCCL
+    all-reduce between the replays (as the DQN learner, agents/dqn.py). The optimizer must be
+    capturable (make_optimizer(..., capturable=True))."""
+
+    MAX_GRAPHS = 64
 
     def __init__(self, net, optimizer, batch, allreduce=None, warmup=3):
         self.net, self.opt, self.batch, self.allreduce = net, optimizer, batch, allreduce
         self.warmup, self.done_eager = warmup, 0
-        self.graphs = None
+        self.graphs = None           # key -> (graphs tuple, loss tensor)
+        self.pool = None
         self.static = None
         self.coef = None
-        self.loss = None
+        self._coef_val = None
 
-    def _alloc(self, mb):
-        self.static = [torch.empty_like(x) for x in mb]
-        self.coef = torch.zeros((), dtype=torch.float32, device=mb[0].device)
+    @staticmethod
+    def _key(mb):
+        return tuple((x.data_ptr(), tuple(x.shape), tuple(x.stride())) for x in mb)
+
+    def _capture(self, mb):
+        ar = self.allreduce
+        self.opt.zero_grad(set_to_none=True)
+        kw = {} if self.pool is None else {"pool": self.pool}
+        if ar is None:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, **kw):
+                loss = ppo_minibatch(self.net, self.opt, *mb, self.coef)
+            gs = (g,)
+        else:
+            ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(ga, **kw):
+                loss = ppo_minibatch(self.net, self.opt, *mb, self.coef, allreduce=ar, phase="a")
+            with torch.cuda.graph(gb, pool=ga.pool()):
+                ppo_minibatch(self.net, self.opt, *mb, self.coef, allreduce=ar, phase="b")
+            gs = (ga, gb)
+        if self.pool is None:
+            self.pool = gs[0].pool()
+        return gs, loss
 
     def step(self, mb, entropy_coef):
-        if self.static is None:
-            self._alloc(mb)
-        for d, x in zip(self.static, mb):
-            d.copy_(x)
-        self.coef.fill_(float(entropy_coef))
-        ar, dev = self.allreduce, mb[0].device
+        dev = mb[0].device
+        if self.coef is None:
+            self.coef = torch.zeros((), dtype=torch.float32, device=dev)
+        if self._coef_val != float(entropy_coef):  # changes once per update, not per minibatch
+            self.coef.fill_(float(entropy_coef))
+            self._coef_val = float(entropy_coef)
+        ar = self.allreduce
+        if self.done_eager < self.warmup:  # real steps on a side stream before any capture
+            s = torch.cuda.Stream(dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                out = ppo_minibatch(self.net, self.opt, *mb, self.coef, allreduce=ar)
+            torch.cuda.current_stream(dev).wait_stream(s)
+            self.done_eager += 1
+            return out
         if self.graphs is None:
-            if self.done_eager < self.warmup:  # real steps on a side stream before capture
-                s = torch.cuda.Stream(dev)
-                s.wait_stream(torch.cuda.current_stream(dev))
-                with torch.cuda.stream(s):
-                    out = ppo_minibatch(self.net, self.opt, *self.static, self.coef, allreduce=ar)
-                torch.cuda.current_stream(dev).wait_stream(s)
-                self.done_eager += 1
-                return out
-            self.opt.zero_grad(set_to_none=True)
-            if ar is None:
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    self.loss = ppo_minibatch(self.net, self.opt, *self.static, self.coef)
-                self.graphs = (g,)
-            else:
-                ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-                with torch.cuda.graph(ga):
-                    self.loss = ppo_minibatch(self.net, self.opt, *self.static, self.coef,
-                                              allreduce=ar, phase="a")
-                with torch.cuda.graph(gb, pool=ga.pool()):
-                    ppo_minibatch(self.net, self.opt, *self.static, self.coef, allreduce=ar,
-                                  phase="b")
-                self.graphs = (ga, gb)
-        self.graphs[0].replay()
+            self.graphs = {}
+        key = self._key(mb)
+        ent = self.graphs.get(key)
+        if ent is None:
+            if len(self.graphs) < self.MAX_GRAPHS:
+                ent = self.graphs[key] = self._capture(mb)
+            else:  # inputs at new places: copy into the static graph's buffers
+                if self.static is None:
+                    self.static = [torch.empty_like(x) for x in mb]
+                    self.graphs["static"] = self._capture(self.static)
+                for d, x in zip(self.static, mb):
+                    d.copy_(x)
+                ent = self.graphs["static"]
+        gs, loss = ent
+        gs[0].replay()
         if ar is not None:
             ar.reduce()
-            self.graphs[1].replay()
-        return self.loss
+            gs[1].replay()
+        return loss
 
 
 class PPOAgent:

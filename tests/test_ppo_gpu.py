@@ -69,6 +69,42 @@ def test_ppo_graph_minibatches_track_eager(hidden, bs, full):
         assert torch.allclose(pa, pb, rtol=1e-5, atol=1e-5), name
 
 
+@pytest.mark.parametrize("b", [37, 2048])
+def test_fused_head_loss_matches_torch(b):
+    """_PPOHeadLoss (mz_ppo_head_loss) == evaluate() + ppo_losses() + total = pl + 0.5 vl in torch
+    (ppo_agent.py:55-66, 188-203): the loss to 1e-5 relative and every parameter gradient of the
+    actor-critic to 1e-4, with the entropy coefficient as a device scalar (the captured step's)."""
+    import torch.nn.functional as F
+    from mazerl.agents.ppo import ActorCriticNet, _PPOHeadLoss, ppo_losses
+    torch.manual_seed(3)
+    net = ActorCriticNet(3, 6, 4, 32, 256).cuda()
+    g = torch.Generator().manual_seed(4)
+    bits = _bits(b, 5).cuda()
+    s6 = torch.randn(b, 6, generator=g).cuda()
+    act = torch.randint(0, 4, (b, 1), generator=g).cuda()
+    lp_old = (-torch.rand(b, 1, generator=g) * 2).cuda()
+    adv = torch.randn(b, generator=g).cuda()
+    ret = torch.randn(b, generator=g).cuda()
+    coef = torch.tensor(7e-3, device="cuda")
+    out = {}
+    for fused in (False, True):
+        net.zero_grad()
+        logits, value = net((s6, bits))
+        if fused:
+            total = _PPOHeadLoss.apply(logits, value, act, lp_old, adv, ret, coef, 0.3)
+        else:
+            prob = F.softmax(logits, dim=-1)
+            lp_new = F.log_softmax(logits, dim=-1).gather(1, act).squeeze(1)
+            ent = -torch.sum(prob * torch.log(prob + 1e-8), dim=1)
+            pl, vl = ppo_losses(lp_old, lp_new, adv, ent, ret, value, coef)
+            total = pl + 0.5 * vl
+        total.backward()
+        out[fused] = (float(total), [p.grad.clone() for p in net.parameters()])
+    assert out[True][0] == pytest.approx(out[False][0], rel=1e-5, abs=1e-7)
+    for (name, _), x, y in zip(net.named_parameters(), out[False][1], out[True][1]):
+        assert _close(y, x, 1e-4, 1e-6), name
+
+
 def test_pair_surrogate_matches_torch_broadcast():
     """_PairSurrogate (the reference's [b,b] clipped surrogate with a written-out backward)
     against the torch expression it replaces, forward and gradient, incl. ratios on and outside
