@@ -339,12 +339,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local %= max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local)  # before the process group: RCCL binds each rank to its GPU
+    dev = torch.device("cuda", local)
     if world > 1:
         # RCCL ("nccl") on the 8-GPU node; MZ_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs
-        dist.init_process_group(os.environ.get("MZ_DIST_BACKEND", "nccl"), init_method="env://")
-    local %= max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        backend = os.environ.get("MZ_DIST_BACKEND", "nccl")
+        kw = {"device_id": dev} if backend == "nccl" else {}
+        dist.init_process_group(backend, init_method="env://", **kw)
 
     import mazerl
     B = a.envs

@@ -19,12 +19,17 @@ def init_from_env(backend=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ngpu = torch.cuda.device_count()  # counting does not initialise the GPU
+    if ngpu > 0:
+        local %= ngpu  # rehearsal: several ranks share a GPU
     if world > 1 and not dist.is_initialized():
         if backend is None:  # MZ_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs
-            backend = os.environ.get("MZ_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
-        dist.init_process_group(backend, init_method="env://")
-    if torch.cuda.is_available() and torch.cuda.device_count() > 0:
-        local %= torch.cuda.device_count()  # rehearsal: several ranks share a GPU
+            backend = os.environ.get("MZ_DIST_BACKEND") or ("nccl" if ngpu > 0 else "gloo")
+        kw = {}
+        if backend == "nccl":  # bind each rank's RCCL communicator to its GPU up front
+            torch.cuda.set_device(local)
+            kw["device_id"] = torch.device("cuda", local)
+        dist.init_process_group(backend, init_method="env://", **kw)
     return rank, world, local
 
 
