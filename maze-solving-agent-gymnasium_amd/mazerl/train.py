@@ -40,6 +40,8 @@ def parse(argv=None):
                     help="change_algorithm per instance (off_policy_trainer.py:302-310): prim&kill "
                          "from the 5th win, dfs from the 10th, epsilon_decay *3 / *4")
     ap.add_argument("--log-every", type=int, default=50)
+    ap.add_argument("--acting", default="x3", choices=["x3", "bf16"],
+                    help="acting forward: x3 = f32-accurate bf16x3 MFMA (QAct); bf16 = bf16 head")
     ap.add_argument("--overlap", type=int, default=1,
                     help="1: updates on a side HIP stream (acting one update behind); 0: sequential")
     return ap.parse_args(argv)
@@ -65,7 +67,7 @@ def main(argv=None):
                                batch_size=a.batch, capacity=a.capacity,
                                updates_per_step=a.updates_per_step, target_every=a.target_every,
                                allreduce=GradAllReduce() if world > 1 else None, seed=a.seed,
-                               overlap=bool(a.overlap))
+                               overlap=bool(a.overlap), acting=a.acting)
     if world > 1:
         broadcast_params(learner.source)
         learner.target.load_state_dict(learner.source.state_dict())
