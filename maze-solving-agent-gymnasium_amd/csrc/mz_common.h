@@ -102,7 +102,11 @@ struct MzOut {
   float* window;
   int32_t* done_idx;
   int32_t* done_count;
+  int window_nt;  // set by mz_launch_step: f32 windows as non-temporal stores (past the MALL)
 };
+// f32 window bytes per step above which k_step stores them non-temporally (the 256 MB
+// Infinity Cache no longer holds the stream; mz_env.hip store_window_f32)
+#define MZ_WINDOW_NT_BYTES (256ull << 20)
 
 // BaseMazeEnv.ACTIONS (base_maze_env.py:19-24): 0 down, 1 up, 2 right, 3 left
 __host__ __device__ inline int mz_dr(int a) { return a == 0 ? 1 : (a == 1 ? -1 : 0); }

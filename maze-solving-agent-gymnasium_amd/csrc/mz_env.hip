@@ -175,6 +175,10 @@ __device__ inline void write_obs6(float* o6, int r, int c, int gr, int gc, int b
 // write-through (buffer-store aux 16 = sc1): the window leaves no dirty L2 lines for the kernel
 // end to drain. k_step at 65,536 x 81 (bench, 500 launches): default policy 37.0 us, sc1 36.2,
 // nt 43.6, sc1 + nt 43.5.
+// Past the 256 MB Infinity Cache the same stream is faster as non-temporal stores (aux 2): at
+// 131,072 x 81 (354 MB of windows per step) nt 75.0-75.7 us vs sc1 89.2, plain 105.0, sc0|sc1
+// 107.2; at 65,536 (177 MB) sc1 31.7 vs nt 38.1-38.4 (profiles/r03wp_window_store_policy.json):
+// the launcher picks nt when the step's f32 windows exceed MZ_WINDOW_NT_BYTES (MzOut::window_nt).
 typedef __attribute__((ext_vector_type(4))) unsigned int mz_u32x4;
 template <int POL = 16>
 __device__ inline void store_window_f32(const uint32_t* cat, float* out, int nb, int lane) {
@@ -472,7 +476,10 @@ __device__ inline void step_group(const MzDev& d, const int32_t* __restrict__ ac
   if (ENRICH) {
     __syncthreads();
     if (o.window_bits) store_window_bits(cat, o.window_bits + (size_t)e0 * MZ_WINDOW_WORDS, nb, lane);
-    if (o.window && !(MZ_PROBE & 16)) store_window_f32(cat, o.window + (size_t)e0 * 675, nb, lane);
+    if (o.window && !(MZ_PROBE & 16)) {
+      if (o.window_nt) store_window_f32<2>(cat, o.window + (size_t)e0 * 675, nb, lane);
+      else store_window_f32<16>(cat, o.window + (size_t)e0 * 675, nb, lane);
+    }
   }
 
   if (AR && !(MZ_PROBE & 4)) {  // reset instances: visited plane = {start}; counts cleared when the tag wraps
@@ -856,9 +863,11 @@ void launch_step_te(const MzDev& d, const int32_t* act, const MzAct& a, bool has
 }
 
 hipError_t mz_launch_step(const MzDev& d, const int32_t* act, const MzAct* ap, bool autoreset,
-                          const MzOut& o, hipStream_t s) {
+                          const MzOut& o0, hipStream_t s) {
   MzAct a{};
   if (ap) a = *ap;
+  MzOut o = o0;
+  o.window_nt = o.window && (size_t)d.B * 675 * sizeof(float) > MZ_WINDOW_NT_BYTES;
   if (d.toroidal) {
     if (d.enrich) launch_step_te<true, true>(d, act, a, ap != nullptr, autoreset, o, s);
     else launch_step_te<true, false>(d, act, a, ap != nullptr, autoreset, o, s);
