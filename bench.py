@@ -145,7 +145,9 @@ def win_rate(a, dev, rank=0, world=1):
     e, _ = evaluate(L, a.eval_mazes, a.dim, a.algo, seed=0x7E570000, eps=0.1, device=dev)
     # the same protocol on mazes chosen as the reference's env chooses them: the easiest (McClendon
     # difficulty) of 6 candidates (base_maze_env.py:78-97) — the README's "new mazes" win-rates
+    t6 = time.perf_counter()
     mz6 = best_of_mazes(a.eval_mazes, a.dim, a.algo, seed=0x7E580000, device=dev)
+    t6 = time.perf_counter() - t6  # 6 x eval_mazes candidates generated + McClendon on the GPU
     g6, _ = evaluate(L, a.eval_mazes, a.dim, a.algo, seed=0x7E580000, eps=0.0, device=dev, mazes=mz6)
     e6, _ = evaluate(L, a.eval_mazes, a.dim, a.algo, seed=0x7E580000, eps=0.1, device=dev, mazes=mz6)
     return {"greedy": g, "eps_0.1": e, "greedy_best_of_6": g6, "eps_0.1_best_of_6": e6,
@@ -163,6 +165,7 @@ def win_rate(a, dev, rank=0, world=1):
                                "one 8.56 MB fp32 bucket per update between two graph replays")
                               if world > 1 else None,
             "acting_argmax_agreement": agree,
+            "best_of_6_selection_seconds": round(t6, 3),
             "note": "fresh GPU-generated mazes never seen in training (test(new=True) protocol); "
                     "*_best_of_6: each maze the easiest of 6 candidates by McClendon difficulty, "
                     "as the reference's env selects new mazes (base_maze_env.py:78-97)"}
