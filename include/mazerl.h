@@ -209,6 +209,22 @@ int mz_bank_use(mz_handle* h, int32_t bank);
  * (device; [3] for a single-size bank). */
 int mz_bank_consumed(mz_handle* h, int32_t bank, int32_t* out3_dev, void* stream);
 
+/* Checkpoint / resume of a handle's env state (the reference has none; its envs keep
+ * their mazes in Python lists, simple_maze_env.py:34,91). One device buffer holds a 256-B header
+ * (magic "MZST", version, B, P, toroidal, enrich, the bank geometry, the active bank and its fill
+ * epochs) and every per-instance array of the handle — cell words (maze, BFS table, visit counts
+ * and tags), open / visited plane strips, meta, position / step / current-cell words, algorithm
+ * ids, last-terminated flags — plus, when the handle has a maze bank, both banks with their
+ * consumed-slot counters. mz_state_bytes: the buffer size; mz_state_save: device-to-device copies
+ * on `stream`; mz_state_load: validates the header against the handle (same num_envs, max_dim,
+ * toroidal, enrich; the same bank geometry, created with mz_bank_create*; MZ_EINVAL otherwise),
+ * then copies back and re-activates the saved bank. Stepping a loaded handle continues
+ * bit-exactly where the saved one stood. */
+#define MZ_STATE_HEADER_BYTES 256
+int mz_state_bytes(mz_handle* h, uint64_t* bytes_out);
+int mz_state_save(mz_handle* h, void* dst_dev, uint64_t bytes, void* stream);
+int mz_state_load(mz_handle* h, const void* src_dev, uint64_t bytes, void* stream);
+
 /* Fused conv stem of the DQN/DDQN Q-network for acting (dqn_agent.py:19-57 forward,
  * ddqn_agent.py:18-52): from n packed windows (window_bits layout) and obs6 [n][6] f32, writes
  * feat_dev [n][ld] bf16 = [MaxPool2(Dropout(LeakyReLU(Conv3x3(window) + b))) (1,568 values,

@@ -27,6 +27,7 @@ struct MzBankStore {  // two banks x the enabled algorithms x sizes x K slots (m
   uint32_t* meta0 = nullptr;   // [2][nA][nD][K]
   uint32_t* meta1 = nullptr;
   int* heads = nullptr;        // [2][3][nD] consumed slots per (algorithm id, size)
+  int* slot = nullptr;         // [3][nD][ceil(B / 64)] winners' first slot per group (k_reset_done)
   // scratch the build writes and nobody reads: [K] ...
   uint32_t *s_posw = nullptr, *s_stw = nullptr, *s_curw = nullptr;
   uint8_t *s_last = nullptr, *s_algo = nullptr;
@@ -538,7 +539,8 @@ int mz_bank_create_dims(mz_handle* h, int32_t slots, const int32_t* dims, int32_
   int rc;
   if ((rc = alloc(h, &b.cells, S * d.P * d.P)) || (rc = alloc(h, &b.planes, S * d.PW)) ||
       (rc = alloc(h, &b.meta0, S)) || (rc = alloc(h, &b.meta1, S)) ||
-      (rc = alloc(h, &b.heads, (size_t)6 * ndims)) || (rc = alloc(h, &b.s_posw, K)) ||
+      (rc = alloc(h, &b.heads, (size_t)6 * ndims)) ||
+      (rc = alloc(h, &b.slot, (size_t)3 * ndims * ((d.B + 63) / 64))) || (rc = alloc(h, &b.s_posw, K)) ||
       (rc = alloc(h, &b.s_stw, K)) || (rc = alloc(h, &b.s_curw, K)) || (rc = alloc(h, &b.s_last, K)) ||
       (rc = alloc(h, &b.s_algo, K)))
     return rc;
@@ -613,6 +615,8 @@ int mz_bank_use(mz_handle* h, int32_t bank) {
   d.bk_meta0 = b.meta0 + blk;
   d.bk_meta1 = b.meta1 + blk;
   d.bk_head = b.heads + 3 * bank * b.nD;
+  d.bk_slot = b.slot;
+  d.bk_G = (d.B + 63) / 64;
   return MZ_OK;
 }
 
@@ -623,6 +627,142 @@ int mz_bank_consumed(mz_handle* h, int32_t bank, int32_t* out3_dev, void* stream
   MZ_HIP(hipMemcpyAsync(out3_dev, h->bank.heads + 3 * bank * nd, 3 * nd * sizeof(int32_t),
                         hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)));
   return MZ_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// ---- checkpoint / resume (mz_state_*): header words and the ordered device sections
+constexpr uint32_t kStateMagic = 0x54535A4Du;  // "MZST"
+constexpr uint32_t kStateVersion = 1u;
+enum : int { SH_MAGIC, SH_VER, SH_B, SH_P, SH_TOR, SH_ENRICH, SH_NS, SH_PW, SH_BK_K, SH_BK_NA,
+             SH_BK_ND, SH_BK_AMASK, SH_BK_ACTIVE, SH_BK_EPOCH0, SH_BK_EPOCH1, SH_DIMS = 16 };
+static_assert(SH_DIMS * 4 + MZ_BANK_MAX_DIMS <= MZ_STATE_HEADER_BYTES, "header too small");
+
+struct Section {
+  void* p;
+  size_t bytes;
+};
+
+std::vector<Section> state_sections(mz_handle* h) {
+  const MzDev& d = h->d;
+  const size_t B = (size_t)d.B, P = (size_t)d.P;
+  std::vector<Section> s = {
+      {d.cells, B * P * P * 4}, {d.planes, (B * (size_t)d.PW + 16) * 4}, {d.meta0, B * 4},
+      {d.meta1, B * 4}, {d.posw, B * 4}, {d.stw, B * 4}, {d.curw, B * 4}, {d.algo, B},
+      {d.last_term, B}};
+  const MzBankStore& b = h->bank;
+  if (b.K) {
+    const size_t S = 2 * (size_t)b.nA * b.nD * b.K;
+    s.push_back({b.cells, S * P * P * 4});
+    s.push_back({b.planes, S * (size_t)d.PW * 4});
+    s.push_back({b.meta0, S * 4});
+    s.push_back({b.meta1, S * 4});
+    s.push_back({b.heads, (size_t)6 * b.nD * 4});
+  }
+  return s;
+}
+
+size_t state_size(mz_handle* h) {
+  size_t n = MZ_STATE_HEADER_BYTES;
+  for (const Section& s : state_sections(h)) n += (s.bytes + 255) & ~(size_t)255;
+  return n;
+}
+
+int active_bank(const mz_handle* h) {
+  const MzDev& d = h->d;
+  if (!d.bk_K || !h->bank.K) return -1;
+  return d.bk_cells == h->bank.cells ? 0 : 1;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mz_state_bytes(mz_handle* h, uint64_t* bytes_out) {
+  if (!h || !bytes_out) return fail(MZ_EINVAL, "bad arguments");
+  *bytes_out = state_size(h);
+  return MZ_OK;
+}
+
+int mz_state_save(mz_handle* h, void* dst_dev, uint64_t bytes, void* stream) {
+  if (!h || !dst_dev) return fail(MZ_EINVAL, "bad arguments");
+  if (bytes < state_size(h)) return fail(MZ_EINVAL, "state buffer of %llu bytes, %zu needed",
+                                         (unsigned long long)bytes, state_size(h));
+  DeviceGuard g(h->cfg.device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const MzDev& d = h->d;
+  const MzBankStore& b = h->bank;
+  uint32_t hdr[MZ_STATE_HEADER_BYTES / 4] = {};
+  hdr[SH_MAGIC] = kStateMagic;
+  hdr[SH_VER] = kStateVersion;
+  hdr[SH_B] = (uint32_t)d.B;
+  hdr[SH_P] = (uint32_t)d.P;
+  hdr[SH_TOR] = (uint32_t)d.toroidal;
+  hdr[SH_ENRICH] = (uint32_t)d.enrich;
+  hdr[SH_NS] = (uint32_t)d.NS;
+  hdr[SH_PW] = (uint32_t)d.PW;
+  hdr[SH_BK_K] = (uint32_t)b.K;
+  hdr[SH_BK_NA] = (uint32_t)b.nA;
+  hdr[SH_BK_ND] = (uint32_t)b.nD;
+  hdr[SH_BK_AMASK] = b.amask;
+  hdr[SH_BK_ACTIVE] = (uint32_t)active_bank(h);
+  hdr[SH_BK_EPOCH0] = b.epoch[0];
+  hdr[SH_BK_EPOCH1] = b.epoch[1];
+  uint8_t* dims = reinterpret_cast<uint8_t*>(hdr + SH_DIMS);
+  for (int i = 0; i < b.nD; ++i) dims[i] = (uint8_t)b.dims[i];
+  uint8_t* dst = static_cast<uint8_t*>(dst_dev);
+  // the header leaves from this stack frame: wait for it (a checkpoint is off the hot path)
+  MZ_HIP(hipMemcpyAsync(dst, hdr, sizeof hdr, hipMemcpyHostToDevice, s));
+  MZ_HIP(hipStreamSynchronize(s));
+  size_t off = MZ_STATE_HEADER_BYTES;
+  for (const Section& sec : state_sections(h)) {
+    MZ_HIP(hipMemcpyAsync(dst + off, sec.p, sec.bytes, hipMemcpyDeviceToDevice, s));
+    off += (sec.bytes + 255) & ~(size_t)255;
+  }
+  return MZ_OK;
+}
+
+int mz_state_load(mz_handle* h, const void* src_dev, uint64_t bytes, void* stream) {
+  if (!h || !src_dev) return fail(MZ_EINVAL, "bad arguments");
+  if (bytes < MZ_STATE_HEADER_BYTES) return fail(MZ_EINVAL, "state buffer too small");
+  DeviceGuard g(h->cfg.device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  uint32_t hdr[MZ_STATE_HEADER_BYTES / 4];
+  MZ_HIP(hipMemcpyAsync(hdr, src_dev, sizeof hdr, hipMemcpyDeviceToHost, s));
+  MZ_HIP(hipStreamSynchronize(s));
+  const MzDev& d = h->d;
+  MzBankStore& b = h->bank;
+  if (hdr[SH_MAGIC] != kStateMagic || hdr[SH_VER] != kStateVersion)
+    return fail(MZ_EINVAL, "not an env state (magic %08x version %u)", hdr[SH_MAGIC], hdr[SH_VER]);
+  if (hdr[SH_B] != (uint32_t)d.B || hdr[SH_P] != (uint32_t)d.P ||
+      hdr[SH_TOR] != (uint32_t)d.toroidal || hdr[SH_ENRICH] != (uint32_t)d.enrich ||
+      hdr[SH_NS] != (uint32_t)d.NS || hdr[SH_PW] != (uint32_t)d.PW)
+    return fail(MZ_EINVAL, "env state of %u instances, max_dim %u, toroidal %u, enrich %u does not "
+                "fit this handle (%d, %d, %d, %d)", hdr[SH_B], hdr[SH_P], hdr[SH_TOR],
+                hdr[SH_ENRICH], d.B, d.P, d.toroidal, d.enrich);
+  const uint8_t* dims = reinterpret_cast<const uint8_t*>(hdr + SH_DIMS);
+  bool same_bank = hdr[SH_BK_K] == (uint32_t)b.K && hdr[SH_BK_NA] == (uint32_t)b.nA &&
+                   hdr[SH_BK_ND] == (uint32_t)b.nD && hdr[SH_BK_AMASK] == b.amask;
+  for (int i = 0; same_bank && i < b.nD; ++i) same_bank = dims[i] == (uint8_t)b.dims[i];
+  if (!same_bank)
+    return fail(MZ_EINVAL, "env state has a maze bank of %u slots x %u algorithms x %u sizes "
+                "(mask %u); this handle's is %d x %d x %d (mask %u)", hdr[SH_BK_K], hdr[SH_BK_NA],
+                hdr[SH_BK_ND], hdr[SH_BK_AMASK], b.K, b.nA, b.nD, b.amask);
+  if (bytes < state_size(h)) return fail(MZ_EINVAL, "state buffer of %llu bytes, %zu needed",
+                                         (unsigned long long)bytes, state_size(h));
+  const uint8_t* src = static_cast<const uint8_t*>(src_dev);
+  size_t off = MZ_STATE_HEADER_BYTES;
+  for (const Section& sec : state_sections(h)) {
+    MZ_HIP(hipMemcpyAsync(sec.p, src + off, sec.bytes, hipMemcpyDeviceToDevice, s));
+    off += (sec.bytes + 255) & ~(size_t)255;
+  }
+  if (b.K) {
+    b.epoch[0] = hdr[SH_BK_EPOCH0];
+    b.epoch[1] = hdr[SH_BK_EPOCH1];
+  }
+  return mz_bank_use(h, (int32_t)hdr[SH_BK_ACTIVE]);
 }
 
 int mz_maze_metrics(mz_handle* h, const int32_t* env_ids_dev, int32_t n, double* out_dev,

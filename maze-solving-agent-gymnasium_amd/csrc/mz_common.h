@@ -76,6 +76,11 @@ struct MzDev {
   const uint32_t* bk_meta0; // [slots]
   const uint32_t* bk_meta1; // [slots]
   int* bk_head;             // [3][bk_nd]
+  // deterministic slot assignment for k_reset_done (k_bank_count / k_bank_scan): per bank class
+  // (algorithm id a, size index di) -> a * bk_nd + di and 64-instance group g, the first slot
+  // of the group's winners, bk_slot[class * bk_G + g]
+  int* bk_slot;             // [3 * bk_nd][bk_G]
+  int bk_G;                 // 64-instance groups, ceil(B / 64)
 };
 
 __host__ __device__ inline int mz_bank_aidx(uint32_t amask, int a) {

@@ -591,17 +591,29 @@ __global__ __launch_bounds__(WAVE) void k_reset_list(MzDev d, const int32_t* idx
   // ticket here cost one same-address atomic per block, serialised (~30 ns each, up to 1,024)
 }
 
-// Copy the next unconsumed bank maze of algorithm a into instance e (cells + plane rows + meta;
-// reset_one then rebuilds the per-episode state). Returns false (caller builds in place) when no
-// bank is in use, the bank does not hold algorithm a or size N, or it is exhausted.
-__device__ bool bank_take(const MzDev& d, int e, int a, int N) {
-  if (d.bk_K == 0 || N < 0 || N >= 128 || !((d.bk_amask >> a) & 1u)) return false;
+// Bank class of a winner k_reset_done regenerates: a * bk_nd + di for its algorithm id a and maze
+// size index di, -1 when no bank is in use or the bank does not hold that algorithm / size.
+__device__ inline int bank_class(const MzDev& d, int e) {
+  if (d.bk_K == 0) return -1;
+  const int a = d.algo[e], N = (int)(d.meta0[e] & 0xFF);
+  if (N >= 128 || !((d.bk_amask >> a) & 1u)) return -1;
   const int di = d.bk_didx[N];
-  if (di < 0) return false;
-  int slot = 0;
-  if (threadIdx.x == 0) slot = atomicAdd(&d.bk_head[a * d.bk_nd + di], 1);
-  slot = __shfl(slot, 0);
-  if (slot >= d.bk_K) return false;
+  return di < 0 ? -1 : a * d.bk_nd + di;
+}
+
+// whether instance e is a winner k_reset_done(regen) gives a new maze
+__device__ inline bool regen_winner(const MzDev& d, int e) {
+  return e < d.B && ((d.posw[e] >> 20) & 1u) && d.last_term[e];
+}
+
+// Copy bank slot `slot` of class `cls` (bank_class) into instance e (cells + plane rows + meta;
+// reset_one then rebuilds the per-episode state). Returns false (the caller builds in place) for
+// cls < 0 or an exhausted bank (slot >= K). The slots come from k_bank_count / k_bank_scan: the
+// winners of one reset_done launch take consecutive slots of their class in instance order, so
+// which winner receives which maze does not depend on the order the waves run in.
+__device__ bool bank_take(const MzDev& d, int e, int cls, int slot) {
+  if (cls < 0 || slot >= d.bk_K) return false;
+  const int a = cls / d.bk_nd, di = cls - a * d.bk_nd;
   const size_t src = ((size_t)mz_bank_aidx(d.bk_amask, a) * d.bk_nd + di) * d.bk_K + slot;
   const size_t es = (size_t)e;
   const size_t pp = (size_t)d.P * d.P;
@@ -618,6 +630,52 @@ __device__ bool bank_take(const MzDev& d, int e, int a, int N) {
   }
   __syncthreads();  // reset_one reads meta0 / the start cell word written above
   return true;
+}
+
+// Slot assignment, pass 1 (one wave per 64-instance group g): winners per bank class in the
+// group -> bk_slot[class * G + g] (the array is zeroed before the launch).
+__global__ __launch_bounds__(WAVE) void k_bank_count(MzDev d) {
+  const int lane = threadIdx.x, g = blockIdx.x, e = g * WAVE + lane;
+  const int cls = regen_winner(d, e) ? bank_class(d, e) : -1;
+  unsigned long long pend = __ballot(cls >= 0);
+  while (pend) {  // one pass per distinct class in the wave (wave-uniform loop)
+    const int cj = __shfl(cls, __ffsll((long long)pend) - 1);
+    const unsigned long long m = __ballot(cls == cj);
+    if (lane == 0) d.bk_slot[cj * d.bk_G + g] = __popcll(m);
+    pend &= ~m;
+  }
+}
+
+// Pass 2 (one workgroup per class): exclusive prefix over the groups in group order, offset by
+// the class's consumed-slot counter -> the first slot of each group's winners; the counter then
+// advances by the class's winners (what the per-winner atomic used to add).
+constexpr int BS_T = 1024;
+__global__ __launch_bounds__(BS_T) void k_bank_scan(MzDev d) {
+  __shared__ int wsum[BS_T / WAVE];
+  __shared__ int carry;
+  const int c = blockIdx.x, t = threadIdx.x, lane = t & (WAVE - 1), w = t / WAVE;
+  int* cnt = d.bk_slot + (size_t)c * d.bk_G;
+  if (t == 0) carry = d.bk_head[c];
+  __syncthreads();
+  for (int base = 0; base < d.bk_G; base += BS_T) {
+    const int i = base + t;
+    const int v = i < d.bk_G ? cnt[i] : 0;
+    int x = v;  // inclusive wave scan
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+      const int y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == WAVE - 1) wsum[w] = x;
+    __syncthreads();
+    int before = carry;
+    for (int k = 0; k < w; ++k) before += wsum[k];
+    if (i < d.bk_G) cnt[i] = before + x - v;
+    __syncthreads();
+    if (t == BS_T - 1) carry = before + x;
+    __syncthreads();
+  }
+  if (t == 0) d.bk_head[c] = carry;
 }
 
 // Fill one bank block (algorithm `algo`, `bd` = MzDev view whose instance arrays are the block's
@@ -642,16 +700,30 @@ __global__ __launch_bounds__(WAVE) void k_reset_done(MzDev d, int regen, uint64_
                                                      uint32_t epoch, MzOut o) {
   extern __shared__ __align__(16) uint8_t lds[];
   __shared__ __align__(16) uint32_t wsh[32];
-  const int e = blockIdx.x * WAVE + threadIdx.x;
+  const int lane = threadIdx.x, e = blockIdx.x * WAVE + lane;
   const bool done = e < d.B && ((d.posw[e] >> 20) & 1u);
+  // this lane's bank slot if it is a winner with a bank class: the group's first slot of the
+  // class (k_bank_scan) + its rank among the group's winners of the class
+  int cls = -1, slot = 0;
+  if (regen && d.bk_K) {
+    cls = regen_winner(d, e) ? bank_class(d, e) : -1;
+    unsigned long long pend = __ballot(cls >= 0);
+    while (pend) {
+      const int cj = __shfl(cls, __ffsll((long long)pend) - 1);
+      const unsigned long long m = __ballot(cls == cj);
+      if (cls == cj) slot = d.bk_slot[cj * d.bk_G + blockIdx.x] + __popcll(m & ((1ull << lane) - 1ull));
+      pend &= ~m;
+    }
+  }
   unsigned long long bal = __ballot(done);
   while (bal) {
     const int j = __ffsll((long long)bal) - 1;
     bal &= bal - 1;
     const int ej = blockIdx.x * WAVE + j;
+    const int cj = __shfl(cls, j), sj = __shfl(slot, j);
     if (regen && d.last_term[ej]) {
       const int a = d.algo[ej], N = (int)(d.meta0[ej] & 0xFF);
-      if (!bank_take(d, ej, a, N))
+      if (!bank_take(d, ej, cj, sj))
         mz_build_one(d, ej, TOR, true, a, seed + (uint64_t)ej + ((uint64_t)epoch << 32), N,
                      nullptr, 0, 0, 0, 0, lds);
       __syncthreads();  // this workgroup's global stores are visible to it past the barrier
@@ -897,6 +969,12 @@ hipError_t mz_launch_reset_done(const MzDev& d, int regen, uint64_t seed, uint32
   const int blocks = (d.B + WAVE - 1) / WAVE;
   size_t lds = 0;
   hipError_t ae = hipSuccess;
+  if (regen && d.bk_K) {  // the winners' bank slots, in instance order (k_bank_count / k_bank_scan)
+    ae = hipMemsetAsync(d.bk_slot, 0, sizeof(int) * 3 * (size_t)d.bk_nd * d.bk_G, s);
+    if (ae != hipSuccess) return ae;
+    hipLaunchKernelGGL(k_bank_count, dim3(d.bk_G), dim3(WAVE), 0, s, d);
+    hipLaunchKernelGGL(k_bank_scan, dim3(3 * d.bk_nd), dim3(BS_T), 0, s, d);
+  }
 #define MZ_RD(T, E)                                                                           \
   do {                                                                                        \
     if (regen) {                                                                              \

@@ -39,7 +39,7 @@ EXPORTS = ["mz_last_error", "mz_device_count", "mz_create", "mz_destroy", "mz_lo
            "mz_act", "mz_step_act", "mz_expand_window", "mz_set_algorithm", "mz_query", "mz_get_grid",
            "mz_difficulty", "mz_maze_complexity", "mz_maze_metrics", "mz_difficulty_batch", "mz_get_meta", "mz_discounted_returns", "mz_q_front",
            "mz_bank_create", "mz_bank_create_dims", "mz_bank_fill", "mz_bank_use",
-           "mz_bank_consumed",
+           "mz_bank_consumed", "mz_state_bytes", "mz_state_save", "mz_state_load",
            "mz_stem_forward", "mz_stem_backward", "mz_stem_workspace_floats", "mz_adamw_flat",
            "mz_pair_surrogate", "mz_leaky_relu_bf16", "mz_colsum_f32",
            "mz_replay_gather", "mz_host_alloc", "mz_host_free", "mz_q_front_rows", "mz_greedy_rows",
@@ -101,6 +101,9 @@ def load(build_if_missing=True):
     L.mz_bank_fill.argtypes = [vp, C.c_int32, C.c_uint64, vp]
     L.mz_bank_use.argtypes = [vp, C.c_int32]
     L.mz_bank_consumed.argtypes = [vp, C.c_int32, vp, vp]
+    L.mz_state_bytes.argtypes = [vp, C.POINTER(C.c_uint64)]
+    L.mz_state_save.argtypes = [vp, vp, C.c_uint64, vp]
+    L.mz_state_load.argtypes = [vp, vp, C.c_uint64, vp]
     L.mz_q_front.argtypes = [vp, vp, C.c_int32, vp, vp, C.c_float, C.c_uint64, C.c_uint64, vp,
                              C.c_int32, vp]
     L.mz_q_front_rows.argtypes = [vp, vp, vp, vp, C.c_int32, vp, vp, C.c_float, C.c_uint64,

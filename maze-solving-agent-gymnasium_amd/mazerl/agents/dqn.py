@@ -519,6 +519,108 @@ class VectorDQNLearner:
             self._async = False
             self.fused.invalidate()
 
+    # ---- checkpoint / resume (Q-nets, optimizer, replay, counters) -----------------
+    def state_dict(self):
+        """Everything the learner's future updates and acting depend on: both nets (the
+        reference's module names, so the Q-net part loads into its DQN / DDQN classes), the
+        optimizer moments, step count and learning rate, the cosine schedule, per-instance
+        steps_done / epsilon decay, the filled replay rows and its pointer, the sample and dropout
+        streams (replay index counter, the stems' device-side dropout counters and salts, the
+        acting heads' (seed, counter), torch's RNG states). The side stream is joined first."""
+        self.finish()
+        rp, n = self.replay, self.replay.size
+        opt = self.opt
+        if hasattr(opt, "exp_avg"):  # FlatAdamW (device-side lr and step count)
+            ost = {"exp_avg": opt.exp_avg.clone(), "exp_avg_sq": opt.exp_avg_sq.clone(),
+                   "step": opt._step_buf.clone(), "lr": float(opt.param_groups[0]["lr"])}
+        else:
+            ost = {"torch": opt.state_dict()}
+        heads = [self.fused] + list(getattr(self, "actor_fused", []))
+        ed = self.eps_decay
+        return {"format": "mazerl.VectorDQNLearner/1", "variant": self.variant,
+                "source": {k: v.clone() for k, v in self.source.state_dict().items()},
+                "target": {k: v.clone() for k, v in self.target.state_dict().items()},
+                "opt": ost, "sched": self.sched.state_dict(),
+                "steps_done": self.steps_done.clone(),
+                "eps_decay": ed.clone() if torch.is_tensor(ed) else float(ed),
+                "n_updates": self.n_updates, "graph": self._graph is not None,
+                "sample_seed": getattr(self, "_sample_seed", None),
+                "sample_counter": getattr(self, "_sample_counter", None),
+                "replay": {"capacity": rp.capacity, "ptr": rp.ptr, "size": n,
+                           "rows": {k: getattr(rp, k)[:n].clone()
+                                    for k in ("s6", "sw", "a", "r", "s6n", "swn")},
+                           "gen": rp._gen.get_state()},
+                "salts": [self.source._salt, self.target._salt],
+                "stem_rng": [None if m._stem_rng is None else m._stem_rng.clone()
+                             for m in (self.source, self.target)],
+                "heads": [None if h is None else (h.stem.seed, h.stem.counter) if hasattr(h, "stem")
+                          else (h.seed, h.counter) for h in heads],
+                "torch_rng": torch.get_rng_state(),
+                "cuda_rng": torch.cuda.get_rng_state(self.device) if self.device.type == "cuda" else None}
+
+    def load_state_dict(self, sd):
+        """Restore a state_dict() in place (captured update graphs keep their buffers). A learner
+        whose update graphs do not exist yet while the saved one had them first captures its
+        own (warm-up updates on the loaded replay, then the capture), so that the resumed run
+        takes the same update path; the state is then loaded again over what those changed."""
+        if sd.get("format") != "mazerl.VectorDQNLearner/1" or sd["variant"] != self.variant:
+            raise ValueError("not a state_dict of a VectorDQNLearner of this variant")
+        if sd["replay"]["capacity"] != self.replay.capacity:
+            raise ValueError("replay capacity differs from the saved learner's")
+        # construction-order salts of the stems' dropout masks: before any capture bakes them in
+        self.source._salt, self.target._salt = sd["salts"]
+        self._load(sd)
+        if sd["graph"] and self.use_graph and self._graph is None:
+            while self._graph is None:
+                self._graph_update(None)
+            self._load(sd)
+
+    def _load(self, sd):
+        dev = self.device
+        with torch.no_grad():
+            self.source.load_state_dict(sd["source"])
+            self.target.load_state_dict(sd["target"])
+        o = sd["opt"]
+        if "torch" in o:
+            self.opt.load_state_dict(o["torch"])
+        else:
+            self.opt.exp_avg.copy_(o["exp_avg"])
+            self.opt.exp_avg_sq.copy_(o["exp_avg_sq"])
+            self.opt._step_buf.copy_(o["step"])
+        self.sched.load_state_dict(sd["sched"])
+        lr = self.opt.param_groups[0]["lr"]
+        if "lr" in o and torch.is_tensor(lr):
+            lr.fill_(o["lr"])
+        self.steps_done.copy_(sd["steps_done"])
+        ed = sd["eps_decay"]
+        self.eps_decay = ed.to(dev).clone() if torch.is_tensor(ed) else float(ed)
+        self.n_updates = int(sd["n_updates"])
+        if sd["sample_seed"] is not None and hasattr(self, "_sample_seed"):
+            self._sample_seed, self._sample_counter = sd["sample_seed"], sd["sample_counter"]
+        rp, r = self.replay, sd["replay"]
+        n = int(r["size"])
+        for k, v in r["rows"].items():
+            getattr(rp, k)[:n].copy_(v)
+        rp.ptr, rp.size = int(r["ptr"]), n
+        rp.size_dev.fill_(float(n))
+        rp._gen.set_state(r["gen"].cpu())  # (map_location may have moved it)
+        for m, st in zip((self.source, self.target), sd["stem_rng"]):
+            if st is None:
+                continue
+            if m._stem_rng is None:
+                m._stem_rng = torch.zeros(1, dtype=torch.int64, device=dev)
+            m._stem_rng.copy_(st)  # in place: a captured graph advances this very tensor
+        heads = [self.fused] + list(getattr(self, "actor_fused", []))
+        for h, st in zip(heads, sd["heads"]):
+            if h is None or st is None:
+                continue
+            tgt = h.stem if hasattr(h, "stem") else h
+            tgt.seed, tgt.counter = st
+            h.invalidate()
+        torch.set_rng_state(sd["torch_rng"].cpu())
+        if sd["cuda_rng"] is not None and dev.type == "cuda":
+            torch.cuda.set_rng_state(sd["cuda_rng"].cpu(), dev)
+
     def _one_update(self, expand, static):
         if self.overlap and not torch.cuda.is_current_stream_capturing():
             fresh = self.replay.sample_indices(self.batch_size)  # eager (pre-capture) update

@@ -44,7 +44,15 @@ def parse(argv=None):
                     help="acting forward: x3 = f32-accurate bf16x3 MFMA (QAct); bf16 = bf16 head")
     ap.add_argument("--overlap", type=int, default=1,
                     help="1: updates on a side HIP stream (acting one update behind); 0: sequential")
+    ap.add_argument("--resume", default=None,
+                    help="checkpoint to continue from (mazerl/checkpoint.py; rank r reads "
+                         "<path>.rank<r> when world > 1)")
+    ap.add_argument("--save", default=None, help="checkpoint written after training (same naming)")
     return ap.parse_args(argv)
+
+
+def _ck_path(path, rank, world):
+    return path if world == 1 else f"{path}.rank{rank}"
 
 
 def main(argv=None):
@@ -72,6 +80,9 @@ def main(argv=None):
         broadcast_params(learner.source)
         learner.target.load_state_dict(learner.source.state_dict())
     trainer = VectorOffPolicyTrainer(env, learner, seed=a.seed + 7919 * rank, curriculum=a.curriculum)
+    if a.resume:  # every rank its own shard's env / replay; the nets are identical on all ranks
+        from .checkpoint import load_checkpoint
+        load_checkpoint(_ck_path(a.resume, rank, world), trainer)
     secs = trainer.train(a.steps, log_every=a.log_every if rank == 0 else 0,
                          log=(lambda r: print(json.dumps(r), flush=True)) if rank == 0 else None)
     stats = torch.stack([trainer.wins, trainer.episodes]).to(torch.float64)
@@ -81,6 +92,9 @@ def main(argv=None):
         import torch.distributed as dist
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     secs = float(t.item())
+    if a.save:
+        from .checkpoint import save_checkpoint
+        save_checkpoint(_ck_path(a.save, rank, world), trainer)
     res = {}
     if rank == 0:
         eval_algo = "r-prim" if a.algo == "mixed" else a.algo

@@ -128,6 +128,32 @@ class VectorOffPolicyTrainer:
         outer.wait_stream(s)
         return secs
 
+    def state_dict(self):
+        """Checkpoint of the whole run (mazerl/checkpoint.py): this trainer's counters, the env
+        (VectorMazeEnv.state_dict) and the learner (VectorDQNLearner.state_dict). train() calls
+        after a load_state_dict continue exactly as further train() calls on the saved trainer
+        would have."""
+        L = self.learner
+        return {"format": "mazerl.VectorOffPolicyTrainer/1", "seed": self.seed,
+                "counter": self.counter, "wins": self.wins.clone(), "episodes": self.episodes.clone(),
+                "inst_wins": self.inst_wins.clone(), "curriculum": self.curriculum,
+                "regen_won": self.regen_won, "history": list(self.history),
+                "learner": L.state_dict(), "env": self.env.state_dict()}
+
+    def load_state_dict(self, sd):
+        if sd.get("format") != "mazerl.VectorOffPolicyTrainer/1":
+            raise ValueError("not a VectorOffPolicyTrainer state_dict")
+        if bool(sd["curriculum"]) != bool(self.curriculum) or bool(sd["regen_won"]) != bool(self.regen_won):
+            raise ValueError("curriculum / regen_won differ from the saved trainer's")
+        self.env.load_state_dict(sd["env"])
+        self.learner.load_state_dict(sd["learner"])
+        self.seed, self.counter = int(sd["seed"]), int(sd["counter"])
+        self.wins.copy_(sd["wins"])
+        self.episodes.copy_(sd["episodes"])
+        self.inst_wins.copy_(sd["inst_wins"])
+        self.history = list(sd["history"])
+        self._eps = None
+
     def _train(self, vector_steps, log_every, log, t0):
         # the next step's epsilon and its issued greedy-row list are recomputed on entry: the
         # caller may have changed steps_done (a reload, a reset) since the last train() call

@@ -299,6 +299,62 @@ class VectorMazeEnv:
         N.check(self.lib.mz_bank_consumed(self._h, b, out.data_ptr(), self._stream()))
         return out if nd == 1 else out.view(3, nd)
 
+    # ---------------------------------------------------------------------------------------
+    # Checkpoint / resume (the reference has none for its envs)
+    _OUTPUTS = ("reward", "reward64", "terminated", "truncated", "pos", "best_dir", "actions",
+                "obs6", "window", "window_bits", "done_idx", "done_count")
+
+    def state_dict(self):
+        """Everything a resumed env needs to continue bit-exactly: the handle's device state
+        (mz_state_save: mazes, tables, visit planes, per-instance state, the maze bank) as one
+        uint8 device tensor, the last step's outputs (the next step's observation), and the
+        host-side counters (regeneration epoch, bank rotation)."""
+        main = torch.cuda.current_stream(self.device)
+        if self._bank is not None:  # a refill still running on the side stream writes a bank
+            for ev in self._bank["ready"]:
+                if ev is not None:
+                    main.wait_event(ev)
+        n = N.C.c_uint64()
+        N.check(self.lib.mz_state_bytes(self._h, N.C.byref(n)))
+        blob = torch.empty(n.value, dtype=torch.uint8, device=self.device)
+        N.check(self.lib.mz_state_save(self._h, blob.data_ptr(), n.value, self._stream()))
+        out = {k: getattr(self, k).clone() for k in self._OUTPUTS if getattr(self, k) is not None}
+        bank = None
+        if self._bank is not None:
+            bank = {k: self._bank[k] for k in ("K", "dims", "swap", "calls", "cur", "seed")}
+        return {"format": "mazerl.VectorMazeEnv/1", "num_envs": self.num_envs,
+                "maze_dim": self.maze_dim, "max_dim": self.max_dim, "toroidal": self.toroidal,
+                "enrich": self.enrich, "seed": self.seed, "epoch": self.epoch,
+                "count_zero": self._count_zero, "algos_in_use": sorted(self.algos_in_use),
+                "device_state": blob, "outputs": out, "bank": bank}
+
+    def load_state_dict(self, sd):
+        """Restore a state_dict() into this env (same num_envs / max_dim / toroidal / enrich and,
+        if the saved env had a maze bank, enable_bank() called with the same geometry first)."""
+        if sd.get("format") != "mazerl.VectorMazeEnv/1":
+            raise ValueError("not a VectorMazeEnv state_dict")
+        bank = sd.get("bank")
+        if (bank is None) != (self._bank is None) or (bank is not None and (
+                bank["K"] != self._bank["K"] or list(bank["dims"]) != list(self._bank["dims"]))):
+            raise ValueError("maze bank mismatch: call enable_bank() with the saved geometry "
+                             "(or not at all) before load_state_dict()")
+        blob = sd["device_state"].to(device=self.device, dtype=torch.uint8).contiguous()
+        N.check(self.lib.mz_state_load(self._h, blob.data_ptr(), blob.numel(), self._stream()))
+        for k, v in sd["outputs"].items():
+            dst = getattr(self, k, None)
+            if dst is None or tuple(dst.shape) != tuple(v.shape):
+                raise ValueError(f"output {k!r}: this env's buffer does not match the saved one")
+            dst.copy_(v)
+        self.seed, self.epoch = int(sd["seed"]), int(sd["epoch"])
+        self._count_zero = bool(sd["count_zero"])
+        self.algos_in_use = set(sd.get("algos_in_use", ()))
+        if bank is not None:
+            self._bank.update(swap=int(bank["swap"]), calls=int(bank["calls"]),
+                              cur=int(bank["cur"]), seed=int(bank["seed"]), ready=[None, None])
+            # later refills run on the side stream: order them after this load
+            self._bank["side"].wait_stream(torch.cuda.current_stream(self.device))
+        self._host_sync()
+
     def reset_done_list(self, regen_won=False, seed=None):
         """Auto-reset from the step's device done list (consumes done_count)."""
         self.reset_list(self.done_idx, self.done_count, regen_won=regen_won, seed=seed)

@@ -92,6 +92,34 @@ def test_bank_serves_generated_slots():
     env.close()
 
 
+def test_bank_slots_go_to_winners_in_instance_order():
+    """The winners of one reset_done launch take consecutive slots in instance order (k_bank_count
+    / k_bank_scan), so the maze each winner receives does not depend on wave scheduling: runs
+    from the same seeds are reproducible (and a resumed checkpoint continues exactly)."""
+    from mazerl import VectorMazeEnv
+    B, K, seed = 48, 64, 0xBA4C0000
+    env = VectorMazeEnv(B, DIM, enrich=True, device="cuda", seed=12, algorithm="dfs",
+                        done_list=False)
+    env.enable_bank(slots=K, swap_every=10 ** 9, algorithms=["dfs"], seed=seed)
+    slots = slot_mazes(K, seed ^ ((3 * 0 + 1 + 1) << 56), "dfs")
+    solver = Solver(env)
+    multi = 0
+    for _ in range(2000):
+        env.step(solver.actions())
+        winners = torch.nonzero(env.terminated).flatten().tolist()
+        c0 = int(env.bank_consumed()[1])
+        env.reset_done(regen_won=True)
+        if winners:
+            multi += len(winners) > 1
+            for k, i in enumerate(winners):
+                if c0 + k < K:
+                    assert signature(env, i) == slots[c0 + k], (i, c0 + k)
+        if c0 >= K:
+            break
+    assert multi > 0  # some launch had several winners racing for slots
+    env.close()
+
+
 def test_bank_exhaustion_and_swap_keep_valid_mazes():
     """Tiny banks: most wins fall back to in-place builds; swaps refill on the side stream."""
     from mazerl import VectorMazeEnv
