@@ -25,7 +25,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, outdir, overlap):
+def _worker(rank, world, port, outdir, overlap, backend="gloo"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK="0")
     import torch.distributed as dist
@@ -33,8 +33,13 @@ def _worker(rank, world, port, outdir, overlap):
     from mazerl.agents.dqn import VectorDQNLearner
     from mazerl.distributed import GradAllReduce, broadcast_params, init_from_env
     from test_learner_graph import _fill
-    init_from_env("gloo")
     torch.cuda.set_device(0)
+    if world > 1:
+        init_from_env(backend)
+    else:  # one rank: init_from_env leaves the group out; RCCL binds the communicator to cuda:0
+        dist.init_process_group(backend, init_method="env://",
+                                **({"device_id": torch.device("cuda", 0)} if backend == "nccl" else {}))
+    assert dist.get_backend() == backend
     env = VectorMazeEnv(4, 21, enrich=True, device="cuda", seed=1)
     mk = lambda g, ov: VectorDQNLearner(4, "cuda", variant="ddqn", batch_size=32, capacity=64,  # noqa: E731
                                         updates_per_step=1, target_every=4, updates_per_epoch=2,
@@ -86,3 +91,19 @@ def test_graph_allreduce_update_tracks_eager_two_ranks(overlap):
         assert torch.equal(pb0, pb1)
     # and the ranks' data differed: rank 0's and rank 1's first losses are not the same
     assert r[0]["losses"][0][0] != r[1]["losses"][0][0]
+
+
+@pytest.mark.parametrize("overlap", [False, True], ids=["sequential", "overlapped"])
+def test_graph_allreduce_update_over_rccl_one_rank(overlap):
+    """The same learner path with the all-reduce over RCCL ("nccl" backend, RCCL 2.26 on ROCm):
+    a gpurun box has one GPU and RCCL refuses two ranks on one device ("Duplicate GPU detected",
+    profiles/r03z_rccl_probe.txt), so this runs one rank — the RCCL communicator bound to cuda:0,
+    the flat-bucket all-reduce issued between the two captured graphs (and, overlapped, on the
+    side stream) — and checks it against the eager update as above."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(1, _free_port(), d, overlap, "nccl"), nprocs=1, join=True)
+        r = torch.load(os.path.join(d, "r0.pt"), weights_only=True)
+    for la, lb in r["losses"]:
+        assert la == pytest.approx(lb, rel=1e-4, abs=1e-7)
+    for pa, pb in zip(r["A"], r["B"]):
+        assert torch.allclose(pa, pb, rtol=1e-5, atol=1e-5)
