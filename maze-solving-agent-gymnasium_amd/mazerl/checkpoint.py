@@ -12,6 +12,9 @@ whole run of a VectorOffPolicyTrainer:
            random stream the next updates and acts draw from
   trainer  vector-step counter, win / episode counters, history
 
+The same two calls take config 5's VectorPPOTrainer (its net and optimizer, the in-flight
+episodes' records, the update pool, its counters and the env).
+
 A resumed run continues bit-exactly where the saved one stood (tests/test_checkpoint_gpu.py).
 Files are written with torch.save and read with torch.load(weights_only=True): tensors, numbers,
 strings, lists and dicts only — nothing in a checkpoint executes on load.

@@ -31,6 +31,9 @@ def main(argv=None):
     ap.add_argument("--eager-update", action="store_true", help="no captured minibatch step")
     ap.add_argument("--no-bank", action="store_true",
                     help="build winners' new mazes inline instead of copying them from a maze bank")
+    ap.add_argument("--resume", default=None, help="checkpoint to continue from (<path>.rank<r> "
+                                                    "per rank when world > 1)")
+    ap.add_argument("--save", default=None, help="checkpoint written after training")
     a = ap.parse_args(argv)
     if "-" in a.dims:
         lo, hi = (int(x) for x in a.dims.split("-"))
@@ -48,8 +51,15 @@ def main(argv=None):
                           allreduce=GradAllReduce() if world > 1 else None)
     if world > 1:
         broadcast_params(tr.net)
+    ck = (lambda p: p if world == 1 else f"{p}.rank{rank}")  # noqa: E731
+    if a.resume:
+        from .checkpoint import load_checkpoint
+        load_checkpoint(ck(a.resume), tr)
     secs = tr.train(a.steps, log_every=100 if rank == 0 else 0,
                     log=(lambda r: print(json.dumps(r), flush=True)) if rank == 0 else None)
+    if a.save:
+        from .checkpoint import save_checkpoint
+        save_checkpoint(ck(a.save), tr)
     st = allreduce_sum(torch.tensor([tr.episodes, tr.wins], dtype=torch.float64, device=dev))
     if rank == 0:
         rate, k = evaluate(tr, a.eval_mazes, dims, a.algo, seed=0x7E570000, eps=0.0, toroidal=True,

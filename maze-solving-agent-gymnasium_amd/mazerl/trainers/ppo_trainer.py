@@ -233,6 +233,64 @@ class VectorPPOTrainer:
         torch.cuda.synchronize()
         return time.perf_counter() - t0
 
+    # ---- checkpoint / resume (mazerl/checkpoint.py) -------------------------------------------
+    _REC = ("b_s6", "b_w", "b_a", "b_lp", "b_v", "b_r")
+    _POOL = ("p_s6", "p_w", "p_a", "p_lp", "p_adv", "p_ret")
+
+    def state_dict(self):
+        """The run between two vector steps: the net, the optimizer (moments, step, per-group
+        learning rates), the in-flight episodes' records (only each instance's first t[i] rows of
+        the [B, L] buffers), the update pool's filled rows, the counters and the env."""
+        torch.cuda.synchronize(self.device)
+        t = self.t.clone()
+        live = torch.arange(self.L, device=self.device)[None, :] < t[:, None].long()
+        fill = int(self.pool_fill.item())
+        o = self.opt
+        if hasattr(o, "exp_avg"):
+            ost = {k: getattr(o, k).clone() for k in ("exp_avg", "exp_avg_sq", "step_t", "lr_dev")}
+        else:
+            ost = {"torch": o.state_dict()}
+        return {"format": "mazerl.VectorPPOTrainer/1", "L": self.L, "cap": self.cap,
+                "net": {k: v.clone() for k, v in self.net.state_dict().items()}, "opt": ost,
+                "t": t, "records": {k: getattr(self, k)[live] for k in self._REC},
+                "pool_fill": fill, "pool": {k: getattr(self, k)[:fill].clone() for k in self._POOL},
+                "pool_total": self.pool_total.clone(), "stats": self.stats.clone(),
+                # the appended total the next _due() reads (copied one vector step late)
+                "total_host": int(self._total_host[0]) if self._total_ev is not None else None,
+                "counters": {k: getattr(self, k) for k in ("seed", "counter", "consumed", "updates",
+                                                           "rows_trained")},
+                "env": self.env.state_dict()}
+
+    def load_state_dict(self, sd):
+        if sd.get("format") != "mazerl.VectorPPOTrainer/1" or sd["L"] != self.L or sd["cap"] != self.cap:
+            raise ValueError("not a VectorPPOTrainer state_dict of this shape")
+        self.env.load_state_dict(sd["env"])
+        with torch.no_grad():
+            self.net.load_state_dict(sd["net"])
+        o, so = self.opt, sd["opt"]
+        if "torch" in so:
+            o.load_state_dict(so["torch"])
+        else:
+            for k, v in so.items():
+                getattr(o, k).copy_(v)
+        self.t.copy_(sd["t"])
+        live = torch.arange(self.L, device=self.device)[None, :] < self.t[:, None].long()
+        for k in self._REC:
+            getattr(self, k)[live] = sd["records"][k].to(self.device)
+        fill = int(sd["pool_fill"])
+        for k in self._POOL:
+            getattr(self, k)[:fill].copy_(sd["pool"][k])
+        self.pool_fill.fill_(fill)
+        self.pool_total.copy_(sd["pool_total"])
+        self.stats.copy_(sd["stats"])
+        for k, v in sd["counters"].items():
+            setattr(self, k, int(v))
+        self._total_ev = None
+        if sd["total_host"] is not None:  # what the saved trainer's next _due() would have read
+            self._total_host[0] = int(sd["total_host"])
+            self._total_ev = torch.cuda.Event()
+            self._total_ev.record()
+
     @torch.no_grad()
     def greedy(self, obs6, window, bits=None):
         """PPOAgent.evaluate's action (ppo_agent.py:239-252): argmax of softmax(logits), f32."""

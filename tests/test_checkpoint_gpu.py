@@ -117,3 +117,36 @@ def test_trainer_resume_is_bit_exact(tmp_path):
     assert torch.equal(ra.sw[:ra.size], rb.sw[:rb.size]) and torch.equal(ra.a[:ra.size], rb.a[:rb.size])
     A.env.close()
     B.env.close()
+
+
+def _ppo(seed):
+    from mazerl.trainers.ppo_trainer import VectorPPOTrainer
+    from mazerl.trainers.vector_trainer import make_env
+    env = make_env(512, [17, 21, 25, 29], toroidal=True, device="cuda", seed=0x70500000 + seed,
+                   done_list=False, reward64=True, window=False, window_bits=True)
+    return VectorPPOTrainer(env, "cuda", hidden_dim=256, batch_size=512, ppo_steps=2,
+                            pool_size=4096, seed=seed)
+
+
+def test_ppo_trainer_resume_is_bit_exact(tmp_path):
+    """Config 5's trainer (on-device rollout, episode records, the update pool, the captured
+    minibatch step, a maze bank per size) resumed from a file continues exactly."""
+    from mazerl.checkpoint import load_checkpoint, save_checkpoint
+    A = _ppo(1)
+    A.train(40)
+    assert A.updates > 0
+    path = save_checkpoint(str(tmp_path / "ppo.pt"), A)
+    A.train(30)
+    B = _ppo(2)
+    load_checkpoint(path, B)
+    B.train(30)
+    torch.cuda.synchronize()
+    assert A.updates == B.updates and A.counter == B.counter and A.consumed == B.consumed
+    assert torch.equal(A.stats, B.stats) and torch.equal(A.t, B.t)
+    for (ka, pa), (kb, pb) in zip(A.net.state_dict().items(), B.net.state_dict().items()):
+        assert torch.equal(pa, pb), ka
+    assert torch.equal(A.env.obs6, B.env.obs6) and torch.equal(A.env.window_bits, B.env.window_bits)
+    fill = int(A.pool_fill)
+    assert fill == int(B.pool_fill) and torch.equal(A.p_w[:fill], B.p_w[:fill])
+    A.env.close()
+    B.env.close()
