@@ -14,6 +14,12 @@
 #pragma once
 #include "mz_common.h"
 
+// Distance fields of Philox-generated mazes from the carved tree (mz_tree_dist) instead of
+// level-synchronous BFS; 0 = the BFS everywhere (A/B builds)
+#ifndef MZ_TREE_DIST
+#define MZ_TREE_DIST 1
+#endif
+
 struct MzBuildLds {
   uint8_t* g;        // [G*G] grid
   uint16_t* dist;    // [G*G]
@@ -99,11 +105,13 @@ __device__ inline int mz_fc(int k) { return k == 0 ? -1 : (k == 1 ? 1 : 0); }
 __device__ void mz_gen_rprim(const MzBuildLds& L, int G, int s, MzRng& rng) {
   uint8_t* m = L.g;
   uint16_t* fr = L.queue;
+  uint16_t* dep = L.dist;  // distance from s in the carved tree (MZ_TREE_DIST)
   uint32_t* inF = L.vis;
   for (int i = 0; i < (G * G + 31) / 32; ++i) inF[i] = 0u;
   int nf = 0;
   const int sr = s / G, sc = s - sr * G;
   m[s] = 1;
+  dep[s] = 0;
   for (int k = 0; k < 4; ++k) {
     int r = sr + mz_g2r(k), c = sc + mz_g2c(k);
     if (r < 0 || r >= G || c < 0 || c >= G) continue;
@@ -125,8 +133,11 @@ __device__ void mz_gen_rprim(const MzBuildLds& L, int G, int s, MzRng& rng) {
     if (cnt) {
       const int nn = mz_k4(nb, (int)rng.below((uint32_t)cnt));
       const int nx = nn / G, ny = nn - nx * G;
+      const int pass = ((fx + nx) / 2) * G + (fy + ny) / 2, dn = dep[nn];
       m[f] = 1;
-      m[((fx + nx) / 2) * G + (fy + ny) / 2] = 1;
+      m[pass] = 1;
+      dep[pass] = (uint16_t)(dn + 1);
+      dep[f] = (uint16_t)(dn + 2);
       for (int k = 0; k < 4; ++k) {
         int r = fx + mz_g2r(k), c = fy + mz_g2c(k);
         if (r < 0 || r >= G || c < 0 || c >= G) continue;
@@ -142,8 +153,10 @@ __device__ void mz_gen_rprim(const MzBuildLds& L, int G, int s, MzRng& rng) {
 __device__ void mz_gen_dfs(const MzBuildLds& L, int G, int s, MzRng& rng) {
   uint8_t* m = L.g;
   uint16_t* st = L.queue;
+  uint16_t* dep = L.dist;  // distance from s in the carved tree (MZ_TREE_DIST)
   int sp = 0;
   st[sp++] = (uint16_t)s;
+  dep[s] = 0;
   while (sp > 0) {
     const int top = st[sp - 1], x = top / G, y = top - x * G;
     uint64_t cand = 0;
@@ -154,9 +167,12 @@ __device__ void mz_gen_dfs(const MzBuildLds& L, int G, int s, MzRng& rng) {
     }
     if (!cnt) { --sp; continue; }
     const int k = mz_k4(cand, (int)rng.below((uint32_t)cnt));
-    m[(x + mz_fr(k)) * G + (y + mz_fc(k))] = 1;
+    const int pass = (x + mz_fr(k)) * G + (y + mz_fc(k)), dt = dep[top];
+    m[pass] = 1;
     const int nx = x + 2 * mz_fr(k), ny = y + 2 * mz_fc(k);
     m[nx * G + ny] = 1;
+    dep[pass] = (uint16_t)(dt + 1);
+    dep[nx * G + ny] = (uint16_t)(dt + 2);
     st[sp++] = (uint16_t)(nx * G + ny);
   }
 }
@@ -205,7 +221,10 @@ __device__ void mz_pk_walk(const MzBuildLds& L, int G, int cur, MzRng& rng) {
   while ((cnt = mz_pk_nbrs(L.dist, G, cur, nb)) != 0) {
     const int nx = mz_k4(nb, (int)rng.below((uint32_t)cnt));
     const int cx = cur / G, cy = cur - cx * G, x = nx / G, y = nx - x * G;
-    L.g[(cx + (x - cx) / 2) * G + (cy + (y - cy) / 2)] = 1;
+    const int pass = (cx + (x - cx) / 2) * G + (cy + (y - cy) / 2), dc = L.queue[cur];
+    L.g[pass] = 1;
+    L.queue[pass] = (uint16_t)(dc + 1);  // distance from s in the carved tree (MZ_TREE_DIST)
+    L.queue[nx] = (uint16_t)(dc + 2);
     cur = nx;
     mz_pk_mark(L, G, cur);
     L.sh[1] -= 1;
@@ -225,6 +244,7 @@ __device__ void mz_gen_primkill(const MzBuildLds& L, int G, int s, MzRng& rng) {
   __syncthreads();
   if (lane == 0) {
     L.sh[1] = W * W - 1;  // unmarked count
+    L.queue[s] = 0;
     mz_pk_mark(L, G, s);
     mz_pk_walk(L, G, s, rng);
   }
@@ -272,9 +292,10 @@ __device__ void mz_gen_primkill(const MzBuildLds& L, int G, int s, MzRng& rng) {
   }
 }
 
-// find_random_position (maze_generation.py:187-218) on the euclidean G x G grid
-__device__ int mz_goal_select(const MzBuildLds& L, int G, int s) {
-  mz_wave_bfs(L, G, false, s);
+// find_random_position (maze_generation.py:187-218) on the euclidean G x G grid, from dist =
+// the distance of every open square from the start s: the dead end (odd cell, exactly one open
+// neighbour, not s) with the largest path length, the first in row-major order on ties
+__device__ int mz_goal_scan(const MzBuildLds& L, int G, int s, const uint16_t* dist) {
   const int lane = threadIdx.x, C = G * G;
   uint32_t best = 0;  // (dist << 16) | (0xFFFF - idx); 0 = none
   for (int p = lane; p < C; p += 64) {
@@ -282,7 +303,7 @@ __device__ int mz_goal_select(const MzBuildLds& L, int G, int s) {
     if (!(r & 1) || !(c & 1) || L.g[p] != 1 || p == s || r + 1 >= G || c + 1 >= G) continue;
     const int nb = (L.g[p - G] != 0) + (L.g[p + G] != 0) + (L.g[p - 1] != 0) + (L.g[p + 1] != 0);
     if (nb != 1) continue;
-    const uint32_t key = ((uint32_t)(L.dist[p] + 1) << 16) | (uint32_t)(0xFFFF - p);
+    const uint32_t key = ((uint32_t)(dist[p] + 1) << 16) | (uint32_t)(0xFFFF - p);
     best = key > best ? key : best;
   }
   for (int o = 32; o > 0; o >>= 1) {
@@ -290,6 +311,82 @@ __device__ int mz_goal_select(const MzBuildLds& L, int G, int s) {
     best = x > best ? x : best;
   }
   return best ? (int)(0xFFFF - (best & 0xFFFF)) : -1;
+}
+
+__device__ int mz_goal_select(const MzBuildLds& L, int G, int s) {
+  mz_wave_bfs(L, G, false, s);
+  return mz_goal_scan(L, G, s, L.dist);
+}
+
+// Distance-to-goal field of a perfect maze without a level-synchronous BFS (MZ_TREE_DIST).
+// The Philox generators carve a spanning tree of the open squares rooted at the start s and
+// record each square's depth (its distance from s) in L.queue as they carve. In that tree every
+// open square's open neighbours are its parent (depth - 1) and its children (depth + 1), so
+//   D(x) = dep(x) + dep(goal) - 2 dep(a(x)),  a(x) = x's first ancestor on the goal's root path,
+// which is what mz_wave_bfs(L, N, false, goal) computes (a BFS over a tree is its path lengths).
+// A BFS costs one wave-synchronous round per level (up to ~3,200 levels at 81 x 81); this costs
+// one pass for the parents, one serial walk from the goal to s marking its path (L.vis), and
+// ~log2(depth) pointer-jumping passes. Returns false (L.dist untouched except scratch, the caller
+// runs the BFS) if the grid is not such a tree (a square without a parent, a walk that does not
+// reach s, or no convergence in 32 passes) — never for the generators here.
+__device__ bool mz_tree_dist(const MzBuildLds& L, int N, int s, int goal) {
+  const int lane = threadIdx.x, C = N * N;
+  const uint16_t* dep = L.queue;
+  uint16_t* A = L.dist;  // parent, then first ancestor on the goal path, then D
+  bool bad = false;
+  for (int p = lane; p < C; p += 64) {
+    uint16_t a = 0xFFFF;
+    if (L.g[p] != 0) {
+      a = (uint16_t)p;  // the root points to itself
+      if (p != s) {
+        const int r = p / N, c = p - r * N, want = (int)dep[p] - 1;
+        a = 0xFFFF;
+        if (r > 0 && L.g[p - N] != 0 && dep[p - N] == want) a = (uint16_t)(p - N);
+        if (r + 1 < N && L.g[p + N] != 0 && dep[p + N] == want) a = (uint16_t)(p + N);
+        if (c > 0 && L.g[p - 1] != 0 && dep[p - 1] == want) a = (uint16_t)(p - 1);
+        if (c + 1 < N && L.g[p + 1] != 0 && dep[p + 1] == want) a = (uint16_t)(p + 1);
+        bad |= a == 0xFFFF;
+      }
+    }
+    A[p] = a;
+  }
+  for (int i = lane; i < (C + 31) / 32; i += 64) L.vis[i] = 0u;
+  if (__any(bad)) return false;
+  __syncthreads();
+  if (lane == 0) {  // mark the goal's root path
+    int x = goal, n = 0;
+    for (; n <= C; ++n) {
+      L.vis[x >> 5] |= 1u << (x & 31);
+      if (x == s) break;
+      x = A[x];
+      if (x == 0xFFFF) { n = C + 1; break; }
+    }
+    L.sh[3] = n > C;
+  }
+  __syncthreads();
+  if (L.sh[3]) return false;
+  // pointer jumping, in place: A[p] only ever moves up p's root path and never past a marked
+  // square, so any interleaving of the lanes' updates converges to a(p)
+  bool conv = false;
+  for (int it = 0; it < 32 && !conv; ++it) {
+    bool ch = false;
+    for (int p = lane; p < C; p += 64) {
+      const int a = A[p];
+      if (a == 0xFFFF || ((L.vis[a >> 5] >> (a & 31)) & 1u)) continue;
+      A[p] = A[a];
+      ch = true;
+    }
+    conv = !__any(ch);
+    __syncthreads();
+  }
+  if (!conv) return false;
+  const int dg = dep[goal];
+  for (int p = lane; p < C; p += 64) {
+    const int a = A[p];
+    if (a != 0xFFFF) A[p] = (uint16_t)((int)dep[p] + dg - 2 * (int)dep[a]);
+  }
+  __syncthreads();
+  return true;
 }
 
 // Cell word of open cell (r,c) of the final N x N maze in L.g with distance field L.dist.
@@ -358,6 +455,7 @@ __device__ void mz_build_one(const MzDev& d, int e, bool tor, bool generate, int
   const int lane = threadIdx.x;
   const MzBuildLds L = mz_build_lds(lds, d.P);
   int sr, sc, gr, gc;
+  bool tree = false;  // L.queue holds the carve depths of a perfect euclidean maze
   if (generate && pymode != MZ_PY_PHILOX) {
     const int G = tor ? N + 2 : N;
     for (int i = lane; i < G * G; i += 64) L.g[i] = 0;
@@ -407,13 +505,17 @@ __device__ void mz_build_one(const MzDev& d, int e, bool tor, bool generate, int
     __syncthreads();
     s = L.sh[2];
     if (algo != MZ_ALGO_RPRIM_DEV && algo != MZ_ALGO_DFS_DEV) mz_gen_primkill(L, G, s, rng);
+    else  // r-prim / dfs carve depths into L.dist (their stack / frontier lives in L.queue)
+      for (int i = lane; i < G * G; i += 64) L.queue[i] = L.dist[i];
     __syncthreads();
-    int goal = mz_goal_select(L, G, s);
+    // goal from the carve depths (== a BFS from s over the carved tree)
+    int goal = MZ_TREE_DIST ? mz_goal_scan(L, G, s, L.queue) : mz_goal_select(L, G, s);
     if (goal < 0) goal = s;  // unreachable for G >= 5 (a spanning tree has >= 2 leaves)
     __syncthreads();
     if (lane == 0) L.g[goal] = 2;
     __syncthreads();
     sr = s / G; sc = s - sr * G; gr = goal / G; gc = goal - gr * G;
+    tree = MZ_TREE_DIST && !tor;
     if (tor) {  // crop the border (maze_generation.py:53-55)
       for (int i = lane; i < N * N; i += 64) {
         const int r = i / N, c = i - r * N;
@@ -429,8 +531,10 @@ __device__ void mz_build_one(const MzDev& d, int e, bool tor, bool generate, int
     sr = isr; sc = isc; gr = igr; gc = igc;
     __syncthreads();
   }
-  // distance-to-goal field (len(find_path(p)) = D[p] + 1)
-  mz_wave_bfs(L, N, tor, gr * N + gc);
+  // distance-to-goal field (len(find_path(p)) = D[p] + 1): from the carved tree for
+  // a Philox-generated euclidean maze, else a BFS (toroidal: the crop's wrap adds cycles;
+  // imported and CPython-exact mazes carry no carve depths)
+  if (!tree || !mz_tree_dist(L, N, sr * N + sc, gr * N + gc)) mz_wave_bfs(L, N, tor, gr * N + gc);
   const size_t es = (size_t)e;
   const int P = d.P;
   for (int p = lane; p < P * P; p += 64) {

@@ -606,6 +606,21 @@ __device__ inline bool regen_winner(const MzDev& d, int e) {
   return e < d.B && ((d.posw[e] >> 20) & 1u) && d.last_term[e];
 }
 
+// Copy n words, each lane keeping 16 loads in flight (a one-word-per-pass loop waits a full
+// round trip per 256 B: 103 of them for an 81 x 81 maze's cell words).
+__device__ inline void wave_copy(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src,
+                                 size_t n) {
+  constexpr int U = 16;
+  for (size_t i = threadIdx.x & (WAVE - 1); i < n; i += U * WAVE) {
+    uint32_t v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = i + u * WAVE < n ? src[i + u * WAVE] : 0u;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i + u * WAVE < n) dst[i + u * WAVE] = v[u];
+  }
+}
+
 // Copy bank slot `slot` of class `cls` (bank_class) into instance e (cells + plane rows + meta;
 // reset_one then rebuilds the per-episode state). Returns false (the caller builds in place) for
 // cls < 0 or an exhausted bank (slot >= K). The slots come from k_bank_count / k_bank_scan: the
@@ -617,13 +632,9 @@ __device__ bool bank_take(const MzDev& d, int e, int cls, int slot) {
   const size_t src = ((size_t)mz_bank_aidx(d.bk_amask, a) * d.bk_nd + di) * d.bk_K + slot;
   const size_t es = (size_t)e;
   const size_t pp = (size_t)d.P * d.P;
-  const uint32_t* cs = d.bk_cells + src * pp;
-  uint32_t* cd = d.cells + es * pp;
-  for (size_t i = threadIdx.x; i < pp; i += WAVE) cd[i] = cs[i];
+  wave_copy(d.cells + es * pp, d.bk_cells + src * pp, pp);
   const size_t pw = (size_t)d.PW;
-  const uint32_t* ps = d.bk_planes + src * pw;
-  uint32_t* pd = d.planes + es * pw;
-  for (size_t i = threadIdx.x; i < pw; i += WAVE) pd[i] = ps[i];
+  wave_copy(d.planes + es * pw, d.bk_planes + src * pw, pw);
   if (threadIdx.x == 0) {
     d.meta0[e] = d.bk_meta0[src];
     d.meta1[e] = d.bk_meta1[src];
@@ -692,15 +703,22 @@ __global__ __launch_bounds__(WAVE) void k_bank_fill(MzDev bd, const int* head, i
 }
 
 // Auto-reset by flag scan: each wave looks at 64 instances' done flags (one coalesced load),
-// then resets its done instances cooperatively, one after another — waves with nothing to do
-// exit at once, no device list or counter is involved. With regen, instances whose last step
-// terminated first get a new maze (win -> update_maze, off_policy_trainer.py:190-202).
+// then resets the done instances of its share of them cooperatively, one after another — waves
+// with nothing to do exit at once, no device list or counter is involved. With regen, instances
+// whose last step terminated first get a new maze (win -> update_maze,
+// off_policy_trainer.py:190-202). MZ_RD_SPLIT waves share a 64-instance group (each resets the
+// done instances of 64 / MZ_RD_SPLIT of its lanes): a reset is a chain of ~10 dependent global
+// round trips, and the launch lasts as long as the group with the most done instances.
+#ifndef MZ_RD_SPLIT
+#define MZ_RD_SPLIT 4
+#endif
 template <bool TOR, bool ENRICH>
 __global__ __launch_bounds__(WAVE) void k_reset_done(MzDev d, int regen, uint64_t seed,
                                                      uint32_t epoch, MzOut o) {
   extern __shared__ __align__(16) uint8_t lds[];
   __shared__ __align__(16) uint32_t wsh[32];
-  const int lane = threadIdx.x, e = blockIdx.x * WAVE + lane;
+  const int grp = blockIdx.x / MZ_RD_SPLIT, part = blockIdx.x - grp * MZ_RD_SPLIT;
+  const int lane = threadIdx.x, e = grp * WAVE + lane;
   const bool done = e < d.B && ((d.posw[e] >> 20) & 1u);
   // this lane's bank slot if it is a winner with a bank class: the group's first slot of the
   // class (k_bank_scan) + its rank among the group's winners of the class
@@ -711,15 +729,17 @@ __global__ __launch_bounds__(WAVE) void k_reset_done(MzDev d, int regen, uint64_
     while (pend) {
       const int cj = __shfl(cls, __ffsll((long long)pend) - 1);
       const unsigned long long m = __ballot(cls == cj);
-      if (cls == cj) slot = d.bk_slot[cj * d.bk_G + blockIdx.x] + __popcll(m & ((1ull << lane) - 1ull));
+      if (cls == cj) slot = d.bk_slot[cj * d.bk_G + grp] + __popcll(m & ((1ull << lane) - 1ull));
       pend &= ~m;
     }
   }
-  unsigned long long bal = __ballot(done);
+  constexpr int SH = WAVE / MZ_RD_SPLIT;
+  const unsigned long long share = (~0ull >> (WAVE - SH)) << (part * SH);
+  unsigned long long bal = __ballot(done) & share;
   while (bal) {
     const int j = __ffsll((long long)bal) - 1;
     bal &= bal - 1;
-    const int ej = blockIdx.x * WAVE + j;
+    const int ej = grp * WAVE + j;
     const int cj = __shfl(cls, j), sj = __shfl(slot, j);
     if (regen && d.last_term[ej]) {
       const int a = d.algo[ej], N = (int)(d.meta0[ej] & 0xFF);

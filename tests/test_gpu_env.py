@@ -104,6 +104,38 @@ def test_generation_matches_oracle(mazerl, tor, dims):
         env.close()
 
 
+def _cell_words(env):
+    """The handle's cell words [B, P, P] (the first section of mz_state_save's blob)."""
+    blob = env.state_dict()["device_state"].cpu().numpy()
+    B, P = env.num_envs, env.max_dim
+    return blob[256:256 + B * P * P * 4].view(np.uint32).reshape(B, P, P)
+
+
+@pytest.mark.parametrize("tor,dims", [(False, (15, 21, 41, 81, 127)), (True, (17, 41, 79))])
+def test_generated_distance_field_matches_bfs(mazerl, tor, dims):
+    """The distance-to-goal field in the cell words (len(find_path(p)) = D[p] + 1, a5) of
+    Philox-generated mazes — derived from the carved tree (mz_tree_dist) for euclidean mazes,
+    by the wave BFS on the torus — == the oracle's BFS from the goal on every open cell, and the
+    open / open-neighbour bits == the grid, for all three generators."""
+    import pyoracle as O
+    B = 48
+    algos = np.arange(B) % 3
+    for dim in dims:
+        env = mazerl.VectorMazeEnv(B, dim, toroidal=tor, enrich=False, generate=False)
+        env.generate(algorithm=algos, dim=dim, seed=0xD15700 + dim)
+        torch.cuda.synchronize()
+        cw = _cell_words(env)
+        for i in range(B):
+            g = env.grid(i)
+            q = env.query(i)
+            want = O.bfs(g, (q["goal_r"], q["goal_c"]), tor)
+            w = cw[i, :dim, :dim]
+            open_ = g != 0
+            np.testing.assert_array_equal((w >> 16) & 1, open_.astype(np.uint32), err_msg=f"dim {dim} env {i}")
+            np.testing.assert_array_equal((w & 0x1FFF)[open_], want[open_], err_msg=f"dim {dim} env {i} algo {algos[i]}")
+        env.close()
+
+
 @pytest.mark.parametrize("tor,dims", [(False, (81, 127)), (True, (79, 125))])
 def test_primkill_restart_pick_matches_oracle(mazerl, tor, dims):
     """prim&kill's restart pick (maze_generation.py:151: the k-th marked cell with an unmarked
