@@ -366,7 +366,8 @@ __device__ bool mz_tree_dist(const MzBuildLds& L, int N, int s, int goal) {
   __syncthreads();
   if (L.sh[3]) return false;
   // pointer jumping, in place: A[p] only ever moves up p's root path and never past a marked
-  // square, so any interleaving of the lanes' updates converges to a(p)
+  // square, so any interleaving of the lanes' updates converges to a(p) (for an unmarked p;
+  // a marked p keeps its parent here and is its own a(p) below)
   bool conv = false;
   for (int it = 0; it < 32 && !conv; ++it) {
     bool ch = false;
@@ -382,8 +383,9 @@ __device__ bool mz_tree_dist(const MzBuildLds& L, int N, int s, int goal) {
   if (!conv) return false;
   const int dg = dep[goal];
   for (int p = lane; p < C; p += 64) {
-    const int a = A[p];
-    if (a != 0xFFFF) A[p] = (uint16_t)((int)dep[p] + dg - 2 * (int)dep[a]);
+    if (A[p] == 0xFFFF) continue;
+    const int a = ((L.vis[p >> 5] >> (p & 31)) & 1u) ? p : A[p];  // a path square is its own a()
+    A[p] = (uint16_t)((int)dep[p] + dg - 2 * (int)dep[a]);
   }
   __syncthreads();
   return true;
