@@ -986,7 +986,7 @@ hipError_t mz_launch_reset_list(const MzDev& d, const int32_t* idx, int32_t* cou
 
 hipError_t mz_launch_reset_done(const MzDev& d, int regen, uint64_t seed, uint32_t epoch,
                                 const MzOut& o, hipStream_t s) {
-  const int blocks = (d.B + WAVE - 1) / WAVE;
+  const int blocks = (d.B + WAVE - 1) / WAVE * MZ_RD_SPLIT;  // MZ_RD_SPLIT waves per 64 instances
   size_t lds = 0;
   hipError_t ae = hipSuccess;
   if (regen && d.bk_K) {  // the winners' bank slots, in instance order (k_bank_count / k_bank_scan)
