@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--iters", type=int, default=1000)
     ap.add_argument("--lib", default=None)
+    ap.add_argument("--bits", action="store_true",
+                    help="the trainers' mode: 675-bit window only (window_bits=True, no f32 window)")
     ap.add_argument("--toroidal-variable", action="store_true",
                     help="config 5 shape: toroidal grids 17..79 (instance i gets 17 + 2 (i mod 32))")
     a = ap.parse_args()
@@ -36,7 +38,7 @@ def main():
                        window=True, window_bits=False, pos=False, done_list=False)
     else:
         env = mazerl.VectorMazeEnv(a.envs, a.dim, enrich=True, device="cuda:0", seed=0x5EED0000,
-                                   window=True, window_bits=False, pos=False, done_list=False)
+                                   window=not a.bits, window_bits=a.bits, pos=False, done_list=False)
     st = torch.cuda.current_stream()
     for k in range(a.warmup):
         env.step_act(eps=1.0, seed=0xBE7C4, counter=k, autoreset=True)
@@ -52,7 +54,7 @@ def main():
     e1.record(st)
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / a.iters * 1e3
-    print(json.dumps({"lib": a.lib or "in-tree", "us_per_launch": round(us, 2),
+    print(json.dumps({"lib": a.lib or "in-tree", "bits": a.bits, "envs": a.envs, "us_per_launch": round(us, 2),
                       "resets_per_launch": float(resets) / 50.0}), flush=True)
     env.close()
 

@@ -11,7 +11,7 @@ if [ "$1" = build ]; then
     "$R/profiles/build_variant.sh" "$R/profiles/_bin/probe_$v.so" -DMZ_PROBE=$v &
   done
   wait
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o "$R/profiles/_bin/ubench_store" "$R/profiles/ubench_store.hip"
+  [ -n "$NO_UBENCH" ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o "$R/profiles/_bin/ubench_store" "$R/profiles/ubench_store.hip"
   exit 0
 fi
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
