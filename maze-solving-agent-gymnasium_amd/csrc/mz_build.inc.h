@@ -391,26 +391,28 @@ __device__ bool mz_tree_dist(const MzBuildLds& L, int N, int s, int goal) {
   return true;
 }
 
-// Cell word of open cell (r,c) of the final N x N maze in L.g with distance field L.dist.
-__device__ inline uint32_t mz_cell_word(const MzBuildLds& L, int N, bool tor, int r, int c,
-                                        int gr, int gc) {
+// Cell word of open cell (r,c) of the final N x N maze: open(r, c) (0 <= r, c < N) and dist(r, c)
+// (open squares) describe the maze and its distance-to-goal field.
+template <class OPEN, class DIST>
+__device__ inline uint32_t mz_cell_word_f(const OPEN& open, const DIST& dist, int N, bool tor,
+                                          int r, int c, int gr, int gc) {
   const int M = 2 * N;  // best-dir A* depth 2*min(H,W) (base_maze_env.py:244)
-  const uint32_t D = L.dist[r * N + c];
+  const uint32_t D = (uint32_t)dist(r, c);
   uint32_t nbm = 0u;
   int code = 4;
   double best = __longlong_as_double(0x7FF0000000000000ll);  // +inf
   for (int k = 0; k < 4; ++k) {
     // get_direction_mask / get_toroidal_direction_mask (maze_handler.py:122-162)
     const int mr = mz_wrap(r + mz_dr(k), N), mc = mz_wrap(c + mz_dc(k), N);
-    if (L.g[mr * N + mc] != 0) nbm |= 1u << k;
+    if (open(mr, mc)) nbm |= 1u << k;
   }
   for (int k = 0; k < 4; ++k) {  // _find_best_next_cell (base_maze_env.py:237-260)
     int nr = r + mz_dr(k), nc = c + mz_dc(k);
     bool valid;
-    if (tor) { nr = mz_wrap(nr, N); nc = mz_wrap(nc, N); valid = L.g[nr * N + nc] != 0; }
-    else valid = 0 < nr && nr < N && 0 < nc && nc < N && L.g[nr * N + nc] != 0;
+    if (tor) { nr = mz_wrap(nr, N); nc = mz_wrap(nc, N); valid = open(nr, nc); }
+    else valid = 0 < nr && nr < N && 0 < nc && nc < N && open(nr, nc);
     if (!valid) continue;
-    const int dn = L.dist[nr * N + nc];
+    const int dn = dist(nr, nc);
     const int len = (dn < M ? dn : M) + 1;
     const int manh = abs(nr - gr) + abs(nc - gc);
     const double score = __dadd_rn((double)len, __dmul_rn(0.15, (double)manh));
@@ -418,6 +420,438 @@ __device__ inline uint32_t mz_cell_word(const MzBuildLds& L, int N, bool tor, in
     if (nr == gr && nc == gc) { code = k; break; }
   }
   return D | ((uint32_t)code << MZ_CELL_CODE_SHIFT) | MZ_CELL_OPEN | (nbm << MZ_CELL_NB_SHIFT);
+}
+
+__device__ inline uint32_t mz_cell_word(const MzBuildLds& L, int N, bool tor, int r, int c,
+                                        int gr, int gc) {
+  return mz_cell_word_f([&](int y, int x) { return L.g[y * N + x] != 0; },
+                        [&](int y, int x) { return (int)L.dist[y * N + x]; }, N, tor, r, c, gr, gc);
+}
+
+// Writes instance e's tables from a built maze: cell words, the open / visited plane strips
+// (mz_common.h; visited = {start}), meta / reset state with set_max_steps. All lanes call.
+template <class OPEN, class DIST>
+__device__ void mz_build_write(const MzDev& d, int e, int N, bool tor, int sr, int sc, int gr,
+                               int gc, const OPEN& open, const DIST& dist) {
+  const int lane = threadIdx.x;
+  const size_t es = (size_t)e;
+  const int P = d.P;
+  for (int p = lane; p < P * P; p += 64) {
+    const int r = p / P, c = p - r * P;
+    const bool op = r < N && c < N && open(r, c);
+    d.cells[es * P * P + p] = op ? mz_cell_word_f(open, dist, N, tor, r, c, gr, gc) : 0u;
+  }
+  for (int k = lane; k < d.NS * P; k += 64) {
+    const int st = k / P, R = k - st * P;
+    uint32_t o = 0u, v = 0u;
+    if (R < N) {
+      for (int j = 0; j < 32; ++j) {
+        int c = MZ_STRIP_STRIDE * st + j;
+        if (tor) c = mz_wrap(c, N);
+        else if (c >= N) break;
+        if (open(R, c)) o |= 1u << j;
+      }
+      if (R == sr) v = mz_strip_colmask(st, sc, N, tor);
+    }
+    *mz_strip_row(d, es, st, R) = make_uint2(o, v);
+  }
+  if (lane == 0) {
+    // set_max_steps: ceil((((H-1)*(W-1)) - 1) * (len / CE)), CE = (H-1)*((W-1)//2) - 1
+    const int len = dist(sr, sc) + 1;
+    const int ce = (N - 1) * ((N - 1) / 2) - 1;
+    const double Lf = __ddiv_rn((double)len, (double)ce);
+    const double prod = __dmul_rn((double)((N - 1) * (N - 1) - 1), Lf);
+    int maxs = (int)ceil(prod);
+    if (maxs > 65535) maxs = 65535;
+    d.meta0[e] = (uint32_t)N | ((uint32_t)N << 8) | ((uint32_t)sr << 16) | ((uint32_t)sc << 24);
+    d.meta1[e] = (uint32_t)gr | ((uint32_t)gc << 8) | ((uint32_t)maxs << 16);
+    d.posw[e] = (uint32_t)sr | ((uint32_t)sc << 8);
+    d.stw[e] = 0u;
+    d.last_term[e] = 0;
+    // curw = cells word at start, from LDS (no read-back of global stores inside the launch)
+    d.curw[e] = mz_cell_word_f(open, dist, N, tor, sr, sc, gr, gc);
+  }
+  __syncthreads();
+}
+
+// ---- Cell-space build of a Philox euclidean maze (MZ_CELL_BUILD) ---------------------------
+// A perfect maze lives on its odd squares: cell q = (r >> 1) * W + (c >> 1), W = (N - 1) / 2.
+// The generators below carve the same spanning tree as mz_gen_* (the same Philox draws over the
+// same candidate lists in the same order, the same swap-remove frontier), but keep per cell only
+// the passages to its right and lower neighbours, two bit sets, the frontier / stack list, the
+// carve depth and the distance field: ~7.3 B per cell (11.7 KB at 81 x 81) where the square grid
+// needs ~5.1 B per square (35 KB), so 13 builds share a CU instead of 4 (each build is a serial
+// lane-0 chain of LDS round trips: throughput is the number of builds in flight).
+#ifndef MZ_CELL_BUILD
+#define MZ_CELL_BUILD 1
+#endif
+
+struct MzCellLds {
+  uint8_t* pas;    // [Q] bit 0: passage to the right neighbour, bit 1: to the one below
+  uint32_t* b0;    // [QW] in maze (r-prim, dfs) / marked (prim&kill)
+  uint32_t* b1;    // [QW] in frontier (r-prim) / restart candidate (prim&kill), then goal path
+  uint16_t* list;  // [Q] frontier (r-prim) / stack (dfs) / BFS queue
+  uint16_t* dep;   // [Q] carve depth: distance from the start in squares
+  uint16_t* A;     // [Q] parent, first goal-path ancestor, then the distance to the goal
+  int* sh;
+  int W, Q;
+};
+
+__host__ __device__ inline size_t mz_cell_lds_bytes(int P) {
+  const size_t W = (size_t)P / 2, Q = W * W, QW = (Q + 31) / 32;
+  return 64 + mz_align16(Q) + 2 * mz_align16(4 * QW) + 3 * mz_align16(2 * Q);
+}
+
+__device__ inline MzCellLds mz_cell_lds(uint8_t* base, int P, int N) {
+  const size_t Wp = (size_t)P / 2, Qp = Wp * Wp, QW = (Qp + 31) / 32;
+  MzCellLds L;
+  L.sh = reinterpret_cast<int*>(base);
+  size_t off = 64;
+  L.pas = base + off; off += mz_align16(Qp);
+  L.b0 = reinterpret_cast<uint32_t*>(base + off); off += mz_align16(4 * QW);
+  L.b1 = reinterpret_cast<uint32_t*>(base + off); off += mz_align16(4 * QW);
+  L.list = reinterpret_cast<uint16_t*>(base + off); off += mz_align16(2 * Qp);
+  L.dep = reinterpret_cast<uint16_t*>(base + off); off += mz_align16(2 * Qp);
+  L.A = reinterpret_cast<uint16_t*>(base + off);
+  L.W = (N - 1) / 2;
+  L.Q = L.W * L.W;
+  return L;
+}
+
+__device__ inline bool cs_bit(const uint32_t* b, int q) { return (b[q >> 5] >> (q & 31)) & 1u; }
+__device__ inline void cs_set(uint32_t* b, int q) { b[q >> 5] |= 1u << (q & 31); }
+__device__ inline void cs_clr(uint32_t* b, int q) { b[q >> 5] &= ~(1u << (q & 31)); }
+
+// neighbour cell of q in direction k — 0 up, 1 down, 2 left, 3 right (the generators' order
+// (-2,0),(2,0),(0,-2),(0,2), maze_generation.py:72) — or -1 outside the grid
+__device__ inline int cs_nb(int q, int k, int W) {
+  const int r = q / W, c = q - r * W;
+  if (k == 0) return r > 0 ? q - W : -1;
+  if (k == 1) return r + 1 < W ? q + W : -1;
+  if (k == 2) return c > 0 ? q - 1 : -1;
+  return c + 1 < W ? q + 1 : -1;
+}
+// open the passage from q in direction k
+__device__ inline void cs_link(const MzCellLds& L, int q, int k) {
+  if (k == 0) L.pas[q - L.W] |= 2;
+  else if (k == 1) L.pas[q] |= 2;
+  else if (k == 2) L.pas[q - 1] |= 1;
+  else L.pas[q] |= 1;
+}
+// whether the passage from q in direction k is open (the neighbour exists)
+__device__ inline bool cs_open_dir(const MzCellLds& L, int q, int k) {
+  const int r = q / L.W, c = q - r * L.W;
+  if (k == 0) return r > 0 && (L.pas[q - L.W] & 2);
+  if (k == 1) return (L.pas[q] & 2) != 0;
+  if (k == 2) return c > 0 && (L.pas[q - 1] & 1);
+  return (L.pas[q] & 1) != 0;
+}
+
+// random_prim_visit (maze_generation.py:59-99), lane 0; as mz_gen_rprim
+__device__ void mz_cs_rprim(const MzCellLds& L, int s, MzRng& rng) {
+  const int W = L.W;
+  int nf = 0;
+  cs_set(L.b0, s);
+  L.dep[s] = 0;
+  for (int k = 0; k < 4; ++k) {
+    const int j = cs_nb(s, k, W);
+    if (j >= 0) { L.list[nf++] = (uint16_t)j; cs_set(L.b1, j); }
+  }
+  while (nf > 0) {
+    const int i = (int)rng.below((uint32_t)nf);
+    const int f = L.list[i];
+    L.list[i] = L.list[--nf];
+    uint64_t nb = 0;  // in-maze neighbours: cell | direction from f << 12
+    int cnt = 0;
+    for (int k = 0; k < 4; ++k) {
+      const int j = cs_nb(f, k, W);
+      if (j >= 0 && cs_bit(L.b0, j)) mz_k4_push(nb, cnt, j | (k << 12));
+    }
+    if (cnt) {
+      const int v = mz_k4(nb, (int)rng.below((uint32_t)cnt)), nn = v & 0xFFF;
+      cs_set(L.b0, f);
+      cs_link(L, f, v >> 12);
+      L.dep[f] = (uint16_t)(L.dep[nn] + 2);
+      for (int k = 0; k < 4; ++k) {
+        const int j = cs_nb(f, k, W);
+        if (j >= 0 && !cs_bit(L.b0, j) && !cs_bit(L.b1, j)) {
+          L.list[nf++] = (uint16_t)j;
+          cs_set(L.b1, j);
+        }
+      }
+    }
+  }
+}
+
+// deept_first_visit (maze_generation.py:101-128), lane 0; as mz_gen_dfs. Its direction order
+// (0,-1),(0,1),(-1,0),(1,0) is left, right, up, down.
+__device__ void mz_cs_dfs(const MzCellLds& L, int s, MzRng& rng) {
+  const int W = L.W;
+  int sp = 0;
+  L.list[sp++] = (uint16_t)s;
+  cs_set(L.b0, s);
+  L.dep[s] = 0;
+  while (sp > 0) {
+    const int top = L.list[sp - 1];
+    uint64_t cand = 0;
+    int cnt = 0;
+    for (int k = 0; k < 4; ++k) {
+      const int j = cs_nb(top, k == 0 ? 2 : (k == 1 ? 3 : k - 2), W);
+      if (j >= 0 && !cs_bit(L.b0, j)) mz_k4_push(cand, cnt, k);
+    }
+    if (!cnt) { --sp; continue; }
+    const int k = mz_k4(cand, (int)rng.below((uint32_t)cnt));
+    const int dir = k == 0 ? 2 : (k == 1 ? 3 : k - 2);
+    const int j = cs_nb(top, dir, W);
+    cs_link(L, top, dir);
+    cs_set(L.b0, j);
+    L.dep[j] = (uint16_t)(L.dep[top] + 2);
+    L.list[sp++] = (uint16_t)j;
+  }
+}
+
+// prim_and_kill_visit (maze_generation.py:130-185); as mz_gen_primkill: b0 = marked, b1 = the
+// restart candidates (marked cells with an unmarked neighbour), kept current by the walk
+__device__ inline int mz_cs_pk_nbrs(const MzCellLds& L, int p, uint64_t& out) {
+  int cnt = 0;
+  out = 0;
+  for (int k = 0; k < 4; ++k) {
+    const int j = cs_nb(p, k, L.W);
+    if (j >= 0 && !cs_bit(L.b0, j)) mz_k4_push(out, cnt, j | (k << 12));
+  }
+  return cnt;
+}
+__device__ inline void mz_cs_pk_mark(const MzCellLds& L, int p) {
+  uint64_t tmp;
+  cs_set(L.b0, p);
+  if (mz_cs_pk_nbrs(L, p, tmp) > 0) cs_set(L.b1, p); else cs_clr(L.b1, p);
+  for (int k = 0; k < 4; ++k) {
+    const int n = cs_nb(p, k, L.W);
+    if (n >= 0 && cs_bit(L.b0, n) && mz_cs_pk_nbrs(L, n, tmp) == 0) cs_clr(L.b1, n);
+  }
+}
+__device__ void mz_cs_pk_walk(const MzCellLds& L, int cur, MzRng& rng) {
+  uint64_t nb;
+  int cnt;
+  while ((cnt = mz_cs_pk_nbrs(L, cur, nb)) != 0) {
+    const int v = mz_k4(nb, (int)rng.below((uint32_t)cnt)), nx = v & 0xFFF;
+    cs_link(L, cur, v >> 12);
+    L.dep[nx] = (uint16_t)(L.dep[cur] + 2);
+    cur = nx;
+    mz_cs_pk_mark(L, cur);
+    L.sh[1] -= 1;
+  }
+}
+__device__ void mz_cs_primkill(const MzCellLds& L, int s, MzRng& rng) {
+  const int lane = threadIdx.x, nw = (L.Q + 31) / 32;
+  if (lane == 0) {
+    L.sh[1] = L.Q - 1;  // unmarked count
+    L.dep[s] = 0;
+    mz_cs_pk_mark(L, s);
+    mz_cs_pk_walk(L, s, rng);
+  }
+  __syncthreads();
+  while (L.sh[1] > 0) {
+    int total = 0;
+    for (int b = 0; b < nw; b += 64) {
+      int pc = b + lane < nw ? __popc(L.b1[b + lane]) : 0;
+      for (int o = 32; o > 0; o >>= 1) pc += __shfl_xor(pc, o);
+      total += pc;
+    }
+    int k = 0;
+    if (lane == 0) k = (int)rng.below((uint32_t)total);
+    k = __shfl(k, 0);
+    int chosen = -1;
+    for (int b = 0; b < nw && chosen < 0; b += 64) {
+      const int w = b + lane;
+      const uint32_t v = w < nw ? L.b1[w] : 0u;
+      const int pc = __popc(v);
+      int inc = pc;  // inclusive prefix sum over the lanes' words
+      for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(inc, o);
+        if (lane >= o) inc += t;
+      }
+      const int tot = __shfl(inc, 63);
+      if (k < tot) {
+        const unsigned long long bal = __ballot(inc > k && inc - pc <= k);
+        const int src = __ffsll((long long)bal) - 1;
+        int q = 0;
+        if (lane == src) {
+          uint32_t m = v;
+          for (int t = inc - pc; t < k; ++t) m &= m - 1;  // drop the lower candidates
+          q = w * 32 + __ffs(m) - 1;
+        }
+        chosen = __shfl(q, src);
+      } else {
+        k -= tot;
+      }
+    }
+    __syncthreads();
+    if (chosen < 0) break;  // unreachable for a connected cell grid; never walk from -1
+    if (lane == 0) mz_cs_pk_walk(L, chosen, rng);
+    __syncthreads();
+  }
+}
+
+// find_random_position (maze_generation.py:187-218) from the carve depths: as mz_goal_scan
+// (same key: path length, then the smallest square index); returns the goal cell or -1
+__device__ int mz_cs_goal(const MzCellLds& L, int N, int s) {
+  const int lane = threadIdx.x, W = L.W;
+  uint32_t best = 0;
+  for (int q = lane; q < L.Q; q += 64) {
+    if (q == s) continue;
+    int nb = 0;
+    for (int k = 0; k < 4; ++k) nb += cs_open_dir(L, q, k);
+    if (nb != 1) continue;
+    const int r = q / W, c = q - r * W, p = (2 * r + 1) * N + 2 * c + 1;
+    const uint32_t key = ((uint32_t)(L.dep[q] + 1) << 16) | (uint32_t)(0xFFFF - p);
+    best = key > best ? key : best;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t x = __shfl_xor(best, o);
+    best = x > best ? x : best;
+  }
+  if (!best) return -1;
+  const int p = 0xFFFF - (int)(best & 0xFFFF), r = p / N, c = p - r * N;
+  return (r >> 1) * W + (c >> 1);
+}
+
+// Distance to the goal cell of every cell, in squares, into L.A: mz_tree_dist in cell space
+// (parents are the neighbours across an open passage at depth - 2); a cell-space BFS when the
+// tree walk fails (never for these generators) or MZ_TREE_DIST is 0.
+__device__ void mz_cs_dist(const MzCellLds& L, int s, int goal) {
+  const int lane = threadIdx.x, Q = L.Q, W = L.W;
+  bool ok = MZ_TREE_DIST;
+  if (ok) {
+    bool bad = false;
+    for (int q = lane; q < Q; q += 64) {
+      int a = q;
+      if (q != s) {
+        const int want = (int)L.dep[q] - 2;
+        a = 0xFFFF;
+        for (int k = 0; k < 4; ++k)
+          if (cs_open_dir(L, q, k)) {
+            const int n = cs_nb(q, k, W);
+            if ((int)L.dep[n] == want) a = n;
+          }
+        bad |= a == 0xFFFF;
+      }
+      L.A[q] = (uint16_t)a;
+    }
+    for (int i = lane; i < (Q + 31) / 32; i += 64) L.b1[i] = 0u;
+    ok = !__any(bad);
+    __syncthreads();
+  }
+  if (ok) {
+    if (lane == 0) {  // mark the goal's root path
+      int x = goal, n = 0;
+      for (; n <= Q; ++n) {
+        cs_set(L.b1, x);
+        if (x == s) break;
+        x = L.A[x];
+      }
+      L.sh[3] = n > Q;
+    }
+    __syncthreads();
+    ok = !L.sh[3];
+  }
+  if (ok) {
+    bool conv = false;
+    for (int it = 0; it < 32 && !conv; ++it) {
+      bool ch = false;
+      for (int q = lane; q < Q; q += 64) {
+        const int a = L.A[q];
+        if (cs_bit(L.b1, a)) continue;
+        L.A[q] = L.A[a];
+        ch = true;
+      }
+      conv = !__any(ch);
+      __syncthreads();
+    }
+    ok = conv;
+  }
+  if (ok) {
+    const int dg = L.dep[goal];
+    for (int q = lane; q < Q; q += 64) {
+      const int a = cs_bit(L.b1, q) ? q : L.A[q];
+      L.A[q] = (uint16_t)((int)L.dep[q] + dg - 2 * (int)L.dep[a]);
+    }
+    __syncthreads();
+    return;
+  }
+  // level-synchronous BFS over the cells from the goal (distances in squares)
+  for (int q = lane; q < Q; q += 64) L.A[q] = 0xFFFF;
+  for (int i = lane; i < (Q + 31) / 32; i += 64) L.b1[i] = 0u;
+  __syncthreads();
+  if (lane == 0) {
+    L.A[goal] = 0;
+    L.list[0] = (uint16_t)goal;
+    cs_set(L.b1, goal);
+    L.sh[0] = 1;
+  }
+  __syncthreads();
+  int head = 0, tail = 1;
+  while (head < tail) {
+    for (int base = head; base < tail; base += 64) {
+      const int i = base + lane;
+      if (i < tail) {
+        const int v = L.list[i], dv = L.A[v];
+        for (int k = 0; k < 4; ++k) {
+          if (!cs_open_dir(L, v, k)) continue;
+          const int n = cs_nb(v, k, W);
+          const uint32_t bit = 1u << (n & 31);
+          if (atomicOr(&L.b1[n >> 5], bit) & bit) continue;
+          L.A[n] = (uint16_t)(dv + 2);
+          L.list[atomicAdd(&L.sh[0], 1)] = (uint16_t)n;
+        }
+      }
+    }
+    __syncthreads();
+    head = tail;
+    tail = L.sh[0];
+    __syncthreads();
+  }
+}
+
+// Generation + tables of a Philox euclidean maze in cell space (lds >= mz_cell_lds_bytes(P)).
+__device__ void mz_build_cells(const MzDev& d, int e, int algo, uint64_t seed, int N, uint8_t* lds) {
+  const int lane = threadIdx.x;
+  const MzCellLds L = mz_cell_lds(lds, d.P, N);
+  const int W = L.W, Q = L.Q;
+  for (int q = lane; q < Q; q += 64) L.pas[q] = 0;
+  for (int i = lane; i < (Q + 31) / 32; i += 64) { L.b0[i] = 0u; L.b1[i] = 0u; }
+  __syncthreads();
+  MzRng rng{seed, 0ull, {0u, 0u, 0u, 0u}};
+  if (lane == 0) {
+    // start = (randrange(1, G-1, 2), randrange(1, G-1, 2)) (maze_generation.py:21)
+    const int a = (int)rng.below((uint32_t)W), b = (int)rng.below((uint32_t)W);
+    L.sh[2] = a * W + b;
+    if (algo == MZ_ALGO_RPRIM_DEV) mz_cs_rprim(L, a * W + b, rng);
+    else if (algo == MZ_ALGO_DFS_DEV) mz_cs_dfs(L, a * W + b, rng);
+  }
+  __syncthreads();
+  const int s = L.sh[2];
+  if (algo != MZ_ALGO_RPRIM_DEV && algo != MZ_ALGO_DFS_DEV) mz_cs_primkill(L, s, rng);
+  __syncthreads();
+  int goal = mz_cs_goal(L, N, s);
+  if (goal < 0) goal = s;  // unreachable for W >= 2 (a spanning tree has >= 2 leaves)
+  mz_cs_dist(L, s, goal);
+  const int sr = 2 * (s / W) + 1, sc = 2 * (s % W) + 1;
+  const int gr = 2 * (goal / W) + 1, gc = 2 * (goal % W) + 1;
+  auto open = [&](int r, int c) -> bool {
+    const bool ro = r & 1, co = c & 1;
+    if (ro && co) return true;  // every cell is in the tree
+    if (!ro && !co) return false;
+    if (ro) return c > 0 && c < N - 1 && (L.pas[(r >> 1) * W + ((c - 1) >> 1)] & 1);
+    return r > 0 && r < N - 1 && (L.pas[((r - 1) >> 1) * W + (c >> 1)] & 2);
+  };
+  auto dist = [&](int r, int c) -> int {  // open squares: a passage is one step from its nearer cell
+    if ((r & 1) && (c & 1)) return L.A[(r >> 1) * W + (c >> 1)];
+    const int q = (r & 1) ? (r >> 1) * W + ((c - 1) >> 1) : ((r - 1) >> 1) * W + (c >> 1);
+    const int q2 = (r & 1) ? q + 1 : q + W;
+    return min((int)L.A[q], (int)L.A[q2]) + 1;
+  };
+  mz_build_write(d, e, N, false, sr, sc, gr, gc, open, dist);
 }
 
 #include "mz_pygen.inc.h"
@@ -454,6 +888,10 @@ __device__ void mz_build_one(const MzDev& d, int e, bool tor, bool generate, int
                              uint64_t seed, int N, const uint8_t* grid_src, int isr, int isc,
                              int igr, int igc, uint8_t* lds, int pymode = MZ_PY_PHILOX,
                              uint32_t* py_state = nullptr, int* py_err = nullptr) {
+  if (MZ_CELL_BUILD && generate && pymode == MZ_PY_PHILOX && !tor) {
+    mz_build_cells(d, e, algo, seed, N, lds);
+    return;
+  }
   const int lane = threadIdx.x;
   const MzBuildLds L = mz_build_lds(lds, d.P);
   int sr, sc, gr, gc;
@@ -537,44 +975,6 @@ __device__ void mz_build_one(const MzDev& d, int e, bool tor, bool generate, int
   // a Philox-generated euclidean maze, else a BFS (toroidal: the crop's wrap adds cycles;
   // imported and CPython-exact mazes carry no carve depths)
   if (!tree || !mz_tree_dist(L, N, sr * N + sc, gr * N + gc)) mz_wave_bfs(L, N, tor, gr * N + gc);
-  const size_t es = (size_t)e;
-  const int P = d.P;
-  for (int p = lane; p < P * P; p += 64) {
-    const int r = p / P, c = p - r * P;
-    const bool open = r < N && c < N && L.g[r * N + c] != 0;
-    d.cells[es * P * P + p] = open ? mz_cell_word(L, N, tor, r, c, gr, gc) : 0u;
-  }
-  // open / visited plane strips (mz_common.h); visited = {start} (reset)
-  for (int k = lane; k < d.NS * P; k += 64) {
-    const int st = k / P, R = k - st * P;
-    uint32_t o = 0u, v = 0u;
-    if (R < N) {
-      for (int j = 0; j < 32; ++j) {
-        int c = MZ_STRIP_STRIDE * st + j;
-        if (tor) c = mz_wrap(c, N);
-        else if (c >= N) break;
-        if (L.g[R * N + c] != 0) o |= 1u << j;
-      }
-      if (R == sr) v = mz_strip_colmask(st, sc, N, tor);
-    }
-    *mz_strip_row(d, es, st, R) = make_uint2(o, v);
-  }
-  if (lane == 0) {
-    // set_max_steps: ceil((((H-1)*(W-1)) - 1) * (len / CE)), CE = (H-1)*((W-1)//2) - 1
-    const int len = (int)L.dist[sr * N + sc] + 1;
-    const int ce = (N - 1) * ((N - 1) / 2) - 1;
-    const double Lf = __ddiv_rn((double)len, (double)ce);
-    const double prod = __dmul_rn((double)((N - 1) * (N - 1) - 1), Lf);
-    int maxs = (int)ceil(prod);
-    if (maxs > 65535) maxs = 65535;
-    d.meta0[e] = (uint32_t)N | ((uint32_t)N << 8) | ((uint32_t)sr << 16) | ((uint32_t)sc << 24);
-    d.meta1[e] = (uint32_t)gr | ((uint32_t)gc << 8) | ((uint32_t)maxs << 16);
-    d.posw[e] = (uint32_t)sr | ((uint32_t)sc << 8);
-    d.stw[e] = 0u;
-    d.last_term[e] = 0;
-  }
-  __syncthreads();
-  // curw = cells word at start, from LDS (no read-back of global stores inside the launch)
-  if (lane == 0) d.curw[e] = mz_cell_word(L, N, tor, sr, sc, gr, gc);
-  __syncthreads();
+  mz_build_write(d, e, N, tor, sr, sc, gr, gc, [&](int y, int x) { return L.g[y * N + x] != 0; },
+                 [&](int y, int x) { return (int)L.dist[y * N + x]; });
 }

@@ -899,7 +899,17 @@ hipError_t mz_lds_attr(const void* fn, size_t bytes) {
   return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
-int mz_grid_for(int n) { return n < 4096 ? n : 4096; }
+// Build launches: the LDS one maze build needs — the cell-space layout for Philox euclidean
+// mazes (mz_build_cells), else the square grid (+ the CPython generator's tables) — and a
+// persistent grid of as many workgroups as can be resident at once (256 CUs x LDS share).
+size_t mz_build_lds_launch(int P, bool tor, bool generate, int pymode) {
+  if (MZ_CELL_BUILD && generate && pymode == MZ_PY_PHILOX && !tor) return mz_cell_lds_bytes(P);
+  return mz_build_lds_bytes_mode(P, generate ? pymode : 0);
+}
+int mz_build_grid(int n, size_t lds) {
+  const int per_cu = (int)std::min<size_t>(32, std::max<size_t>(1, (160 * 1024) / std::max<size_t>(lds, 1)));
+  return std::max(1, std::min(n, std::max(4096, 256 * per_cu)));
+}
 
 }  // namespace
 
@@ -912,10 +922,10 @@ hipError_t mz_launch_build(const MzDev& d, const int32_t* env_ids, int32_t n, bo
                            const uint8_t* grids, const int32_t* start_goal, int pymode,
                            uint32_t* py_state, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  const size_t lds = mz_build_lds_bytes_mode(d.P, generate ? pymode : 0);
+  const size_t lds = mz_build_lds_launch(d.P, d.toroidal, generate, pymode);
   hipError_t ae = mz_lds_attr(reinterpret_cast<const void*>(k_build), lds);
   if (ae != hipSuccess) return ae;
-  hipLaunchKernelGGL(k_build, dim3(mz_grid_for(n)), dim3(WAVE), lds, s, d, env_ids, n,
+  hipLaunchKernelGGL(k_build, dim3(mz_build_grid(n, lds)), dim3(WAVE), lds, s, d, env_ids, n,
                      (int)generate, algo_list, algo_all, dim, seed, grids, start_goal, pymode,
                      py_state);
   return hipGetLastError();
@@ -924,10 +934,11 @@ hipError_t mz_launch_build(const MzDev& d, const int32_t* env_ids, int32_t n, bo
 hipError_t mz_launch_regen(const MzDev& d, const int32_t* idx, const int32_t* count,
                            int32_t n_static, uint64_t seed, uint32_t epoch, hipStream_t s) {
   if (n_static <= 0) return hipSuccess;
-  hipError_t ae = mz_lds_attr(reinterpret_cast<const void*>(k_regen_list), mz_build_lds_bytes(d.P));
+  const size_t lds = mz_build_lds_launch(d.P, d.toroidal, true, MZ_PY_PHILOX);
+  hipError_t ae = mz_lds_attr(reinterpret_cast<const void*>(k_regen_list), lds);
   if (ae != hipSuccess) return ae;
-  hipLaunchKernelGGL(k_regen_list, dim3(mz_grid_for(n_static)), dim3(WAVE),
-                     mz_build_lds_bytes(d.P), s, d, idx, count, n_static, seed, epoch);
+  hipLaunchKernelGGL(k_regen_list, dim3(mz_build_grid(n_static, lds)), dim3(WAVE), lds, s, d, idx,
+                     count, n_static, seed, epoch);
   return hipGetLastError();
 }
 
@@ -998,7 +1009,7 @@ hipError_t mz_launch_reset_done(const MzDev& d, int regen, uint64_t seed, uint32
 #define MZ_RD(T, E)                                                                           \
   do {                                                                                        \
     if (regen) {                                                                              \
-      lds = mz_build_lds_bytes(d.P);                                                          \
+      lds = mz_build_lds_launch(d.P, d.toroidal, true, MZ_PY_PHILOX);                         \
       ae = mz_lds_attr(reinterpret_cast<const void*>(k_reset_done<T, E>), lds);              \
       if (ae != hipSuccess) return ae;                                                        \
     }                                                                                         \
@@ -1013,10 +1024,10 @@ hipError_t mz_launch_reset_done(const MzDev& d, int regen, uint64_t seed, uint32
 
 hipError_t mz_launch_bank_fill(const MzDev& bd, const int* head, int K, int algo, int dim,
                                uint64_t seed, uint32_t epoch, hipStream_t s) {
-  const size_t lds = mz_build_lds_bytes(bd.P);
+  const size_t lds = mz_build_lds_launch(bd.P, bd.toroidal, true, MZ_PY_PHILOX);
   hipError_t ae = mz_lds_attr(reinterpret_cast<const void*>(k_bank_fill), lds);
   if (ae != hipSuccess) return ae;
-  hipLaunchKernelGGL(k_bank_fill, dim3(mz_grid_for(K)), dim3(WAVE), lds, s, bd, head, K, algo, dim,
+  hipLaunchKernelGGL(k_bank_fill, dim3(mz_build_grid(K, lds)), dim3(WAVE), lds, s, bd, head, K, algo, dim,
                      seed, epoch);
   return hipGetLastError();
 }
