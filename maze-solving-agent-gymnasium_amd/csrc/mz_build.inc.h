@@ -485,6 +485,11 @@ __device__ void mz_build_write(const MzDev& d, int e, int N, bool tor, int sr, i
 #ifndef MZ_CELL_BUILD
 #define MZ_CELL_BUILD 1
 #endif
+// Timing probes of mz_build_cells (wrong tables — never in the product build): 1 no cell words /
+// planes, 2 no distance field, 4 no goal scan
+#ifndef MZ_GPROBE
+#define MZ_GPROBE 0
+#endif
 
 struct MzCellLds {
   uint8_t* pas;    // [Q] bit 0: passage to the right neighbour, bit 1: to the one below
@@ -833,9 +838,9 @@ __device__ void mz_build_cells(const MzDev& d, int e, int algo, uint64_t seed, i
   const int s = L.sh[2];
   if (algo != MZ_ALGO_RPRIM_DEV && algo != MZ_ALGO_DFS_DEV) mz_cs_primkill(L, s, rng);
   __syncthreads();
-  int goal = mz_cs_goal(L, N, s);
+  int goal = (MZ_GPROBE & 4) ? s : mz_cs_goal(L, N, s);
   if (goal < 0) goal = s;  // unreachable for W >= 2 (a spanning tree has >= 2 leaves)
-  mz_cs_dist(L, s, goal);
+  if (!(MZ_GPROBE & 2)) mz_cs_dist(L, s, goal);
   const int sr = 2 * (s / W) + 1, sc = 2 * (s % W) + 1;
   const int gr = 2 * (goal / W) + 1, gc = 2 * (goal % W) + 1;
   auto open = [&](int r, int c) -> bool {
@@ -851,6 +856,10 @@ __device__ void mz_build_cells(const MzDev& d, int e, int algo, uint64_t seed, i
     const int q2 = (r & 1) ? q + 1 : q + W;
     return min((int)L.A[q], (int)L.A[q2]) + 1;
   };
+  if (MZ_GPROBE & 1) {  // probe: only the meta words (no cell words / planes)
+    if (lane == 0) { d.meta0[e] = (uint32_t)N | ((uint32_t)N << 8) | ((uint32_t)sr << 16) | ((uint32_t)sc << 24); d.meta1[e] = (uint32_t)gr | ((uint32_t)gc << 8); }
+    return;
+  }
   mz_build_write(d, e, N, false, sr, sc, gr, gc, open, dist);
 }
 

@@ -899,6 +899,9 @@ hipError_t mz_lds_attr(const void* fn, size_t bytes) {
   return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
+#ifndef MZ_BANK_WGS
+#define MZ_BANK_WGS 0
+#endif
 // Build launches: the LDS one maze build needs — the cell-space layout for Philox euclidean
 // mazes (mz_build_cells), else the square grid (+ the CPython generator's tables) — and a
 // persistent grid of as many workgroups as can be resident at once (256 CUs x LDS share).
@@ -1027,7 +1030,10 @@ hipError_t mz_launch_bank_fill(const MzDev& bd, const int* head, int K, int algo
   const size_t lds = mz_build_lds_launch(bd.P, bd.toroidal, true, MZ_PY_PHILOX);
   hipError_t ae = mz_lds_attr(reinterpret_cast<const void*>(k_bank_fill), lds);
   if (ae != hipSuccess) return ae;
-  hipLaunchKernelGGL(k_bank_fill, dim3(mz_build_grid(K, lds)), dim3(WAVE), lds, s, bd, head, K, algo, dim,
+  // a refill runs beside the trainer's acting and update kernels: MZ_BANK_WGS caps its resident
+  // builds (0 = as many as fit) so that it leaves CUs / LDS to them
+  const int grid = MZ_BANK_WGS > 0 ? std::min(K, MZ_BANK_WGS) : mz_build_grid(K, lds);
+  hipLaunchKernelGGL(k_bank_fill, dim3(std::max(grid, 1)), dim3(WAVE), lds, s, bd, head, K, algo, dim,
                      seed, epoch);
   return hipGetLastError();
 }
