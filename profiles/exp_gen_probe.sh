@@ -19,3 +19,10 @@ for v in default bank1024 bank512 bank2048 default bank1024 bank512; do
   MZ_LIB_OVERRIDE=$lib timeout -k 10 300 python3 -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --eval-mazes 200 --legs bits > $O/bench_$v.json
   python3 -c "import json; d=json.load(open('$O/bench_$v.json')); w=d['win_rate']; print(json.dumps({'lib': '$v', 'train_env_steps_per_s': w['train_env_steps_per_s'], 'greedy': w['greedy']}))" >> $O/train.jsonl
 done
+# (3) the same caps in config 5 (PPO, 4,096 toroidal 17..79: square-grid builds, 35 KB each)
+export PYTHONPATH="$GRAFT_REPO_ROOT/maze-solving-agent-gymnasium_amd:$PYTHONPATH"
+for v in default bank512 bank1024 default bank512 bank1024; do
+  lib=$D; [ $v = default ] || lib=$B/gen_$v.so
+  MZ_LIB_OVERRIDE=$lib timeout -k 10 300 python3 -u -m mazerl.train_ppo --envs 4096 --steps 600 > $O/cfg5_$v.jsonl 2> $O/cfg5_$v.err
+  tail -1 $O/cfg5_$v.jsonl | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'lib': '$v', 'train_env_steps_per_s': d['train_env_steps_per_s'], 'win_rate_greedy': d['win_rate_greedy']}))" >> $O/cfg5.jsonl
+done
