@@ -818,10 +818,35 @@ __device__ void mz_cs_dist(const MzCellLds& L, int s, int goal) {
   }
 }
 
-// Generation + tables of a Philox euclidean maze in cell space (lds >= mz_cell_lds_bytes(P)).
-__device__ void mz_build_cells(const MzDev& d, int e, int algo, uint64_t seed, int N, uint8_t* lds) {
+// Toroidal mazes (gen_maze_no_border, maze_generation.py:37-56): generated in cell space on the
+// (N + 2)^2 bordered grid, the goal picked there, then cropped to N x N — where the wrap joins
+// the first and last rows / columns, so the maze has cycles and its distance field is a BFS. That
+// BFS runs bit-parallel over row masks (one 128-bit row of open squares per lane, a level = a
+// shift / or / and-not of the frontier rows) in the region the generator's lists used, after the
+// passages: 20 KB of LDS at 79 x 79 instead of the square grid's 34 KB.
+typedef unsigned __int128 mz_u128;
+
+__device__ inline mz_u128 mz_row_rotl(mz_u128 v, int N, mz_u128 mask) {  // column x -> x + 1 mod N
+  return ((v << 1) & mask) | ((v >> (N - 1)) & 1u);
+}
+__device__ inline mz_u128 mz_row_rotr(mz_u128 v, int N) {  // column x -> x - 1 mod N
+  return (v >> 1) | ((v & 1u) << (N - 1));
+}
+
+__host__ __device__ inline size_t mz_torus_lds_bytes(int P) {
+  const size_t Wp = (size_t)(P + 2) / 2, Qp = Wp * Wp;
+  const size_t bfs = 64 + mz_align16(Qp) + mz_align16(2 * (size_t)P * P) + 4 * 16 * (size_t)P;
+  const size_t gen = mz_cell_lds_bytes(P + 2);
+  return gen > bfs ? gen : bfs;
+}
+
+// Generation + tables of a Philox maze in cell space (lds >= mz_cell_lds_bytes(P), toroidal:
+// mz_torus_lds_bytes(P)).
+__device__ void mz_build_cells(const MzDev& d, int e, int algo, uint64_t seed, int N, bool tor,
+                               uint8_t* lds) {
   const int lane = threadIdx.x;
-  const MzCellLds L = mz_cell_lds(lds, d.P, N);
+  const int G = tor ? N + 2 : N;
+  const MzCellLds L = mz_cell_lds(lds, tor ? d.P + 2 : d.P, G);
   const int W = L.W, Q = L.Q;
   for (int q = lane; q < Q; q += 64) L.pas[q] = 0;
   for (int i = lane; i < (Q + 31) / 32; i += 64) { L.b0[i] = 0u; L.b1[i] = 0u; }
@@ -838,29 +863,84 @@ __device__ void mz_build_cells(const MzDev& d, int e, int algo, uint64_t seed, i
   const int s = L.sh[2];
   if (algo != MZ_ALGO_RPRIM_DEV && algo != MZ_ALGO_DFS_DEV) mz_cs_primkill(L, s, rng);
   __syncthreads();
-  int goal = (MZ_GPROBE & 4) ? s : mz_cs_goal(L, N, s);
+  int goal = (MZ_GPROBE & 4) ? s : mz_cs_goal(L, G, s);
   if (goal < 0) goal = s;  // unreachable for W >= 2 (a spanning tree has >= 2 leaves)
-  if (!(MZ_GPROBE & 2)) mz_cs_dist(L, s, goal);
-  const int sr = 2 * (s / W) + 1, sc = 2 * (s % W) + 1;
-  const int gr = 2 * (goal / W) + 1, gc = 2 * (goal % W) + 1;
-  auto open = [&](int r, int c) -> bool {
+  // open squares of the G x G generation grid
+  auto open_g = [&](int r, int c) -> bool {
     const bool ro = r & 1, co = c & 1;
     if (ro && co) return true;  // every cell is in the tree
     if (!ro && !co) return false;
-    if (ro) return c > 0 && c < N - 1 && (L.pas[(r >> 1) * W + ((c - 1) >> 1)] & 1);
-    return r > 0 && r < N - 1 && (L.pas[((r - 1) >> 1) * W + (c >> 1)] & 2);
+    if (ro) return c > 0 && c < G - 1 && (L.pas[(r >> 1) * W + ((c - 1) >> 1)] & 1);
+    return r > 0 && r < G - 1 && (L.pas[((r - 1) >> 1) * W + (c >> 1)] & 2);
   };
-  auto dist = [&](int r, int c) -> int {  // open squares: a passage is one step from its nearer cell
-    if ((r & 1) && (c & 1)) return L.A[(r >> 1) * W + (c >> 1)];
-    const int q = (r & 1) ? (r >> 1) * W + ((c - 1) >> 1) : ((r - 1) >> 1) * W + (c >> 1);
-    const int q2 = (r & 1) ? q + 1 : q + W;
-    return min((int)L.A[q], (int)L.A[q2]) + 1;
-  };
-  if (MZ_GPROBE & 1) {  // probe: only the meta words (no cell words / planes)
-    if (lane == 0) { d.meta0[e] = (uint32_t)N | ((uint32_t)N << 8) | ((uint32_t)sr << 16) | ((uint32_t)sc << 24); d.meta1[e] = (uint32_t)gr | ((uint32_t)gc << 8); }
+  const int off = tor ? 1 : 0;  // crop the border (maze_generation.py:53-55)
+  const int sr = 2 * (s / W) + 1 - off, sc = 2 * (s % W) + 1 - off;
+  const int gr = 2 * (goal / W) + 1 - off, gc = 2 * (goal % W) + 1 - off;
+  if (!tor) {
+    if (!(MZ_GPROBE & 2)) mz_cs_dist(L, s, goal);
+    auto dist = [&](int r, int c) -> int {  // open squares: a passage is one step from its nearer cell
+      if ((r & 1) && (c & 1)) return L.A[(r >> 1) * W + (c >> 1)];
+      const int q = (r & 1) ? (r >> 1) * W + ((c - 1) >> 1) : ((r - 1) >> 1) * W + (c >> 1);
+      const int q2 = (r & 1) ? q + 1 : q + W;
+      return min((int)L.A[q], (int)L.A[q2]) + 1;
+    };
+    if (MZ_GPROBE & 1) {  // probe: only the meta words (no cell words / planes)
+      if (lane == 0) { d.meta0[e] = (uint32_t)N | ((uint32_t)N << 8) | ((uint32_t)sr << 16) | ((uint32_t)sc << 24); d.meta1[e] = (uint32_t)gr | ((uint32_t)gc << 8); }
+      return;
+    }
+    mz_build_write(d, e, N, false, sr, sc, gr, gc, open_g, dist);
     return;
   }
-  mz_build_write(d, e, N, false, sr, sc, gr, gc, open, dist);
+  // torus: BFS from the goal over row masks, in the region after the passages
+  const int P = d.P;
+  uint8_t* rb = reinterpret_cast<uint8_t*>(L.b0);  // first byte after pas (16-B aligned)
+  uint16_t* dist = reinterpret_cast<uint16_t*>(rb);
+  mz_u128* O = reinterpret_cast<mz_u128*>(rb + mz_align16(2 * (size_t)P * P));
+  mz_u128* V = O + P;
+  mz_u128* F = V + P;  // two frontier buffers: F[0..P), F[P..2P)
+  auto open_t = [&](int y, int x) -> bool { return open_g(y + 1, x + 1); };
+  const mz_u128 mask = (N == 128) ? ~(mz_u128)0 : (((mz_u128)1 << N) - 1);
+  __syncthreads();  // the generator's lists are dead: the BFS region may overwrite them
+  for (int y = lane; y < N; y += 64) {
+    mz_u128 o = 0;
+    for (int x = 0; x < N; ++x)
+      if (open_t(y, x)) o |= (mz_u128)1 << x;
+    const mz_u128 g = y == gr ? (mz_u128)1 << gc : 0;
+    O[y] = o;
+    V[y] = g;
+    F[y] = g;
+  }
+  for (int i = lane; i < N * N; i += 64) dist[i] = 0xFFFF;
+  __syncthreads();
+  if (lane == 0) dist[gr * N + gc] = 0;
+  int cur = 0;
+  for (int level = 1;; ++level) {
+    const mz_u128* Fc = F + cur * P;
+    mz_u128* Fn = F + (cur ^ 1) * P;
+    bool any = false;
+    for (int y = lane; y < N; y += 64) {
+      const mz_u128 f = Fc[y];
+      const mz_u128 reach = f | mz_row_rotl(f, N, mask) | mz_row_rotr(f, N) | Fc[y == 0 ? N - 1 : y - 1] |
+                            Fc[y == N - 1 ? 0 : y + 1];
+      mz_u128 nw = reach & O[y] & ~V[y];
+      Fn[y] = nw;
+      if (nw) {
+        any = true;
+        V[y] |= nw;
+        while (nw) {  // the new squares of row y are at distance `level`
+          const uint64_t lo = (uint64_t)nw, hi = (uint64_t)(nw >> 64);
+          const int x = lo ? __ffsll((long long)lo) - 1 : 64 + __ffsll((long long)hi) - 1;
+          dist[y * N + x] = (uint16_t)level;
+          nw &= nw - 1;
+        }
+      }
+    }
+    __syncthreads();
+    if (!__any(any)) break;
+    cur ^= 1;
+  }
+  mz_build_write(d, e, N, true, sr, sc, gr, gc, open_t,
+                 [&](int y, int x) { return (int)dist[y * N + x]; });
 }
 
 #include "mz_pygen.inc.h"
@@ -897,8 +977,8 @@ __device__ void mz_build_one(const MzDev& d, int e, bool tor, bool generate, int
                              uint64_t seed, int N, const uint8_t* grid_src, int isr, int isc,
                              int igr, int igc, uint8_t* lds, int pymode = MZ_PY_PHILOX,
                              uint32_t* py_state = nullptr, int* py_err = nullptr) {
-  if (MZ_CELL_BUILD && generate && pymode == MZ_PY_PHILOX && !tor) {
-    mz_build_cells(d, e, algo, seed, N, lds);
+  if (MZ_CELL_BUILD && generate && pymode == MZ_PY_PHILOX) {
+    mz_build_cells(d, e, algo, seed, N, tor, lds);
     return;
   }
   const int lane = threadIdx.x;

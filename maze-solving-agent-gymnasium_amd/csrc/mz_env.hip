@@ -906,7 +906,8 @@ hipError_t mz_lds_attr(const void* fn, size_t bytes) {
 // mazes (mz_build_cells), else the square grid (+ the CPython generator's tables) — and a
 // persistent grid of as many workgroups as can be resident at once (256 CUs x LDS share).
 size_t mz_build_lds_launch(int P, bool tor, bool generate, int pymode) {
-  if (MZ_CELL_BUILD && generate && pymode == MZ_PY_PHILOX && !tor) return mz_cell_lds_bytes(P);
+  if (MZ_CELL_BUILD && generate && pymode == MZ_PY_PHILOX)
+    return tor ? mz_torus_lds_bytes(P) : mz_cell_lds_bytes(P);
   return mz_build_lds_bytes_mode(P, generate ? pymode : 0);
 }
 int mz_build_grid(int n, size_t lds) {
