@@ -479,9 +479,10 @@ __device__ void mz_build_write(const MzDev& d, int e, int N, bool tor, int sr, i
 // The generators below carve the same spanning tree as mz_gen_* (the same Philox draws over the
 // same candidate lists in the same order, the same swap-remove frontier), but keep per cell only
 // the passages to its right and lower neighbours, two bit sets, the frontier / stack list, the
-// carve depth and the distance field: ~7.3 B per cell (11.7 KB at 81 x 81) where the square grid
-// needs ~5.1 B per square (35 KB), so 13 builds share a CU instead of 4 (each build is a serial
-// lane-0 chain of LDS round trips: throughput is the number of builds in flight).
+// carve depth and then the distance field in place of the list: ~5.3 B per cell (8.5 KB at 81 x 81)
+// where the square grid needs ~5.1 B per square (35 KB), so 18 builds share a CU instead of 4
+// (each build is a serial lane-0 chain of LDS round trips: throughput is the number of builds in
+// flight).
 #ifndef MZ_CELL_BUILD
 #define MZ_CELL_BUILD 1
 #endif
@@ -495,16 +496,21 @@ struct MzCellLds {
   uint8_t* pas;    // [Q] bit 0: passage to the right neighbour, bit 1: to the one below
   uint32_t* b0;    // [QW] in maze (r-prim, dfs) / marked (prim&kill)
   uint32_t* b1;    // [QW] in frontier (r-prim) / restart candidate (prim&kill), then goal path
-  uint16_t* list;  // [Q] frontier (r-prim) / stack (dfs) / BFS queue
-  uint16_t* dep;   // [Q] carve depth: distance from the start in squares
-  uint16_t* A;     // [Q] parent, first goal-path ancestor, then the distance to the goal
+  uint16_t* list;  // [Q] frontier (r-prim) / stack (dfs)
+  uint16_t* dep;   // [Q] carve depth: distance from the start in squares (BFS fallback: queue)
+  uint16_t* A;     // [Q] = list (dead after the carve): parent, first goal-path ancestor, then
+                   //     the distance to the goal
   int* sh;
   int W, Q;
 };
 
+// MZ_CELL_ALIAS 0: the distance array separate from the list (A/B builds)
+#ifndef MZ_CELL_ALIAS
+#define MZ_CELL_ALIAS 1
+#endif
 __host__ __device__ inline size_t mz_cell_lds_bytes(int P) {
   const size_t W = (size_t)P / 2, Q = W * W, QW = (Q + 31) / 32;
-  return 64 + mz_align16(Q) + 2 * mz_align16(4 * QW) + 3 * mz_align16(2 * Q);
+  return 64 + mz_align16(Q) + 2 * mz_align16(4 * QW) + (MZ_CELL_ALIAS ? 2 : 3) * mz_align16(2 * Q);
 }
 
 __device__ inline MzCellLds mz_cell_lds(uint8_t* base, int P, int N) {
@@ -517,7 +523,7 @@ __device__ inline MzCellLds mz_cell_lds(uint8_t* base, int P, int N) {
   L.b1 = reinterpret_cast<uint32_t*>(base + off); off += mz_align16(4 * QW);
   L.list = reinterpret_cast<uint16_t*>(base + off); off += mz_align16(2 * Qp);
   L.dep = reinterpret_cast<uint16_t*>(base + off); off += mz_align16(2 * Qp);
-  L.A = reinterpret_cast<uint16_t*>(base + off);
+  L.A = MZ_CELL_ALIAS ? L.list : reinterpret_cast<uint16_t*>(base + off);
   L.W = (N - 1) / 2;
   L.Q = L.W * L.W;
   return L;
@@ -784,13 +790,15 @@ __device__ void mz_cs_dist(const MzCellLds& L, int s, int goal) {
     __syncthreads();
     return;
   }
-  // level-synchronous BFS over the cells from the goal (distances in squares)
+  // level-synchronous BFS over the cells from the goal (distances in squares; the carve depths
+  // are not needed any more: their array is the queue)
+  uint16_t* queue = L.dep;
   for (int q = lane; q < Q; q += 64) L.A[q] = 0xFFFF;
   for (int i = lane; i < (Q + 31) / 32; i += 64) L.b1[i] = 0u;
   __syncthreads();
   if (lane == 0) {
     L.A[goal] = 0;
-    L.list[0] = (uint16_t)goal;
+    queue[0] = (uint16_t)goal;
     cs_set(L.b1, goal);
     L.sh[0] = 1;
   }
@@ -800,14 +808,14 @@ __device__ void mz_cs_dist(const MzCellLds& L, int s, int goal) {
     for (int base = head; base < tail; base += 64) {
       const int i = base + lane;
       if (i < tail) {
-        const int v = L.list[i], dv = L.A[v];
+        const int v = queue[i], dv = L.A[v];
         for (int k = 0; k < 4; ++k) {
           if (!cs_open_dir(L, v, k)) continue;
           const int n = cs_nb(v, k, W);
           const uint32_t bit = 1u << (n & 31);
           if (atomicOr(&L.b1[n >> 5], bit) & bit) continue;
           L.A[n] = (uint16_t)(dv + 2);
-          L.list[atomicAdd(&L.sh[0], 1)] = (uint16_t)n;
+          queue[atomicAdd(&L.sh[0], 1)] = (uint16_t)n;
         }
       }
     }
