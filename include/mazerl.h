@@ -538,7 +538,7 @@ int mz_ppo_head_loss(const float* logits_dev, int32_t ldl, const float* value_de
 
 /* fc1's weight [1024][1574] (torch layout) and fc2's [512][1024] f32 -> the hi / lo bf16 images
  * mz_qact reads, in MFMA fragment order (a wave's operand for one K chunk contiguous): w1 1024 x 1600
- * elements (features in the kernel's order, zero pad), w2 512 x 1024 (16-B aligned). */
+ * elements (features in the kernel's order, zero pad), w2 512 x 1024. Every pointer 16-B aligned (MZ_EINVAL otherwise). */
 int mz_qact_prepare(const float* fc1_w_dev, const float* fc2_w_dev, uint16_t* w1_hi_dev,
                     uint16_t* w1_lo_dev, uint16_t* w2_hi_dev, uint16_t* w2_lo_dev, void* stream);
 

@@ -1078,6 +1078,9 @@ int mz_qact_prepare(const float* fc1_w_dev, const float* fc2_w_dev, uint16_t* w1
                     uint16_t* w1_lo_dev, uint16_t* w2_hi_dev, uint16_t* w2_lo_dev, void* stream) {
   if (!fc1_w_dev || !fc2_w_dev || !w1_hi_dev || !w1_lo_dev || !w2_hi_dev || !w2_lo_dev)
     return fail(MZ_EINVAL, "bad arguments");
+  for (const void* p : {(const void*)fc1_w_dev, (const void*)fc2_w_dev, (const void*)w1_hi_dev,
+                        (const void*)w1_lo_dev, (const void*)w2_hi_dev, (const void*)w2_lo_dev})
+    if (reinterpret_cast<uintptr_t>(p) & 15) return fail(MZ_EINVAL, "weights / images must be 16-B aligned");
   StreamGuard g(stream);
   MZ_HIP(mz_launch_qact_prepare(fc1_w_dev, fc2_w_dev, w1_hi_dev, w1_lo_dev, w2_hi_dev, w2_lo_dev,
                                 static_cast<hipStream_t>(stream)));

@@ -1023,7 +1023,7 @@ __device__ void mz_build_one(const MzDev& d, int e, bool tor, bool generate, int
       __syncthreads();
       sr -= 1; sc -= 1; gr -= 1; gc -= 1;
     }
-  } else if (generate) {
+  } else if (generate) {  // Philox in the square grid: the MZ_CELL_BUILD=0 A/B reference
     const int G = tor ? N + 2 : N;
     for (int i = lane; i < G * G; i += 64) L.g[i] = 0;
     __syncthreads();

@@ -902,9 +902,10 @@ hipError_t mz_lds_attr(const void* fn, size_t bytes) {
 #ifndef MZ_BANK_WGS
 #define MZ_BANK_WGS 0
 #endif
-// Build launches: the LDS one maze build needs — the cell-space layout for Philox euclidean
-// mazes (mz_build_cells), else the square grid (+ the CPython generator's tables) — and a
-// persistent grid of as many workgroups as can be resident at once (256 CUs x LDS share).
+// Build launches: the LDS one maze build needs — the cell-space layouts for Philox mazes
+// (mz_build_cells), else the square grid (+ the CPython generator's tables) — and a persistent
+// grid of 4,096 workgroups or, when more fit, as many as can be resident at once (256 CUs x the
+// LDS share, at most 32 waves per CU).
 size_t mz_build_lds_launch(int P, bool tor, bool generate, int pymode) {
   if (MZ_CELL_BUILD && generate && pymode == MZ_PY_PHILOX)
     return tor ? mz_torus_lds_bytes(P) : mz_cell_lds_bytes(P);

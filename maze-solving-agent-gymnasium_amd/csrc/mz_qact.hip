@@ -569,38 +569,61 @@ __global__ __launch_bounds__(512) void k_qact2(MzQAct q) {
 // 8 (lane / 16) + e] (kernel feature order q * 32 + c, obs6 at 1568, zero pad to 1600); the fc2 image
 // is [chunk 32][wave 8][j][lane][8]. A wave's B fragments for one chunk are then 4 KB contiguous
 // per image: one fully coalesced 1 KB load per 16-column tile instead of 16 rows x 64 B.
-__global__ void k_qact_prepare(const float* __restrict__ w1, const float* __restrict__ w2,
-                               uint16_t* __restrict__ w1h, uint16_t* __restrict__ w1l,
-                               uint16_t* __restrict__ w2h, uint16_t* __restrict__ w2l) {
-  const int64_t n1 = (int64_t)N1 * K1, n2 = (int64_t)N2 * N1;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n1 + n2;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    // element e of the fragment-ordered image: [tile][chunk][wave][j][lane][8] (see w1_frag)
-    const int64_t o = e < n1 ? e : e - n1;
-    const int el = (int)(o & 7), lane = (int)((o >> 3) & 63), j = (int)((o >> 9) & 3);
-    const int64_t rest = o >> 11;
-    float v;
-    uint16_t *ph, *pl;
-    if (e < n1) {
-      const int cq = (int)(rest % QW1), c = (int)((rest / QW1) % NCH), nt = (int)((rest / QW1) / NCH);
-      const int r = nt * NT1 + cq * 64 + 16 * j + (lane & 15);  // fc1 output
-      const int f = 32 * c + 8 * (lane >> 4) + el;                // kernel feature order
-      int src = -1;
-      if (f < CONV_OUT) src = (f & 31) * 49 + (f >> 5);
-      else if (f < CONV_OUT + 6) src = f;
-      v = src >= 0 ? w1[(size_t)r * (CONV_OUT + 6) + src] : 0.0f;
-      ph = w1h; pl = w1l;
-    } else {
-      const int wv = (int)(rest & 7), c = (int)(rest >> 3);
-      const int r = 64 * wv + 16 * j + (lane & 15);            // fc2 output
-      const int k = 32 * c + 8 * (lane >> 4) + el;
-      v = w2[(size_t)r * N1 + k];
-      ph = w2h; pl = w2l;
+// fc1: one workgroup per 16-row fragment block (output tile, wave, j): the block's 16 contiguous
+// rows of W1 (100 KB) are read coalesced into LDS, then each thread turns 8 features of one lane of
+// one chunk into a 16-B hi and a 16-B lo store. (A per-element version — W1 gathered at the conv
+// features' stride of 49 floats, 2-B stores — took 23 us per update inside training.)
+constexpr int PREP_ROWS = 16;
+constexpr int PREP_LD = CONV_OUT + 6;  // 1574: W1's row length
+__global__ __launch_bounds__(256) void k_qact_prep1(const float* __restrict__ w1,
+                                                    uint16_t* __restrict__ w1h,
+                                                    uint16_t* __restrict__ w1l) {
+  extern __shared__ float rows[];  // [PREP_ROWS][PREP_LD]
+  const int blk = blockIdx.x, r0 = blk * PREP_ROWS;
+  const float4* src = reinterpret_cast<const float4*>(w1 + (size_t)r0 * PREP_LD);
+  for (int i = threadIdx.x; i < PREP_ROWS * PREP_LD / 4; i += 256)
+    reinterpret_cast<float4*>(rows)[i] = src[i];
+  __syncthreads();
+  const int nt = r0 / NT1, cq = (r0 % NT1) / 64, j = (r0 % 64) / 16;
+  for (int p = threadIdx.x; p < NCH * 64; p += 256) {  // (chunk, lane) pairs
+    const int c = p >> 6, lane = p & 63;
+    const float* row = rows + (lane & 15) * PREP_LD;
+    uint32_t hi[4], lo[4];
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      float v[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int f = 32 * c + 8 * (lane >> 4) + e + u;  // kernel feature order
+        const int sf = f < CONV_OUT ? (f & 31) * 49 + (f >> 5) : f;
+        v[u] = f < CONV_OUT + 6 ? row[sf] : 0.0f;
+      }
+      split2(v[0], v[1], hi[e >> 1], lo[e >> 1]);
     }
-    const float h = bf16_round(v);
-    ph[o] = (uint16_t)(bf16x2(h, 0.0f) & 0xFFFFu);
-    pl[o] = (uint16_t)(bf16x2(v - h, 0.0f) & 0xFFFFu);
+    const size_t o = ((((size_t)nt * NCH + c) * QW1 + cq) * 4 + j) * 64 + lane;  // in 8-element units
+    reinterpret_cast<uint4*>(w1h)[o] = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+    reinterpret_cast<uint4*>(w1l)[o] = make_uint4(lo[0], lo[1], lo[2], lo[3]);
   }
+}
+
+// fc2: one thread per (chunk, wave, j, lane): 8 consecutive inputs of one output row (two float4
+// loads) -> a 16-B hi and a 16-B lo store
+__global__ __launch_bounds__(256) void k_qact_prep2(const float* __restrict__ w2,
+                                                    uint16_t* __restrict__ w2h,
+                                                    uint16_t* __restrict__ w2l) {
+  const int o = blockIdx.x * 256 + threadIdx.x;  // [chunk 32][wave 8][j 4][lane 64]
+  if (o >= N2 * N1 / 8) return;
+  const int lane = o & 63, j = (o >> 6) & 3, wv = (o >> 8) & 7, c = o >> 11;
+  const int r = 64 * wv + 16 * j + (lane & 15), k = 32 * c + 8 * (lane >> 4);
+  const float4* src = reinterpret_cast<const float4*>(w2 + (size_t)r * N1 + k);
+  const float4 a = src[0], b = src[1];
+  uint32_t hi[4], lo[4];
+  split2(a.x, a.y, hi[0], lo[0]);
+  split2(a.z, a.w, hi[1], lo[1]);
+  split2(b.x, b.y, hi[2], lo[2]);
+  split2(b.z, b.w, hi[3], lo[3]);
+  reinterpret_cast<uint4*>(w2h)[o] = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+  reinterpret_cast<uint4*>(w2l)[o] = make_uint4(lo[0], lo[1], lo[2], lo[3]);
 }
 
 }  // namespace
@@ -626,6 +649,12 @@ hipError_t mz_launch_qact(const MzQAct& q, int relu, hipStream_t s) {
 
 hipError_t mz_launch_qact_prepare(const float* w1, const float* w2, uint16_t* w1h, uint16_t* w1l,
                                   uint16_t* w2h, uint16_t* w2l, hipStream_t s) {
-  hipLaunchKernelGGL(k_qact_prepare, dim3(1024), dim3(256), 0, s, w1, w2, w1h, w1l, w2h, w2l);
+  constexpr size_t lds = sizeof(float) * PREP_ROWS * PREP_LD;  // 100.7 KB
+  static const hipError_t attr =
+      hipFuncSetAttribute(reinterpret_cast<const void*>(k_qact_prep1),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL(k_qact_prep1, dim3(N1 / PREP_ROWS), dim3(256), lds, s, w1, w1h, w1l);
+  hipLaunchKernelGGL(k_qact_prep2, dim3(N2 * N1 / 8 / 256), dim3(256), 0, s, w2, w2h, w2l);
   return hipGetLastError();
 }
