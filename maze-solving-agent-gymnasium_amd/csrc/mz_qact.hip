@@ -55,7 +55,13 @@ constexpr int NTL1 = N1 / NT1;     // fc1 output tiles
 constexpr int XPT = 8 / NTL1;      // XCDs per output tile
 constexpr int PR = 17;             // padded window rows per instance
 constexpr int AST = 40;            // LDS A-tile row stride in bf16 (32 + 8: conflict-free b128)
-constexpr int RT2 = 64;            // k_qact2 rows per workgroup
+// k_qact2 rows per workgroup: each wave streams its 256 KB of fc2 hi / lo fragments once per
+// workgroup, so the rows per workgroup set the L2 traffic (64 rows: 2 MB per 64 rows)
+#ifndef MZ_QACT2_ROWS
+#define MZ_QACT2_ROWS 128
+#endif
+constexpr int RT2 = MZ_QACT2_ROWS;
+constexpr int MI2 = RT2 / 16;      // k_qact2 row fragments per wave
 
 typedef __attribute__((ext_vector_type(8))) __bf16 frag_ab;
 typedef __attribute__((ext_vector_type(4))) float frag_cd;
@@ -92,24 +98,25 @@ __device__ inline float leaky(float x) { return x > 0.0f ? x : x * 0.01f; }
 
 // acc[i][j] += A_i B_j over one 32-deep K chunk, split precision: hi*hi, then hi*lo, then lo*hi
 // over all 16 tiles (product-major: consecutive MFMAs never share an accumulator)
-__device__ inline void mfma_x3(const frag_ab (&ah)[4], const frag_ab (&al)[4], const uint4 (&bh)[4],
-                               const uint4 (&bl)[4], frag_cd (&acc)[4][4]) {
+template <int I>
+__device__ inline void mfma_x3(const frag_ab (&ah)[I], const frag_ab (&al)[I], const uint4 (&bh)[4],
+                               const uint4 (&bl)[4], frag_cd (&acc)[I][4]) {
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < I; ++i)
       acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], __builtin_bit_cast(frag_ab, bh[j]),
                                                           acc[i][j], 0, 0, 0);
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < I; ++i)
       acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], __builtin_bit_cast(frag_ab, bl[j]),
                                                           acc[i][j], 0, 0, 0);
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < I; ++i)
       acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], __builtin_bit_cast(frag_ab, bh[j]),
                                                           acc[i][j], 0, 0, 0);
 }
@@ -429,20 +436,29 @@ __global__ __launch_bounds__(512) void k_qact2(MzQAct q) {
   const int nr = min(RT2, m - r0);
   const int col0 = 64 * w;  // this wave's 64 fc2 outputs
 
-  // A chunk c (32 columns of h1 for the 64 rows): thread -> (row tid / 8, 4 columns)
+  // A chunk c (32 columns of h1 for the RT2 rows): thread -> (rows tid / 8 + 64 u, 4 columns)
+  constexpr int AU = RT2 / 64;
   const int ar = tid >> 3, ak = (tid & 7) * 4;
-  auto load_a = [&](int c) -> float4 {
-    if (ar >= nr) return make_float4(0.f, 0.f, 0.f, 0.f);
-    return *reinterpret_cast<const float4*>(q.h1 + (size_t)(r0 + ar) * N1 + 32 * c + ak);
+  struct AV { float4 v[AU]; };
+  auto load_a = [&](int c) -> AV {
+    AV a;
+#pragma unroll
+    for (int u = 0; u < AU; ++u)
+      a.v[u] = ar + 64 * u >= nr ? make_float4(0.f, 0.f, 0.f, 0.f)
+                                 : *reinterpret_cast<const float4*>(q.h1 + (size_t)(r0 + ar + 64 * u) * N1 + 32 * c + ak);
+    return a;
   };
-  auto store_a = [&](int buf, float4 v) {
-    uint32_t h0, l0, h1, l1;
-    split2(v.x, v.y, h0, l0);
-    split2(v.z, v.w, h1, l1);
-    uint32_t* ph = reinterpret_cast<uint32_t*>(A[buf][0] + ar * AST + ak);
-    uint32_t* pl = reinterpret_cast<uint32_t*>(A[buf][1] + ar * AST + ak);
-    ph[0] = h0; ph[1] = h1;
-    pl[0] = l0; pl[1] = l1;
+  auto store_a = [&](int buf, const AV& a) {
+#pragma unroll
+    for (int u = 0; u < AU; ++u) {
+      uint32_t h0, l0, h1, l1;
+      split2(a.v[u].x, a.v[u].y, h0, l0);
+      split2(a.v[u].z, a.v[u].w, h1, l1);
+      uint32_t* ph = reinterpret_cast<uint32_t*>(A[buf][0] + (ar + 64 * u) * AST + ak);
+      uint32_t* pl = reinterpret_cast<uint32_t*>(A[buf][1] + (ar + 64 * u) * AST + ak);
+      ph[0] = h0; ph[1] = h1;
+      pl[0] = l0; pl[1] = l1;
+    }
   };
   uint4 bh[4], bl[4], nbh[4], nbl[4];
   // B fragments from the fragment-ordered fc2 image: [chunk][wave][j][lane][8]
@@ -459,15 +475,15 @@ __global__ __launch_bounds__(512) void k_qact2(MzQAct q) {
       dl[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs_l, off, 0, 0));
     }
   };
-  frag_cd acc[4][4];
+  frag_cd acc[MI2][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI2; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = frag_cd{0.0f, 0.0f, 0.0f, 0.0f};
   constexpr int NC2 = N1 / 32;
   store_a(0, load_a(0));
   load_b(0, bh, bl);
-  float4 na = make_float4(0.f, 0.f, 0.f, 0.f);
+  AV na = {};
   __syncthreads();
   for (int c = 0; c < NC2; ++c) {
     if (c + 1 < NC2) {
@@ -476,14 +492,17 @@ __global__ __launch_bounds__(512) void k_qact2(MzQAct q) {
     }
     const uint16_t* Ah = A[c & 1][0];
     const uint16_t* Al = A[c & 1][1];
-    frag_ab ah[4], al[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = 16 * i + c16;
-      ah[i] = __builtin_bit_cast(frag_ab, *reinterpret_cast<const uint4*>(Ah + r * AST + 8 * g4));
-      al[i] = __builtin_bit_cast(frag_ab, *reinterpret_cast<const uint4*>(Al + r * AST + 8 * g4));
+    for (int h = 0; h < MI2; h += 4) {  // four row fragments at a time (register pressure)
+      frag_ab ah[4], al[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 16 * (h + i) + c16;
+        ah[i] = __builtin_bit_cast(frag_ab, *reinterpret_cast<const uint4*>(Ah + r * AST + 8 * g4));
+        al[i] = __builtin_bit_cast(frag_ab, *reinterpret_cast<const uint4*>(Al + r * AST + 8 * g4));
+      }
+      mfma_x3<4>(ah, al, bh, bl, *reinterpret_cast<frag_cd(*)[4][4]>(&acc[h]));
     }
-    mfma_x3(ah, al, bh, bl, acc);
     if (c + 1 < NC2) {
       store_a((c + 1) & 1, na);
 #pragma unroll
@@ -495,52 +514,58 @@ __global__ __launch_bounds__(512) void k_qact2(MzQAct q) {
     __syncthreads();
   }
 
-  // h2 = act(acc + b2) in f32; fc3 partial sums over this wave's 64 columns, per row and action
-  float s[4][4][4];  // [i][reg][action]
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int a = 0; a < 4; ++a) s[i][r][a] = 0.0f;
+  // h2 = act(acc + b2) in f32; fc3 partial sums over this wave's 64 columns, per row and action,
+  // four row fragments at a time
+  float b2v[4], w3v[4][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int col = col0 + 16 * j + c16;
-    const float bb = q.b2[col];
-    float w3[4];
+    b2v[j] = q.b2[col];
 #pragma unroll
-    for (int a = 0; a < 4; ++a) w3[a] = q.w3[a * N2 + col];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float h = acc[i][j][r] + bb;
-        const float hv = RELU ? fmaxf(h, 0.0f) : leaky(h);
-#pragma unroll
-        for (int a = 0; a < 4; ++a) s[i][r][a] += hv * w3[a];
-      }
+    for (int a = 0; a < 4; ++a) w3v[j][a] = q.w3[a * N2 + col];
   }
-  // sum over the 16 lanes of a row group (columns), fixed butterfly order
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        float v = s[i][r][a];
-        v += __shfl_xor(v, 1);
-        v += __shfl_xor(v, 2);
-        v += __shfl_xor(v, 4);
-        v += __shfl_xor(v, 8);
-        s[i][r][a] = v;
-      }
-  if (c16 == 0) {
+  for (int i0 = 0; i0 < MI2; i0 += 4) {
+    float s[4][4][4];  // [i][reg][action]
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int a = 0; a < 4; ++a) part[w][16 * i + 4 * g4 + r][a] = s[i][r][a];
+        for (int a = 0; a < 4; ++a) s[i][r][a] = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float h = acc[i0 + i][j][r] + b2v[j];
+          const float hv = RELU ? fmaxf(h, 0.0f) : leaky(h);
+#pragma unroll
+          for (int a = 0; a < 4; ++a) s[i][r][a] += hv * w3v[j][a];
+        }
+    // sum over the 16 lanes of a row group (columns), fixed butterfly order
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          float v = s[i][r][a];
+          v += __shfl_xor(v, 1);
+          v += __shfl_xor(v, 2);
+          v += __shfl_xor(v, 4);
+          v += __shfl_xor(v, 8);
+          s[i][r][a] = v;
+        }
+    if (c16 == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int a = 0; a < 4; ++a) part[w][16 * (i0 + i) + 4 * g4 + r][a] = s[i][r][a];
+    }
   }
   __syncthreads();
   if (tid < nr) {
