@@ -594,25 +594,25 @@ __global__ __launch_bounds__(512) void k_qact2(MzQAct q) {
 // 8 (lane / 16) + e] (kernel feature order q * 32 + c, obs6 at 1568, zero pad to 1600); the fc2 image
 // is [chunk 32][wave 8][j][lane][8]. A wave's B fragments for one chunk are then 4 KB contiguous
 // per image: one fully coalesced 1 KB load per 16-column tile instead of 16 rows x 64 B.
-// fc1: one workgroup per 16-row fragment block (output tile, wave, j): the block's 16 contiguous
-// rows of W1 (100 KB) are read coalesced into LDS, then each thread turns 8 features of one lane of
+// fc1: one workgroup per half of a 16-row fragment block (output tile, wave, j): its 8 contiguous
+// rows of W1 (50 KB) are read coalesced into LDS, then each thread turns 8 features of one lane of
 // one chunk into a 16-B hi and a 16-B lo store. (A per-element version — W1 gathered at the conv
 // features' stride of 49 floats, 2-B stores — took 23 us per update inside training.)
-constexpr int PREP_ROWS = 16;
+constexpr int PREP_ROWS = 8;
 constexpr int PREP_LD = CONV_OUT + 6;  // 1574: W1's row length
 __global__ __launch_bounds__(256) void k_qact_prep1(const float* __restrict__ w1,
                                                     uint16_t* __restrict__ w1h,
                                                     uint16_t* __restrict__ w1l) {
-  extern __shared__ float rows[];  // [PREP_ROWS][PREP_LD]
-  const int blk = blockIdx.x, r0 = blk * PREP_ROWS;
+  __shared__ float rows[PREP_ROWS * PREP_LD];
+  const int r0 = blockIdx.x * PREP_ROWS;
   const float4* src = reinterpret_cast<const float4*>(w1 + (size_t)r0 * PREP_LD);
   for (int i = threadIdx.x; i < PREP_ROWS * PREP_LD / 4; i += 256)
     reinterpret_cast<float4*>(rows)[i] = src[i];
   __syncthreads();
-  const int nt = r0 / NT1, cq = (r0 % NT1) / 64, j = (r0 % 64) / 16;
-  for (int p = threadIdx.x; p < NCH * 64; p += 256) {  // (chunk, lane) pairs
-    const int c = p >> 6, lane = p & 63;
-    const float* row = rows + (lane & 15) * PREP_LD;
+  const int nt = r0 / NT1, cq = (r0 % NT1) / 64, j = (r0 % 64) / 16, half = (r0 % 16) / 8;
+  for (int p = threadIdx.x; p < NCH * 32; p += 256) {  // (chunk, lane of this half) pairs
+    const int c = p >> 5, lane = ((p >> 3) & 3) * 16 + half * 8 + (p & 7);
+    const float* row = rows + (lane & 7) * PREP_LD;
     uint32_t hi[4], lo[4];
 #pragma unroll
     for (int e = 0; e < 8; e += 2) {
@@ -674,12 +674,7 @@ hipError_t mz_launch_qact(const MzQAct& q, int relu, hipStream_t s) {
 
 hipError_t mz_launch_qact_prepare(const float* w1, const float* w2, uint16_t* w1h, uint16_t* w1l,
                                   uint16_t* w2h, uint16_t* w2l, hipStream_t s) {
-  constexpr size_t lds = sizeof(float) * PREP_ROWS * PREP_LD;  // 100.7 KB
-  static const hipError_t attr =
-      hipFuncSetAttribute(reinterpret_cast<const void*>(k_qact_prep1),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL(k_qact_prep1, dim3(N1 / PREP_ROWS), dim3(256), lds, s, w1, w1h, w1l);
+  hipLaunchKernelGGL(k_qact_prep1, dim3(N1 / PREP_ROWS), dim3(256), 0, s, w1, w1h, w1l);
   hipLaunchKernelGGL(k_qact_prep2, dim3(N2 * N1 / 8 / 256), dim3(256), 0, s, w2, w2h, w2l);
   return hipGetLastError();
 }

@@ -656,7 +656,10 @@ class VectorDQNLearner:
                 self._graph = (g,)
             else:
                 ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-                with torch.cuda.graph(ga):
+                # thread-local capture: the process group's watchdog thread polls the events of
+                # the warm-up all-reduces, which a global-mode capture forbids ("operation not
+                # permitted when stream is capturing" on RCCL)
+                with torch.cuda.graph(ga, capture_error_mode="thread_local"):
                     state, a, r, nxt = self.replay.sample(
                         self.batch_size, None if self.bit_stem else expand, static=True,
                         idx_static=self.overlap)
@@ -664,7 +667,7 @@ class VectorDQNLearner:
                     learner_backward(self.opt, loss)
                     ar.pack(self.source)
                     self._graph_loss = loss.detach()
-                with torch.cuda.graph(gb, pool=ga.pool()):
+                with torch.cuda.graph(gb, pool=ga.pool(), capture_error_mode="thread_local"):
                     ar.unpack(self.source)
                     learner_step(self.source, self.opt)
                 self._graph = (ga, gb)

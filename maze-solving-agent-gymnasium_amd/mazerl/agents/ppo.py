@@ -277,9 +277,11 @@ class PPOMinibatchGraph:
             gs = (g,)
         else:
             ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(ga, **kw):
+            # thread-local capture: the process group's watchdog thread polls earlier collectives'
+            # events, which a global-mode capture forbids
+            with torch.cuda.graph(ga, capture_error_mode="thread_local", **kw):
                 loss = ppo_minibatch(self.net, self.opt, *mb, self.coef, allreduce=ar, phase="a")
-            with torch.cuda.graph(gb, pool=ga.pool()):
+            with torch.cuda.graph(gb, pool=ga.pool(), capture_error_mode="thread_local"):
                 ppo_minibatch(self.net, self.opt, *mb, self.coef, allreduce=ar, phase="b")
             gs = (ga, gb)
         if self.pool is None:
