@@ -56,9 +56,11 @@ constexpr int XPT = 8 / NTL1;      // XCDs per output tile
 constexpr int PR = 17;             // padded window rows per instance
 constexpr int AST = 40;            // LDS A-tile row stride in bf16 (32 + 8: conflict-free b128)
 // k_qact2 rows per workgroup: each wave streams its 256 KB of fc2 hi / lo fragments once per
-// workgroup, so the rows per workgroup set the L2 traffic (64 rows: 2 MB per 64 rows)
+// workgroup (2 MB per 64 rows of L2 traffic). 128 rows halve that but need 256 VGPRs with spills:
+// alone no faster (greedy rows 0.466 vs 0.460 ms), inside training 58.2 vs 67.8-68.3 M env steps/s
+// (profiles/r03_qprep/train.jsonl) — 64 stays
 #ifndef MZ_QACT2_ROWS
-#define MZ_QACT2_ROWS 128
+#define MZ_QACT2_ROWS 64
 #endif
 constexpr int RT2 = MZ_QACT2_ROWS;
 constexpr int MI2 = RT2 / 16;      // k_qact2 row fragments per wave
