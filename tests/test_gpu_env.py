@@ -111,7 +111,7 @@ def _cell_words(env):
     return blob[256:256 + B * P * P * 4].view(np.uint32).reshape(B, P, P)
 
 
-@pytest.mark.parametrize("tor,dims", [(False, (15, 21, 41, 81, 127)), (True, (17, 41, 79))])
+@pytest.mark.parametrize("tor,dims", [(False, (15, 21, 41, 81, 127)), (True, (17, 41, 79, 125))])
 def test_generated_distance_field_matches_bfs(mazerl, tor, dims):
     """The distance-to-goal field in the cell words (len(find_path(p)) = D[p] + 1, a5) of
     Philox-generated mazes — derived from the carved tree (mz_tree_dist) for euclidean mazes,
