@@ -530,11 +530,14 @@ __global__ __launch_bounds__(WAVE * MZ_SPW) void k_step(MzDev d, const int32_t* 
 
 // ------------------------------------------------------------------------------------------
 // Wave-cooperative reset of instance e: BaseMazeEnv.reset (base_maze_env.py:136-161).
+// meta: the instance's meta words when the caller has them in registers (a bank maze just
+// copied in: one dependent global round trip fewer), else read here
 template <bool TOR, bool ENRICH>
-__device__ void reset_one(const MzDev& d, int e, const MzOut& o, uint32_t* wsh) {
+__device__ void reset_one(const MzDev& d, int e, const MzOut& o, uint32_t* wsh,
+                          const uint2* meta = nullptr) {
   const int lane = threadIdx.x;
   const size_t es = (size_t)e;
-  const uint32_t m0 = d.meta0[e], m1 = d.meta1[e];
+  const uint32_t m0 = meta ? meta->x : d.meta0[e], m1 = meta ? meta->y : d.meta1[e];
   const int N = m0 & 0xFF, sr = (m0 >> 16) & 0xFF, sc = m0 >> 24;
   const int gr = m1 & 0xFF, gc = (m1 >> 8) & 0xFF;
   const uint32_t cw = d.cells[es * d.P * d.P + (size_t)sr * d.P + sc];
@@ -606,11 +609,11 @@ __device__ inline bool regen_winner(const MzDev& d, int e) {
   return e < d.B && ((d.posw[e] >> 20) & 1u) && d.last_term[e];
 }
 
-// Copy n words, each lane keeping 16 loads in flight (a one-word-per-pass loop waits a full
+// Copy n words, each lane keeping 32 loads in flight (a one-word-per-pass loop waits a full
 // round trip per 256 B: 103 of them for an 81 x 81 maze's cell words).
 __device__ inline void wave_copy(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src,
                                  size_t n) {
-  constexpr int U = 16;
+  constexpr int U = 32;  // an 81 x 81 maze's cell words in 4 round trips
   for (size_t i = threadIdx.x & (WAVE - 1); i < n; i += U * WAVE) {
     uint32_t v[U];
 #pragma unroll
@@ -626,20 +629,21 @@ __device__ inline void wave_copy(uint32_t* __restrict__ dst, const uint32_t* __r
 // cls < 0 or an exhausted bank (slot >= K). The slots come from k_bank_count / k_bank_scan: the
 // winners of one reset_done launch take consecutive slots of their class in instance order, so
 // which winner receives which maze does not depend on the order the waves run in.
-__device__ bool bank_take(const MzDev& d, int e, int cls, int slot) {
+__device__ bool bank_take(const MzDev& d, int e, int cls, int slot, uint2& meta) {
   if (cls < 0 || slot >= d.bk_K) return false;
   const int a = cls / d.bk_nd, di = cls - a * d.bk_nd;
   const size_t src = ((size_t)mz_bank_aidx(d.bk_amask, a) * d.bk_nd + di) * d.bk_K + slot;
   const size_t es = (size_t)e;
   const size_t pp = (size_t)d.P * d.P;
+  meta = make_uint2(d.bk_meta0[src], d.bk_meta1[src]);  // issued with the copy's first loads
   wave_copy(d.cells + es * pp, d.bk_cells + src * pp, pp);
   const size_t pw = (size_t)d.PW;
   wave_copy(d.planes + es * pw, d.bk_planes + src * pw, pw);
   if (threadIdx.x == 0) {
-    d.meta0[e] = d.bk_meta0[src];
-    d.meta1[e] = d.bk_meta1[src];
+    d.meta0[e] = meta.x;
+    d.meta1[e] = meta.y;
   }
-  __syncthreads();  // reset_one reads meta0 / the start cell word written above
+  __syncthreads();  // reset_one reads the start cell word / window rows written above
   return true;
 }
 
@@ -720,11 +724,12 @@ __global__ __launch_bounds__(WAVE) void k_reset_done(MzDev d, int regen, uint64_
   const int grp = blockIdx.x / MZ_RD_SPLIT, part = blockIdx.x - grp * MZ_RD_SPLIT;
   const int lane = threadIdx.x, e = grp * WAVE + lane;
   const bool done = e < d.B && ((d.posw[e] >> 20) & 1u);
+  const bool win = regen && done && d.last_term[e];  // gets a new maze (loaded once, coalesced)
   // this lane's bank slot if it is a winner with a bank class: the group's first slot of the
   // class (k_bank_scan) + its rank among the group's winners of the class
   int cls = -1, slot = 0;
   if (regen && d.bk_K) {
-    cls = regen_winner(d, e) ? bank_class(d, e) : -1;
+    cls = win ? bank_class(d, e) : -1;
     unsigned long long pend = __ballot(cls >= 0);
     while (pend) {
       const int cj = __shfl(cls, __ffsll((long long)pend) - 1);
@@ -741,14 +746,16 @@ __global__ __launch_bounds__(WAVE) void k_reset_done(MzDev d, int regen, uint64_
     bal &= bal - 1;
     const int ej = grp * WAVE + j;
     const int cj = __shfl(cls, j), sj = __shfl(slot, j);
-    if (regen && d.last_term[ej]) {
-      const int a = d.algo[ej], N = (int)(d.meta0[ej] & 0xFF);
-      if (!bank_take(d, ej, cj, sj))
-        mz_build_one(d, ej, TOR, true, a, seed + (uint64_t)ej + ((uint64_t)epoch << 32), N,
-                     nullptr, 0, 0, 0, 0, lds);
+    uint2 meta;
+    bool have_meta = false;
+    if (__shfl((int)win, j)) {
+      have_meta = bank_take(d, ej, cj, sj, meta);
+      if (!have_meta)  // no bank class or the bank is exhausted: build in place
+        mz_build_one(d, ej, TOR, true, d.algo[ej], seed + (uint64_t)ej + ((uint64_t)epoch << 32),
+                     (int)(d.meta0[ej] & 0xFF), nullptr, 0, 0, 0, 0, lds);
       __syncthreads();  // this workgroup's global stores are visible to it past the barrier
     }
-    reset_one<TOR, ENRICH>(d, ej, o, wsh);
+    reset_one<TOR, ENRICH>(d, ej, o, wsh, have_meta ? &meta : nullptr);
     __syncthreads();
   }
 }
