@@ -710,11 +710,13 @@ __global__ __launch_bounds__(WAVE) void k_bank_fill(MzDev bd, const int* head, i
 // then resets the done instances of its share of them cooperatively, one after another — waves
 // with nothing to do exit at once, no device list or counter is involved. With regen, instances
 // whose last step terminated first get a new maze (win -> update_maze,
-// off_policy_trainer.py:190-202). MZ_RD_SPLIT waves share a 64-instance group (each resets the
-// done instances of 64 / MZ_RD_SPLIT of its lanes): a reset is a chain of ~10 dependent global
-// round trips, and the launch lasts as long as the group with the most done instances.
+// off_policy_trainer.py:190-202). MZ_RD_SPLIT waves may share a 64-instance group (each resets
+// the done instances of 64 / MZ_RD_SPLIT of its lanes) to shorten the longest chain of resets;
+// inside training the launch's time is mostly waiting for CU slots beside the acting and update
+// kernels, and one wave per group measured best (68.3 / 68.5 vs 67.0 / 67.4 M env steps/s with 4,
+// profiles/r03_adamw_qw8_rd1/train.jsonl).
 #ifndef MZ_RD_SPLIT
-#define MZ_RD_SPLIT 4
+#define MZ_RD_SPLIT 1
 #endif
 template <bool TOR, bool ENRICH>
 __global__ __launch_bounds__(WAVE) void k_reset_done(MzDev d, int regen, uint64_t seed,

@@ -25,7 +25,6 @@
 #include <math.h>
 #include <stdint.h>
 
-#include <algorithm>
 #include <mutex>
 #include <unordered_map>
 
@@ -41,12 +40,6 @@
 #endif
 #ifndef MZ_ADAMW_TPB
 #define MZ_ADAMW_TPB 512
-#endif
-// MZ_ADAMW_PREINC: a one-thread launch advances the step count before k_adamw, which then reads
-// it and takes no ticket — so its grid is free: 2,048 workgroups of 256 threads (A/B: 0 = the
-// ticketed launch above)
-#ifndef MZ_ADAMW_PREINC
-#define MZ_ADAMW_PREINC 1
 #endif
 
 namespace {
@@ -77,16 +70,15 @@ __device__ inline void publish_step(float* step, unsigned* ticket, float t) {
   }
 }
 
-__global__ void k_adamw_step(float* step_dev) { step_dev[0] = step_dev[0] + 1.0f; }
-
-template <bool PRE>
-__global__ __launch_bounds__(PRE ? 256 : MZ_ADAMW_TPB) void k_adamw(
-    float* __restrict__ p, float* __restrict__ m, float* __restrict__ v, Segs segs,
-    const float* __restrict__ lr_dev, float* step_dev, unsigned* ticket, double b1, double b2,
-    double eps_d, double wd, float clamp, float gscale, int write_grad) {
+__global__ __launch_bounds__(MZ_ADAMW_TPB) void k_adamw(float* __restrict__ p, float* __restrict__ m,
+                                               float* __restrict__ v, Segs segs,
+                                               const float* __restrict__ lr_dev,
+                                               float* step_dev, unsigned* ticket, double b1,
+                                               double b2, double eps_d, double wd, float clamp,
+                                               float gscale, int write_grad) {
   // the per-step scalars as torch's eager AdamW forms them (Python doubles, then f32 operands)
   const double lr = (double)*lr_dev;
-  const float t_next = PRE ? step_dev[0] : step_dev[0] + 1.0f;  // PRE: k_adamw_step advanced it
+  const float t_next = step_dev[0] + 1.0f;
   const double t = (double)t_next;
   const double bc1 = 1.0 - pow(b1, t);
   const float step_size = (float)(lr / bc1);
@@ -127,7 +119,7 @@ __global__ __launch_bounds__(PRE ? 256 : MZ_ADAMW_TPB) void k_adamw(
     reinterpret_cast<float4*>(v)[q] = v4;
     if (write_grad) *gp = g4;  // the clamped gradient stays visible, as with clamp_ in place
   }
-  if (!PRE) publish_step(step_dev, ticket, t_next);
+  publish_step(step_dev, ticket, t_next);
 }
 
 // ---- PPO's optimizer step (ppo_agent.py:232-236): clip_grad_norm_(params, 0.5), then AdamW
@@ -267,14 +259,6 @@ hipError_t mz_launch_adamw(float* p, float* m, float* v, const float* const* gra
     sg.g[k] = grads[k];
     sg.off[k + 1] = sg.off[k] + seg_len[k];
   }
-  if (MZ_ADAMW_PREINC) {
-    hipLaunchKernelGGL(k_adamw_step, dim3(1), dim3(1), 0, s, step);
-    const int64_t n4 = sg.off[nseg] >> 2;
-    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(2048, (n4 + 255) / 256));
-    hipLaunchKernelGGL(k_adamw<true>, dim3(blocks), dim3(256), 0, s, p, m, v, sg, lr, step, nullptr,
-                       b1, b2, eps, wd, clamp, gscale, write_grad);
-    return hipGetLastError();
-  }
   // the ticket slot of this step counter (assigned on first use; hipGetSymbolAddress is not a
   // stream operation, so this also works while a graph is being captured)
   static std::mutex mu;
@@ -300,7 +284,7 @@ hipError_t mz_launch_adamw(float* p, float* m, float* v, const float* const* gra
   int blocks = (int)((n4 + MZ_ADAMW_TPB - 1) / MZ_ADAMW_TPB);
   if (blocks > MZ_ADAMW_MAXWG) blocks = MZ_ADAMW_MAXWG;  // grid-stride beyond
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(k_adamw<false>, dim3(blocks), dim3(MZ_ADAMW_TPB), 0, s, p, m, v, sg, lr, step, ticket, b1, b2, eps, wd,
+  hipLaunchKernelGGL(k_adamw, dim3(blocks), dim3(MZ_ADAMW_TPB), 0, s, p, m, v, sg, lr, step, ticket, b1, b2, eps, wd,
                      clamp, gscale, write_grad);
   return hipGetLastError();
 }
