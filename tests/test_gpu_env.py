@@ -114,8 +114,9 @@ def _cell_words(env):
 @pytest.mark.parametrize("tor,dims", [(False, (15, 21, 41, 81, 127)), (True, (17, 41, 79, 125))])
 def test_generated_distance_field_matches_bfs(mazerl, tor, dims):
     """The distance-to-goal field in the cell words (len(find_path(p)) = D[p] + 1, a5) of
-    Philox-generated mazes — derived from the carved tree (mz_tree_dist) for euclidean mazes,
-    by the wave BFS on the torus — == the oracle's BFS from the goal on every open cell, and the
+    Philox-generated mazes — derived from the carved tree for euclidean mazes (mz_cs_dist of the
+    cell-space build), by the row-mask BFS on the torus — == the oracle's BFS from the goal on
+    every open cell, and the
     open / open-neighbour bits == the grid, for all three generators."""
     import pyoracle as O
     B = 48
