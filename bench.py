@@ -64,7 +64,7 @@ def pmc_traffic(mode, envs, dim):
                                               f"({rec.get('tag')}), k_step sources {rec['source_sha']}")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
@@ -101,21 +101,46 @@ def parse():
     ap.add_argument("--overlap", type=int, default=1,
                     help="1: learner updates on a side HIP stream, overlapped with acting + env "
                          "step (acting weights one update behind); 0: sequential")
-    return ap.parse_args()
+    ap.add_argument("--graph", type=int, default=1,
+                    help="1: the timed env steps replay captured HIP graphs of k_step launches "
+                         "(the Python launch loop is timed beside them); 0: eager launches")
+    ap.add_argument("--graph-chunk", type=int, default=100, help="k_step launches per graph")
+    ap.add_argument("--config-legs", default="cfg4,cfg5",
+                    help="BASELINE configs 4 (DDQN, mixed 81x81) and 5 (PPO, toroidal 17..79) at "
+                         "this N, whole-node env steps/s + win-rates ('' = skip)")
+    ap.add_argument("--cfg4-envs", type=int, default=8192, help="config 4 instances per GPU")
+    ap.add_argument("--cfg5-envs", type=int, default=4096, help="config 5 instances per GPU")
+    ap.add_argument("--cfg4-steps", type=int, default=600)
+    ap.add_argument("--cfg5-steps", type=int, default=600)
+    ap.add_argument("--cfg-eval-mazes", type=int, default=500)
+    ap.add_argument("--launch-timeout", type=float, default=2400.0,
+                    help="--gpus N > 1 without torchrun: seconds before the ranks are killed")
+    return ap.parse_args(argv)
 
 
 def win_rate(a, dev, rank=0, world=1):
     """Second half of the metric: train DDQN (reference DDQN net/loss, vectorised) on the same
-    config, then the win-rate on `eval_mazes` fresh mazes, greedy and with the reference's
-    epsilon (0.1) protocol (off_policy_trainer.py:228-263). With N ranks every rank
-    trains on its own env shard and the source-net gradients are averaged over RCCL once per
-    update (mazerl/distributed.py: one 8.56 MB bucket); rank 0 evaluates."""
+    config, then win-rates on `eval_mazes` fresh mazes (never seen in training), rank 0:
+      greedy / eps_0.1            r-prim mazes as generated, epsilon 0 and a fixed 0.1 (SURVEY
+                                  Q14's reading of the final epsilon);
+      *_best_of_6                 r-prim mazes, each the easiest of 6 candidates by McClendon
+                                  difficulty (the reference env's selection, base_maze_env.py:
+                                  78-97);
+      new_mazes_reference_protocol  NeuralOffPolicyTrainer.test(num, new=True) (off_policy_trainer
+                                  .py:228-263): per maze random.choice(r-prim, prim&kill, dfs) and a
+                                  best-of-6 maze of that algorithm; acting greedy, and through
+                                  get_action with epsilon from steps_done carried over from
+                                  training (dqn_agent.py:104-119) — the protocol of the README's
+                                  99.6 % "new mazes" figure (its 41x41, 125 training episodes).
+    With N ranks every rank trains on its own env shard and the source-net gradients are averaged
+    over RCCL once per update (mazerl/distributed.py: one 8.56 MB bucket)."""
     import torch
     import torch.distributed as dist
     from mazerl import VectorMazeEnv
     from mazerl.agents.dqn import VectorDQNLearner
     from mazerl.distributed import GradAllReduce, broadcast_params
-    from mazerl.trainers.vector_trainer import VectorOffPolicyTrainer, best_of_mazes, evaluate
+    from mazerl.trainers.vector_trainer import (VectorOffPolicyTrainer, best_of_mazes, evaluate,
+                                                maze_algorithms, steps_done_epsilon)
     env = VectorMazeEnv(a.envs, a.dim, enrich=True, device=dev, algorithm=a.algo,
                         seed=0xA11CE + rank * a.envs, done_list=False, window=False,
                         window_bits=True)  # acting reads the bits
@@ -140,18 +165,32 @@ def win_rate(a, dev, rank=0, world=1):
     env.close()
     if rank != 0:
         return None
+    log("win-rate evaluation")
     agree = acting_agreement(L)
-    g, _ = evaluate(L, a.eval_mazes, a.dim, a.algo, seed=0x7E570000, eps=0.0, device=dev)
-    e, _ = evaluate(L, a.eval_mazes, a.dim, a.algo, seed=0x7E570000, eps=0.1, device=dev)
-    # the same protocol on mazes chosen as the reference's env chooses them: the easiest (McClendon
-    # difficulty) of 6 candidates (base_maze_env.py:78-97) — the README's "new mazes" win-rates
+    n = a.eval_mazes
+    g, _ = evaluate(L, n, a.dim, a.algo, seed=0x7E570000, eps=0.0, device=dev)
+    e, _ = evaluate(L, n, a.dim, a.algo, seed=0x7E570000, eps=0.1, device=dev)
     t6 = time.perf_counter()
-    mz6 = best_of_mazes(a.eval_mazes, a.dim, a.algo, seed=0x7E580000, device=dev)
+    mz6 = best_of_mazes(n, a.dim, a.algo, seed=0x7E580000, device=dev)
     t6 = time.perf_counter() - t6  # 6 x eval_mazes candidates generated + McClendon on the GPU
-    g6, _ = evaluate(L, a.eval_mazes, a.dim, a.algo, seed=0x7E580000, eps=0.0, device=dev, mazes=mz6)
-    e6, _ = evaluate(L, a.eval_mazes, a.dim, a.algo, seed=0x7E580000, eps=0.1, device=dev, mazes=mz6)
+    g6, _ = evaluate(L, n, a.dim, a.algo, seed=0x7E580000, eps=0.0, device=dev, mazes=mz6)
+    e6, _ = evaluate(L, n, a.dim, a.algo, seed=0x7E580000, eps=0.1, device=dev, mazes=mz6)
+    algos = maze_algorithms(n, seed=0x7E590000)
+    mzr = best_of_mazes(n, a.dim, algos, seed=0x7E590000, device=dev)
+    gr, _ = evaluate(L, n, a.dim, seed=0x7E590000, eps=0.0, device=dev, mazes=mzr)
+    sde = steps_done_epsilon(L, n)
+    er, kr = evaluate(L, n, a.dim, seed=0x7E590000, eps=sde, device=dev, mazes=mzr)
     return {"greedy": g, "eps_0.1": e, "greedy_best_of_6": g6, "eps_0.1_best_of_6": e6,
-            "eval_mazes": a.eval_mazes, "variant": "ddqn",
+            "new_mazes_reference_protocol": {
+                "greedy": gr, "eps_from_steps_done": er,
+                "eps_start_mean": sde.start_mean, "eps_decay": decay,
+                "algorithms": {x: algos.count(x) for x in sorted(set(algos))},
+                "note": "test(num, new=True): per maze random.choice(ALGOS) + best-of-6 by McClendon "
+                        "difficulty; eps_from_steps_done acts through get_action's epsilon with each "
+                        "maze continuing a training instance's steps_done (episodes side by side "
+                        "here, one after another in the reference); the reference's 99.6 % was "
+                        "measured at 41x41 after 125 single-env episodes (README.md)"},
+            "eval_mazes": n, "variant": "ddqn",
             "ranks": world, "train_vector_steps": a.train_steps + 20,
             "train_seconds_steady": round(secs, 3),
             "train_env_steps_per_s": a.envs * a.train_steps * world / secs,
@@ -166,9 +205,117 @@ def win_rate(a, dev, rank=0, world=1):
                               if world > 1 else None,
             "acting_argmax_agreement": agree,
             "best_of_6_selection_seconds": round(t6, 3),
-            "note": "fresh GPU-generated mazes never seen in training (test(new=True) protocol); "
-                    "*_best_of_6: each maze the easiest of 6 candidates by McClendon difficulty, "
-                    "as the reference's env selects new mazes (base_maze_env.py:78-97)"}
+            "note": "greedy / eps_0.1: fresh r-prim mazes as generated; *_best_of_6: each r-prim "
+                    "maze the easiest of 6 candidates by McClendon difficulty, as the reference's "
+                    "env selects new mazes (base_maze_env.py:78-97); new_mazes_reference_protocol: "
+                    "the reference's test(new=True) protocol (mixed algorithms, epsilon from "
+                    "steps_done)"}
+
+
+def config_legs(a, dev, rank=0, world=1):
+    """BASELINE configs 4 and 5 at the bench's N (north_star's 8-GPU configs; per rank the share of
+    the 8-GPU job: 8,192 and 4,096 instances), each trained for a fixed number of vector steps
+    between a barrier + synchronize on each side, whole-node env steps/s = all ranks' env steps /
+    the max-over-ranks time; rank 0 then evaluates:
+      cfg4  DDQN on 8,192 mixed dfs / r-prim / prim&kill 81x81 mazes per rank (algo = global
+            instance id mod 3, SURVEY §8d), source-net gradients all-reduced over RCCL per update;
+            win-rates under the reference's test(new=True) protocol (mixed algorithms, best-of-6,
+            greedy and epsilon from steps_done);
+      cfg5  PPO on 4,096 toroidal mazes of sizes 17..79 per rank (instance i: 17 + 2 (i mod 32)),
+            gradients all-reduced per minibatch; greedy win-rate on fresh mazes as generated and on
+            best-of-6 mazes (toroidal_maze_env.py:40-54: difficulty of the bordered maze)."""
+    import torch
+    import torch.distributed as dist
+    from mazerl import VectorMazeEnv
+    from mazerl.agents.dqn import VectorDQNLearner
+    from mazerl.distributed import GradAllReduce, broadcast_params
+    from mazerl.trainers.ppo_trainer import VectorPPOTrainer
+    from mazerl.trainers.vector_trainer import (VectorOffPolicyTrainer, best_of_mazes, evaluate,
+                                                make_env, maze_algorithms, steps_done_epsilon)
+
+    def timed_train(tr, steps):
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        secs = tr.train(steps)
+        if world > 1:
+            dist.barrier()
+            t = torch.tensor([secs], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            secs = float(t.item())
+        return secs
+
+    out = {}
+    legs = [x for x in a.config_legs.split(",") if x]
+    if "cfg4" in legs:
+        log("config 4 leg (DDQN, mixed 81x81)")
+        B, dim = a.cfg4_envs, 81
+        algo = ((torch.arange(B) + rank * B) % 3).to(torch.uint8)
+        env = VectorMazeEnv(B, dim, enrich=True, device=dev, algorithm=algo,
+                            seed=0x5EED0000 + rank * B, done_list=False, window=False, window_bits=True)
+        env.set_algorithm(algo)
+        decay = ((dim - 1) * (dim - 1) // 2) * 5 / 40.0
+        L = VectorDQNLearner(B, dev, variant="ddqn", lr=1e-3, eps_start=0.95, eps_final=0.1,
+                             eps_decay=decay, gamma=0.7, batch_size=2048, capacity=2_000_000,
+                             target_every=13, allreduce=GradAllReduce() if world > 1 else None,
+                             overlap=True, seed=0)
+        if world > 1:
+            broadcast_params(L.source)
+            L.target.load_state_dict(L.source.state_dict())
+        tr = VectorOffPolicyTrainer(env, L, seed=7919 * rank)
+        tr.train(20)
+        secs = timed_train(tr, a.cfg4_steps)
+        env.close()
+        rec = {"envs_per_gpu": B, "grid": dim, "algo": "mixed (global id mod 3)",
+               "vector_steps": a.cfg4_steps, "seconds": round(secs, 3),
+               "env_steps_per_s": B * a.cfg4_steps * world / secs, "updates": L.n_updates,
+               "batch": 2048, "grad_allreduce": (dist.get_backend() if world > 1 else None)}
+        if rank == 0:
+            n = a.cfg_eval_mazes
+            algos = maze_algorithms(n, seed=0x7E5A0000)
+            mz = best_of_mazes(n, dim, algos, seed=0x7E5A0000, device=dev)
+            rec["win_rate_reference_protocol_greedy"], _ = evaluate(
+                L, n, dim, seed=0x7E5A0000, eps=0.0, device=dev, mazes=mz)
+            rec["win_rate_reference_protocol_eps_from_steps_done"], _ = evaluate(
+                L, n, dim, seed=0x7E5A0000, eps=steps_done_epsilon(L, n), device=dev, mazes=mz)
+            rec["eval_mazes"] = n
+        out["cfg4"] = rec
+        del tr, L
+    if "cfg5" in legs:
+        log("config 5 leg (PPO, toroidal 17..79)")
+        B = a.cfg5_envs
+        dims = list(range(17, 80, 2))
+        env = make_env(B, dims, toroidal=True, algorithm="r-prim", seed=0x5EED0000 + rank * B,
+                       device=dev, done_list=False, reward64=True, window=False, window_bits=True)
+        tr = VectorPPOTrainer(env, dev, gamma=0.9, batch_size=2048, ppo_steps=2, pool_size=32768,
+                              seed=7919 * rank, allreduce=GradAllReduce() if world > 1 else None)
+        if world > 1:
+            broadcast_params(tr.net)
+        tr.train(20)
+        secs = timed_train(tr, a.cfg5_steps)
+        rec = {"envs_per_gpu": B, "dims": [dims[0], dims[-1]], "toroidal": True,
+               "vector_steps": a.cfg5_steps, "seconds": round(secs, 3),
+               "env_steps_per_s": B * a.cfg5_steps * world / secs, "updates": tr.updates,
+               "grad_allreduce": (dist.get_backend() if world > 1 else None)}
+        env.close()
+        if rank == 0:
+            n = a.cfg_eval_mazes
+            rec["win_rate_greedy"], _ = evaluate(tr, n, dims, "r-prim", seed=0x7E5B0000, eps=0.0,
+                                                 toroidal=True, device=dev)
+            t6 = time.perf_counter()
+            mz = best_of_mazes(n, dims, "r-prim", seed=0x7E5C0000, device=dev, toroidal=True)
+            rec["best_of_6_selection_seconds"] = round(time.perf_counter() - t6, 3)
+            rec["win_rate_greedy_best_of_6"], _ = evaluate(tr, n, dims, seed=0x7E5C0000, eps=0.0,
+                                                           toroidal=True, device=dev, mazes=mz)
+            rec["eval_mazes"] = n
+        out["cfg5"] = rec
+        del tr
+    return out
+
+
+def log(msg):
+    """Progress on stderr (the JSON line is the only stdout output)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
 def acting_agreement(L, n=65536):
@@ -200,6 +347,78 @@ def acting_agreement(L, n=65536):
             "agreement_f32_gap_over_1pct": float((a32 == aa)[clear].float().mean()),
             "rows_f32_gap_over_1pct": int(clear.sum()),
             "acting_dtype": getattr(fused, "dtype_note", "bf16 GEMMs (f32 accumulate), bf16 stem")}
+
+
+def launch_plan(n, environ, port):
+    """The N rank environments `python3 bench.py --gpus N` starts when no launcher set WORLD_SIZE
+    (the variables torchrun gives each rank: one process per GPU, rank r on GPU r)."""
+    plan = []
+    for r in range(n):
+        e = dict(environ)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR=environ.get("MASTER_ADDR", "127.0.0.1"),
+                 MASTER_PORT=str(port), MZ_BENCH_LAUNCHER="1")
+        plan.append(e)
+    return plan
+
+
+def needs_launch(a, environ):
+    """Decided from argv and the environment alone, before anything touches the GPU: --gpus N > 1
+    and no launcher has set WORLD_SIZE -> this process starts the N ranks itself."""
+    return a.gpus > 1 and "WORLD_SIZE" not in environ
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(n, argv, timeout, environ=None, script=None):
+    """Start N child processes of this script (subprocess, never exec: the parent has not touched
+    the GPU and stays a plain supervisor), rank 0's stdout inherited (its JSON line is the
+    output), the other ranks' stdout on stderr. If any rank fails or the deadline passes, every
+    rank's process group is killed and the exit status is non-zero. Returns the exit status."""
+    import signal
+    import subprocess
+    environ = dict(os.environ if environ is None else environ)
+    port = int(environ.get("MASTER_PORT") or _free_port())
+    script = script or os.path.abspath(__file__)
+    procs = []
+    for r, env in enumerate(launch_plan(n, environ, port)):
+        procs.append(subprocess.Popen([sys.executable, "-u", script] + list(argv), env=env,
+                                      stdout=None if r == 0 else sys.stderr.fileno(),
+                                      start_new_session=True))
+    deadline = time.monotonic() + timeout
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:
+            rc = bad[0] if bad[0] > 0 else 128 - bad[0]
+            print(f"bench launcher: a rank exited with {bad[0]}; stopping the others", file=sys.stderr)
+            break
+        if all(c == 0 for c in codes):
+            break
+        if time.monotonic() > deadline:
+            rc = 124
+            print(f"bench launcher: deadline of {timeout:.0f} s passed; stopping the ranks",
+                  file=sys.stderr)
+            break
+        time.sleep(0.2)
+    if rc:
+        for sig, wait in ((signal.SIGTERM, 10.0), (signal.SIGKILL, 5.0)):
+            for p in procs:
+                if p.poll() is None:
+                    try:
+                        os.killpg(p.pid, sig)
+                    except ProcessLookupError:
+                        pass
+            t0 = time.monotonic()
+            while any(p.poll() is None for p in procs) and time.monotonic() - t0 < wait:
+                time.sleep(0.1)
+    return rc
 
 
 BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X bf16 MFMA, dense (MI355X_MICROARCH.md)
@@ -336,6 +555,8 @@ def cpu_baseline(env, seconds):
 
 def main():
     a = parse()
+    if needs_launch(a, os.environ):
+        sys.exit(launch(a.gpus, sys.argv[1:], a.launch_timeout))
     import torch
     import torch.distributed as dist
 
@@ -345,11 +566,15 @@ def main():
     local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)  # before the process group: RCCL binds each rank to its GPU
     dev = torch.device("cuda", local)
+    backend = None
     if world > 1:
         # RCCL ("nccl") on the 8-GPU node; MZ_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs
         backend = os.environ.get("MZ_DIST_BACKEND", "nccl")
         kw = {"device_id": dev} if backend == "nccl" else {}
         dist.init_process_group(backend, init_method="env://", **kw)
+    ranks_seen = dist.get_world_size() if world > 1 else 1
+    if rank == 0:
+        log(f"rank 0 of {ranks_seen} on {dev} (backend {backend})")
 
     import mazerl
     B = a.envs
@@ -371,43 +596,75 @@ def main():
             # one launch: fused act + step, autoreset of the instances that finished last step
             env.step_act(eps=1.0, seed=0xBE7C4 + rank, counter=k, autoreset=True)
 
+        def timed(run):
+            """K steps between a barrier + synchronize on each side: wall seconds (max over the
+            ranks) and the HIP-event time of the K launches on the launch stream."""
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            ev0.record(stream)
+            run()
+            ev1.record(stream)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            el = time.perf_counter() - t0
+            if world > 1:
+                t = torch.tensor([el], dtype=torch.float64, device=dev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                el = float(t.item())
+            return el, ev0.elapsed_time(ev1) / a.steps
+
         for k in range(a.warmup):
             vstep(k)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        ev0.record(stream)
-        for k in range(a.steps):
-            vstep(a.warmup + k)
-        ev1.record(stream)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        el = time.perf_counter() - t0
-        avg_kernel_ms = ev0.elapsed_time(ev1) / a.steps
-        if world > 1:
-            t = torch.tensor([el], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = float(t.item())
+        graphs = []
+        if a.graph:
+            # the K timed launches as replays of captured HIP graphs of `chunk` k_step launches
+            # each (the same launch with the same work per step; counters a.warmup + j of each
+            # chunk, so each replay repeats the chunk's Philox draws over the evolving state)
+            chunk = max(1, min(a.graph_chunk, a.steps))
+            sizes = [chunk] * (a.steps // chunk) + ([a.steps % chunk] if a.steps % chunk else [])
+            made = {}
+            for n_ in sorted(set(sizes)):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    for j in range(n_):
+                        vstep(a.warmup + j)
+                made[n_] = g
+            graphs = [made[n_] for n_ in sizes]
+            for g in made.values():  # untimed: one replay of each graph
+                g.replay()
+        el, avg_kernel_ms = timed(lambda: [g.replay() for g in graphs] if graphs else
+                                  [vstep(a.warmup + k) for k in range(a.steps)])
+        eager = None
+        if graphs:  # the same K steps as K eager launches from the Python loop, for comparison
+            el_e, avg_e = timed(lambda: [vstep(a.warmup + k) for k in range(a.steps)])
+            eager = {"value": B * a.steps * world / el_e, "ms_per_step": el_e / a.steps * 1e3,
+                     "avg_kernel_ms": avg_e}
+        del graphs
         alg = ALG_BYTES_PER_STEP if mode == "window" else ALG_BYTES_PER_STEP_BITS
         achieved = alg * B / (avg_kernel_ms * 1e-3) / 1e9
         traffic, tnote = pmc_traffic(mode, B, a.dim)
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                 "kernel": "k_step", "avg_kernel_ms": avg_kernel_ms,
-                "timing": "HIP events around the timed region on the launch stream",
+                "timing": "HIP events around the timed region on the launch stream"
+                          + (f" (replays of captured HIP graphs of {min(a.graph_chunk, a.steps)} "
+                             "k_step launches)" if a.graph else " (eager launches)"),
                 "alg_bytes_per_instance_step": alg, "traffic_source": tnote}
         return env, {"value": B * a.steps * world / el, "ms_per_step": el / a.steps * 1e3,
-                     "roofline": roof, "gen_s": gen_s}
+                     "roofline": roof, "gen_s": gen_s, "eager_launch_loop": eager}
 
     res = {}
     env = None
     for mode in legs:
         if env is not None:
             env.close()
+        if rank == 0:
+            log(f"env-step leg: {mode}")
         env, res[mode] = leg(mode)
     head = res["window"] if "window" in res else res[legs[0]]
     value, gen_s = head["value"], head["gen_s"]
@@ -430,6 +687,10 @@ def main():
             "value": value,
             "unit": "env steps/s",
             "n_gpus": world,
+            "ranks_seen": ranks_seen,
+            "backend": ("RCCL (torch.distributed nccl)" if backend == "nccl" else backend),
+            "launch": ("bench.py --gpus N (self-launched ranks)" if os.environ.get("MZ_BENCH_LAUNCHER") == "1"
+                       else ("torchrun / external launcher" if world > 1 else "single process")),
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": head["ms_per_step"],
@@ -442,9 +703,11 @@ def main():
                                    f"per GPU: fused act + env step (f32 3x15x15 window) with autoreset, one launch per step",
                        "envs_per_gpu": B, "grid": a.dim, "algo": a.algo, "parallelism": f"dp{world} env shards"},
             "roofline": head["roofline"],
+            "eager_launch_loop": head["eager_launch_loop"],
             "bits_mode": ({"value": res["bits"]["value"], "unit": "env steps/s",
                            "ms_per_step": res["bits"]["ms_per_step"],
                            "roofline": res["bits"]["roofline"],
+                           "eager_launch_loop": res["bits"]["eager_launch_loop"],
                            "note": "the same step in the trainers' mode (window_bits=True: the "
                                    "675-bit window as 88 B of bits, no f32 window)"}
                           if "bits" in res and "window" in res else None),
@@ -456,13 +719,20 @@ def main():
             "win_rate": None,
         }
         if world == 1 and not a.no_cpu_baseline:
+            log("cpu_baseline")
             out["cpu_baseline"] = cpu_baseline(env, a.cpu_seconds)
     env.close()
     if a.train_steps > 0:
+        if rank == 0:
+            log("DDQN win-rate leg (configs[2])")
         wr = win_rate(a, dev, rank, world)  # every rank trains its shard (grad all-reduce)
         if rank == 0:
             out["win_rate"] = wr
             out["q_head"] = q_head(dev, B)
+    if a.config_legs:
+        cl = config_legs(a, dev, rank, world)
+        if rank == 0:
+            out["configs"] = cl
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -496,7 +496,10 @@ int mz_ppo_act(const float* logits_dev, int32_t ldl, const float* value_dev, int
  * episode's returns are NaN: torch.std of one element; counted in stats_dev[2] instead) — an
  * entry in the finished list (instance fin_id, pool row fin_off, length fin_len; instance order)
  * placed after the pool's current *pool_fill_dev rows; *pool_fill_dev and the monotonic
- * *pool_total_dev grow by the listed rows. One workgroup. */
+ * *pool_total_dev grow by the listed rows. stats_dev[3] counts unfinished episodes that reached
+ * L steps (their records would leave the [B][L] buffers; t_dev stays at L - 1): the caller sizes
+ * L past every max_steps + 1 and treats a nonzero count as an error. stats_dev is int64[4].
+ * One workgroup. */
 int mz_ppo_scan(const double* reward64_dev, const uint8_t* term_dev, const uint8_t* trunc_dev,
                 int32_t B, int32_t L, int32_t* t_dev, double* rec_r_dev, int32_t* fin_id_dev,
                 int64_t* fin_off_dev, int32_t* fin_len_dev, int32_t* fin_count_dev,

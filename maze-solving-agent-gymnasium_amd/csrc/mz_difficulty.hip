@@ -6,7 +6,10 @@
 //   - node order = first insertion by create_graph_branch (:115-123) / add_edge (u before v);
 //   - per-node adjacency order = first insertion of each edge (re-adding keeps the position);
 //   - connected components are listed by their first node in node order (nx.connected_components);
-//   - a subgraph's edges iterate (node order, adjacency order, each edge once);
+//   - a hallway's edges iterate (view node order, adjacency order, each edge once), the view's
+//     node order being CPython 3.10 set-table order of show_nodes' set when it holds fewer than
+//     half of G's nodes (networkx 3.4 FilterAdjacency), else node order — the sets rebuilt as the
+//     reference builds them (PySetEm, extract_hallways :194-218);
 //   - branch products run over branch ids 1..m, then branch 0 (:323-329).
 // Used by BaseMazeEnv.get_maze_difficulty (base_maze_env.py:99-105) and best-of-6 generation
 // (base_maze_env.py:78-97). Paths come from a depth-unlimited A* with Python heapq order
@@ -102,20 +105,90 @@ struct Graph {  // insertion-ordered undirected graph (what networkx.Graph keeps
   }
 };
 
-// A node-induced view: edges in (node order, adjacency order), each once.
+// CPython 3.10 set table for int keys (hash(n) == n), Objects/setobject.c: the order networkx's
+// subgraph views iterate their node set in (oracle/pyset.py restates it and checks it against the
+// interpreter). No deletions occur, so no dummy entries.
+struct PySetEm {
+  static constexpr int32_t EMPTY = -1;
+  std::vector<int32_t> t = std::vector<int32_t>(8, EMPTY);
+  size_t mask = 7, fill = 0, used = 0;
+  bool small = true;  // still the 8-slot smalltable
+
+  static void insert_clean(std::vector<int32_t>& tab, size_t m, int32_t key) {
+    size_t perturb = (size_t)key, i = (size_t)key & m;
+    for (;;) {
+      if (tab[i] == EMPTY) { tab[i] = key; return; }
+      if (i + 9 <= m)
+        for (size_t j = 1; j <= 9; ++j)
+          if (tab[i + j] == EMPTY) { tab[i + j] = key; return; }
+      perturb >>= 5;
+      i = (i * 5 + 1 + perturb) & m;
+    }
+  }
+  void resize(size_t minused) {  // set_table_resize
+    size_t ns = 8;
+    while (ns <= minused) ns <<= 1;
+    if (ns == 8 && small) return;
+    std::vector<int32_t> old;
+    old.swap(t);
+    t.assign(ns, EMPTY);
+    mask = ns - 1;
+    small = ns == 8;
+    for (int32_t k : old)
+      if (k != EMPTY) insert_clean(t, mask, k);
+    fill = used;
+  }
+  void add(int32_t key) {  // set_add_entry
+    size_t perturb = (size_t)key, i = (size_t)key & mask;
+    for (;;) {
+      size_t e = i, probes = i + 9 <= mask ? 9 : 0;
+      for (;;) {
+        if (t[e] == EMPTY) {
+          t[e] = key;
+          ++fill;
+          ++used;
+          if (fill * 5 >= mask * 3) resize(used > 50000 ? used * 2 : used * 4);
+          return;
+        }
+        if (t[e] == key) return;
+        if (probes-- == 0) break;
+        ++e;
+      }
+      perturb >>= 5;
+      i = (i * 5 + 1 + perturb) & mask;
+    }
+  }
+  void merge(const PySetEm& o) {  // set_merge with a set argument
+    if (&o == this || o.used == 0) return;
+    if ((fill + o.used) * 5 >= mask * 3) resize((used + o.used) * 2);
+    if (fill == 0 && mask == o.mask) { t = o.t; fill = o.fill; used = o.used; return; }
+    if (fill == 0) {
+      for (int32_t k : o.t)
+        if (k != EMPTY) insert_clean(t, mask, k);
+      fill = used = o.used;
+      return;
+    }
+    for (int32_t k : o.t)
+      if (k != EMPTY) add(k);
+  }
+  PySetEm copy() const { PySetEm s; s.merge(*this); return s; }
+  template <class F> void each(F f) const {
+    for (int32_t k : t)
+      if (k != EMPTY) f(k);
+  }
+};
+
+// A node-induced view's edges (EdgeDataView): nodes in `order`, each node's neighbours in G's
+// adjacency order restricted to the view, every edge reported once from the end met first.
 // complexity_of_hallway (:286-296): D_h * sum(1 / (2 d_e)), D_h = sum(d_e)
 double hallway_complexity(const Graph& G, const std::unordered_map<int64_t, int>& dmap,
-                          const std::unordered_set<int>& nodes) {
+                          const std::unordered_set<int>& nodes, const std::vector<int>& order) {
   long D = 0;
   double s = 0.0;
   bool first = true;
   std::unordered_set<int> seen;
-  std::vector<int> pos;  // the hallway's nodes in G's node order
-  pos.reserve(nodes.size());
-  for (int v : nodes) pos.push_back(G.idx.at(v));
-  std::sort(pos.begin(), pos.end());
-  for (int pv : pos) {
-    const int v = G.order[pv];
+  for (int v : order) {
+    const int pv = G.idx.at(v);
     for (int u : G.adj[pv]) {
       if (!nodes.count(u) || seen.count(u)) continue;
       auto it = dmap.find(Graph::key(v, u));
@@ -130,22 +203,30 @@ double hallway_complexity(const Graph& G, const std::unordered_map<int64_t, int>
   return (double)D * s;
 }
 
-// connected components of G restricted to `keep`, listed by first node in G's node order
+// nx.connected_components(G.copy() minus `removed`): components by first node in G's node order,
+// each as _plain_bfs's insertion sequence (level by level, neighbours in the COPY's adjacency
+// order: G.copy() re-adds edges (u, v) for u in node order, v in adj[u], so a node lists its
+// earlier neighbours by node position first, then its later ones in its own order)
 std::vector<std::vector<int>> components(const Graph& G, const std::unordered_set<int>& removed) {
   std::vector<std::vector<int>> out;
   std::unordered_set<int> seen;
+  std::vector<int> nb;
   for (int v : G.order) {
     if (removed.count(v) || seen.count(v)) continue;
-    std::vector<int> comp{v}, stack{v};
+    std::vector<int> comp{v};
     seen.insert(v);
-    while (!stack.empty()) {
-      const int x = stack.back();
-      stack.pop_back();
-      for (int u : G.adj[G.idx.at(x)]) {
+    for (size_t h = 0; h < comp.size(); ++h) {
+      const int x = comp[h], px = G.idx.at(x);
+      nb.clear();
+      for (int u : G.adj[px])
+        if (G.idx.at(u) < px) nb.push_back(u);
+      std::sort(nb.begin(), nb.end(), [&](int a, int b) { return G.idx.at(a) < G.idx.at(b); });
+      for (int u : G.adj[px])
+        if (G.idx.at(u) > px) nb.push_back(u);
+      for (int u : nb) {
         if (removed.count(u) || seen.count(u)) continue;
         seen.insert(u);
         comp.push_back(u);
-        stack.push_back(u);
       }
     }
     out.push_back(std::move(comp));
@@ -268,21 +349,45 @@ int mcclendon(const uint8_t* g, int32_t H, int32_t W, int32_t sr, int32_t sc, in
   std::unordered_set<int> rm_h(p);
   rm_h.insert(s_p.begin(), s_p.end());
   std::vector<std::unordered_set<int>> hallways;  // index i+1
+  std::vector<std::vector<int>> hall_order;        // the view's node iteration order
+  const size_t nG = G.order.size();
   for (const auto& comp : components(G, rm_h)) {
-    std::unordered_set<int> all(comp.begin(), comp.end());
-    for (int v : comp)
-      for (int u : G.adj[G.idx.at(v)]) {
+    // the sets hold the reference's node ids, cantor_pairing((r, c)) (:7-20), which are also
+    // their hashes; cell ids here are r * W + c
+    auto cid = [&](int v) { const int r = v / W, c = v % W; return (r + c) * (r + c + 1) / 2 + c; };
+    std::unordered_map<int, int> cell_of;
+    PySetEm seen;  // _plain_bfs's `seen`, then set(component_nodes) (:205)
+    for (int v : comp) { seen.add(cid(v)); cell_of[cid(v)] = v; }
+    const PySetEm cset = seen.copy();
+    PySetEm asp;   // adjacent_split_points, filled in cset's order (:208-214)
+    cset.each([&](int k) {
+      for (int u : G.adj[G.idx.at(cell_of.at(k))]) {
         if (!p.count(u)) continue;
-        all.insert(u);
+        asp.add(cid(u));
+        cell_of[cid(u)] = u;
         if (s_p.count(u)) break;  // the reference's break (:213-214)
       }
-    hallways.push_back(std::move(all));
+    });
+    PySetEm all = cset.copy();  // component_nodes.union(adjacent_split_points) (:217)
+    all.merge(asp);
+    PySetEm shown;              // show_nodes(nbunch_iter(all_nodes)).nodes (G.subgraph, :218)
+    all.each([&](int k) { shown.add(k); });
+    std::unordered_set<int> members;
+    std::vector<int> order;
+    shown.each([&](int k) { members.insert(cell_of.at(k)); order.push_back(cell_of.at(k)); });
+    if (2 * shown.used >= nG) {  // FilterAdjacency iterates G's node order then
+      std::sort(order.begin(), order.end(),
+                [&](int a, int b) { return G.idx.at(a) < G.idx.at(b); });
+    }
+    hallways.push_back(std::move(members));
+    hall_order.push_back(std::move(order));
   }
   // get_branches (:223-259): components of G minus non-junction solution points
   std::unordered_set<int> rm_b;
   for (int v : s_nodes)
     if (!p.count(v)) rm_b.insert(v);
   const std::unordered_set<int> h0_nodes(s_nodes.begin(), s_nodes.end());
+  const std::vector<int> h0_order(H0.order);  // solution_branch is a Graph: its node order
   std::vector<char> taken(hallways.size() + 1, 0);
   double prod = 1.0, sum = 0.0;  // p = 1 / s = 0, over branches 1..m then branch 0
   for (const auto& comp : components(G, rm_b)) {
@@ -297,15 +402,15 @@ int mcclendon(const uint8_t* g, int32_t H, int32_t W, int32_t sr, int32_t sc, in
         if (!bset.count(v)) { sub = false; break; }
       if (!sub) continue;
       taken[i] = 1;
-      const double c = i == 0 ? hallway_complexity(H0, d_sol, h0_nodes)
-                              : hallway_complexity(G, dmap, hallways[i - 1]);
+      const double c = i == 0 ? hallway_complexity(H0, d_sol, h0_nodes, h0_order)
+                              : hallway_complexity(G, dmap, hallways[i - 1], hall_order[i - 1]);
       cx = any ? cx + c : 0 + c;  // s = 0; s += ...
       any = true;
     }
     prod *= (any ? cx : 0.0) + 1;  // p *= complexity_of_branch(h) + 1
     sum += any ? cx : 0.0;         // s += complexity_of_branch(b)
   }
-  const double c0 = hallway_complexity(H0, d_sol, h0_nodes);  // branch 0 = [0], last
+  const double c0 = hallway_complexity(H0, d_sol, h0_nodes, h0_order);  // branch 0 = [0], last
   prod *= c0;
   sum += c0;
   if (difficulty) {

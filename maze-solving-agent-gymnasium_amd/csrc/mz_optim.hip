@@ -25,6 +25,7 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <map>
 #include <mutex>
 #include <unordered_map>
 
@@ -259,26 +260,34 @@ hipError_t mz_launch_adamw(float* p, float* m, float* v, const float* const* gra
     sg.g[k] = grads[k];
     sg.off[k + 1] = sg.off[k] + seg_len[k];
   }
-  // the ticket slot of this step counter (assigned on first use; hipGetSymbolAddress is not a
-  // stream operation, so this also works while a graph is being captured)
+  // the ticket slot of this step counter on the current device (assigned on first use; neither
+  // hipGetDevice nor hipGetSymbolAddress is a stream operation, so this also works while a graph
+  // is being captured). The symbol has one instance per device: base and slots are per device.
   static std::mutex mu;
-  static std::unordered_map<const float*, int> slots;
-  static unsigned* base = nullptr;
+  static std::map<std::pair<int, const float*>, int> slots;
+  static std::map<int, int> used;
+  static std::map<int, unsigned*> bases;
   unsigned* ticket;
   {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
     std::lock_guard<std::mutex> lk(mu);
-    if (!base) {
+    auto b = bases.find(dev);
+    if (b == bases.end()) {
       void* p = nullptr;
-      const hipError_t e = hipGetSymbolAddress(&p, HIP_SYMBOL(g_adamw_ticket));
+      e = hipGetSymbolAddress(&p, HIP_SYMBOL(g_adamw_ticket));
       if (e != hipSuccess) return e;
-      base = static_cast<unsigned*>(p);
+      b = bases.emplace(dev, static_cast<unsigned*>(p)).first;
     }
-    auto it = slots.find(step);
+    const auto key = std::make_pair(dev, static_cast<const float*>(step));
+    auto it = slots.find(key);
     if (it == slots.end()) {
-      if ((int)slots.size() >= ADAMW_TICKETS) return hipErrorOutOfMemory;
-      it = slots.emplace(step, (int)slots.size()).first;
+      int& n = used[dev];
+      if (n >= ADAMW_TICKETS) return hipErrorOutOfMemory;
+      it = slots.emplace(key, n++).first;
     }
-    ticket = base + it->second;
+    ticket = b->second + it->second;
   }
   const int64_t n4 = sg.off[nseg] >> 2;
   int blocks = (int)((n4 + MZ_ADAMW_TPB - 1) / MZ_ADAMW_TPB);

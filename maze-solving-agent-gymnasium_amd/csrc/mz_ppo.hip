@@ -119,7 +119,7 @@ __global__ __launch_bounds__(SCAN_T) void k_ppo_scan(MzPpoScan q) {
   int64_t base = *q.pool_fill;  // rows already in the pool
   int64_t rows_acc = 0;
   int fin_acc = 0;
-  unsigned long long n_done = 0, n_win = 0, n_short = 0;
+  unsigned long long n_done = 0, n_win = 0, n_short = 0, n_over = 0;
   for (int c0 = 0; c0 < q.B; c0 += SCAN_T) {
     const int i = c0 + threadIdx.x;
     int len = 0, keep = 0;
@@ -138,6 +138,9 @@ __global__ __launch_bounds__(SCAN_T) void k_ppo_scan(MzPpoScan q) {
           n_short += 1;
         }
         t = 0;
+      } else if (t >= q.L) {
+        n_over += 1;  // the episode outgrew its record buffer: k_ppo_act would stop recording
+        t = q.L - 1;  // keep t inside the buffer; the host raises on stats[3] at the next update
       }
       q.t[i] = t;
     }
@@ -154,28 +157,31 @@ __global__ __launch_bounds__(SCAN_T) void k_ppo_scan(MzPpoScan q) {
     fin_acc += tot_fin;
   }
   // counters: one wave reduction per quantity, added by thread 0
-  __shared__ unsigned long long red[3][SCAN_T / WAVE];
+  __shared__ unsigned long long red[4][SCAN_T / WAVE];
   for (int o = WAVE / 2; o; o >>= 1) {
     n_done += __shfl_xor(n_done, o);
     n_win += __shfl_xor(n_win, o);
     n_short += __shfl_xor(n_short, o);
+    n_over += __shfl_xor(n_over, o);
   }
   if ((threadIdx.x & (WAVE - 1)) == 0) {
     red[0][threadIdx.x / WAVE] = n_done;
     red[1][threadIdx.x / WAVE] = n_win;
     red[2][threadIdx.x / WAVE] = n_short;
+    red[3][threadIdx.x / WAVE] = n_over;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    unsigned long long s[3] = {0, 0, 0};
+    unsigned long long s[4] = {0, 0, 0, 0};
     for (int k = 0; k < SCAN_T / WAVE; ++k)
-      for (int j = 0; j < 3; ++j) s[j] += red[j][k];
+      for (int j = 0; j < 4; ++j) s[j] += red[j][k];
     *q.fin_count = fin_acc;
     *q.pool_fill = base + rows_acc;
     *q.pool_total += rows_acc;
     q.stats[0] += (long long)s[0];  // episodes
     q.stats[1] += (long long)s[1];  // wins
     q.stats[2] += (long long)s[2];  // dropped 1-step episodes
+    q.stats[3] += (long long)s[3];  // record-buffer overflows (never, with L from max_steps' bound)
   }
 }
 

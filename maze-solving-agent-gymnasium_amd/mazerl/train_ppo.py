@@ -46,7 +46,7 @@ def main(argv=None):
     env = make_env(a.envs, dims, toroidal=True, algorithm=a.algo, seed=0x5EED0000 + rank * a.envs,
                    device=dev, done_list=False, reward64=True, window=False, window_bits=True)
     tr = VectorPPOTrainer(env, dev, gamma=a.gamma, batch_size=a.batch, ppo_steps=a.ppo_steps,
-                          pool_size=a.pool, seed=a.seed, use_graph=not a.eager_update,
+                          pool_size=a.pool, seed=a.seed + 7919 * rank, use_graph=not a.eager_update,
                           bank=not a.no_bank,
                           allreduce=GradAllReduce() if world > 1 else None)
     if world > 1:

@@ -5,8 +5,8 @@ Per vector step, with no host round trip (csrc/mz_ppo.hip):
   act      the f32 ActorCriticNet forward (HIP f32 conv stem from the window bits + f32 GEMMs —
            the reference acts in f32, ppo_agent.py:55-68), then mz_ppo_act: softmax, one draw per
            instance, the draw's log-prob, and the record of (obs6, window bits, action, log-prob,
-           value) at the instance's step index t[i] of [B, L] episode buffers in HBM (L = the
-           longest possible episode, (N-1)^2 + 2);
+           value) at the instance's step index t[i] of [B, L] episode buffers in HBM (L = more
+           than the longest possible episode, episode_bound);
   step     the env step (float64 rewards: the reference's Python floats);
   scan     mz_ppo_scan: the reward at t[i], t[i] += 1; for finished episodes the counters, t[i] = 0
            and the list of finished episodes with their pool offsets (instance order);
@@ -29,6 +29,23 @@ import torch.nn.functional as F
 
 from .. import _native as N
 from ..agents.ppo import ActorCriticNet, PPOMinibatchGraph, make_optimizer, optimize_model
+
+
+def episode_bound(max_dim, toroidal):
+    """Record-buffer length L: more than the longest possible episode of any maze up to max_dim.
+    An episode ends at the latest on step max_steps + 1 (base_maze_env.py:205-208), max_steps =
+    ceil(((N-1)^2 - 1) * len / CE) with CE = (N-1) * ((N-1) // 2) - 1 and len = the solution's
+    squares (simple_maze_env.py:52-58), at most the maze's open squares: 2 c - 1 for c cells,
+    c = ((N-1)/2)^2 euclidean and ((N+1)/2)^2 on the torus (generated on the (N+2)^2 bordered grid,
+    so len / CE can exceed 1 there and (N-1)^2 + 2 is not a bound). +2: the float rounding of
+    len / CE and the step that reports truncation."""
+    best = 0
+    for n in range(5, int(max_dim) + 1, 2):
+        c = ((n + 1) // 2) ** 2 if toroidal else ((n - 1) // 2) ** 2
+        ce = (n - 1) * ((n - 1) // 2) - 1
+        a = (n - 1) ** 2 - 1
+        best = max(best, -(-a * (2 * c - 1) // ce) + 2)
+    return best
 
 
 def pool_update(net, opt, cols, coef, batch_size, ppo_steps, allreduce=None, graph=None):
@@ -79,7 +96,7 @@ class VectorPPOTrainer:
         self.seed = int(seed)
         self.counter = 0
         B = env.num_envs
-        self.L = L = (env.max_dim - 1) ** 2 + 2
+        self.L = L = episode_bound(env.max_dim, env.toroidal)
         kw = dict(device=self.device)
         # per-instance episode records [B, L]
         self.b_s6 = torch.zeros(B, L, 6, dtype=torch.float32, **kw)
@@ -90,9 +107,10 @@ class VectorPPOTrainer:
         self.b_r = torch.zeros(B, L, dtype=torch.float64, **kw)
         self.t = torch.zeros(B, dtype=torch.int32, **kw)
         self.act_out = torch.zeros(B, dtype=torch.int32, **kw)
-        # the update pool. Fill bound at an update: < pool_size + the rows two vector steps can
-        # append (an instance appends <= L rows over two steps: an episode that ends at step t-1
-        # leaves a 1-step one at step t); 2 B L leaves room for ranks that fill at different rates
+        # the update pool. Fill bound at an update: < pool_size + the rows the w <= 5 vector steps
+        # between a check's issue and its use can append (an instance appends <= L + w rows over
+        # w steps: one episode of <= L steps ending in the window plus episodes inside it);
+        # 2 B L also leaves room for ranks that fill at different rates
         self.cap = int(pool_capacity or self.pool_size + 2 * B * L)
         C = self.cap
         self.p_s6 = torch.zeros(C, 6, dtype=torch.float32, **kw)
@@ -107,9 +125,12 @@ class VectorPPOTrainer:
         self.fin_count = torch.zeros(1, dtype=torch.int32, **kw)
         self.pool_fill = torch.zeros(1, dtype=torch.int64, **kw)
         self.pool_total = torch.zeros(1, dtype=torch.int64, **kw)
-        self.stats = torch.zeros(3, dtype=torch.int64, **kw)  # episodes, wins, dropped 1-step
+        # episodes, wins, dropped 1-step episodes, record-buffer overflows (an error, _update)
+        self.stats = torch.zeros(4, dtype=torch.int64, **kw)
         self._total_host = torch.zeros(1, dtype=torch.int64, pin_memory=True)
         self._total_ev = None
+        self.calls = 0  # _due() calls; a pool check is issued every check_every of them
+        self.check_every = 1 if allreduce is None else 4
         self.consumed = 0
         self.updates = 0
         self.rows_trained = 0
@@ -171,36 +192,43 @@ class VectorPPOTrainer:
             self.p_ret.data_ptr(), st))
 
     def _due(self):
-        """True when the pool held >= pool_size rows after the PREVIOUS vector step (the host copy
-        of the appended total lands while this step runs; it only grows, so a late look never
-        overshoots). Then issues this step's copy (MIN over the ranks with an all-reduce, so all
-        ranks decide alike)."""
+        """True when the pool held >= pool_size rows when the last check was issued (the host
+        copy of the appended total lands while the next vector step runs; it only grows, so a
+        late look never overshoots). A check is issued every `check_every` vector steps (1 on
+        one rank; with a gradient all-reduce every 4th step, and the copy is the MIN over the
+        ranks, so all ranks decide alike with one small collective per 4 vector steps: the pool's
+        capacity covers the 2 L rows per instance that the delay can add)."""
         due = False
         if self._total_ev is not None:
             self._total_ev.synchronize()
             due = int(self._total_host[0]) - self.consumed >= self.pool_size
-        src = self.pool_total
-        if self.allreduce is not None:
-            import torch.distributed as dist
-            src = self.pool_total.clone()
-            dist.all_reduce(src, op=dist.ReduceOp.MIN)
-        self._total_host.copy_(src, non_blocking=True)
-        if self._total_ev is None:
+            self._total_ev = None
+        if self.calls % self.check_every == 0:
+            src = self.pool_total
+            if self.allreduce is not None:
+                import torch.distributed as dist
+                src = self.pool_total.clone()
+                dist.all_reduce(src, op=dist.ReduceOp.MIN)
+            self._total_host.copy_(src, non_blocking=True)
             self._total_ev = torch.cuda.Event()
-        self._total_ev.record()
+            self._total_ev.record()
+        self.calls += 1
         return due
 
     def _update(self, frac):
-        fill = int(self.pool_fill.item())  # one synchronisation per update
-        if fill > self.cap:
-            raise RuntimeError(f"PPO pool overflow: {fill} rows > capacity {self.cap} "
-                               "(raise pool_capacity)")
         P = self.pool_size
-        k = torch.tensor([fill // P], dtype=torch.int64, device=self.device)
+        k = torch.div(self.pool_fill, P, rounding_mode="floor")
         if self.allreduce is not None:
             import torch.distributed as dist
             dist.all_reduce(k, op=dist.ReduceOp.MIN)
-        k = int(k.item())
+        # one synchronisation per update: the fill, the update count over the ranks, overflows
+        fill, k, over = (int(x) for x in torch.cat([self.pool_fill, k, self.stats[3:4]]).cpu())
+        if over:
+            raise RuntimeError(f"PPO episode records overflowed: {over} episodes reached "
+                               f"L = {self.L} steps (mz_ppo_scan stats[3])")
+        if fill > self.cap:
+            raise RuntimeError(f"PPO pool overflow: {fill} rows > capacity {self.cap} "
+                               "(raise pool_capacity)")
         coef = 1e-2 - (1e-2 - 5e-4) * frac  # ppo_trainer.py:73
         for j in range(k):
             self.rows_trained += pool_update(self.net, self.opt, self._cols(j * P, (j + 1) * P),
@@ -258,7 +286,7 @@ class VectorPPOTrainer:
                 # the appended total the next _due() reads (copied one vector step late)
                 "total_host": int(self._total_host[0]) if self._total_ev is not None else None,
                 "counters": {k: getattr(self, k) for k in ("seed", "counter", "consumed", "updates",
-                                                           "rows_trained")},
+                                                           "rows_trained", "calls")},
                 "env": self.env.state_dict()}
 
     def load_state_dict(self, sd):

@@ -198,43 +198,106 @@ def make_env(num_envs, dims, toroidal=False, algorithm="r-prim", seed=0x5EED0000
     return env
 
 
-def best_of_mazes(num_mazes, dim, algorithm="r-prim", seed=0x7E57, device=None, candidates=6):
+def maze_algorithms(num_mazes, seed, algos=("r-prim", "prim&kill", "dfs")):
+    """NeuralOffPolicyTrainer.test(new=True)'s per-maze `random.choice(OffPolicyTrainer.ALGOS)`
+    (off_policy_trainer.py:231-233), drawn from a Python random.Random(seed): a list of names."""
+    import random
+    rng = random.Random(seed)
+    return [rng.choice(list(algos)) for _ in range(num_mazes)]
+
+
+def best_of_mazes(num_mazes, dim, algorithm="r-prim", seed=0x7E57, device=None, candidates=6,
+                  toroidal=False):
     """The reference's maze selection for new mazes (BaseMazeEnv.generate_maze,
-    base_maze_env.py:78-97): per maze, `candidates` generated mazes, keep the one with the
-    smallest McClendon difficulty (strict <: the first minimum). The candidates are GPU-generated
-    (Philox) and scored on the GPU in one launch (mz_difficulty_batch, one workgroup per maze;
-    host mz_difficulty for the mazes it declines); returns (grids uint8 [n, dim, dim],
-    start_goal [n, 4]) for VectorMazeEnv.load_mazes."""
+    base_maze_env.py:78-97; toroidal: ToroidalMazeEnv.generate_maze, toroidal_maze_env.py:40-54,
+    scored on the bordered maze): per maze, `candidates` generated mazes of the same size and
+    algorithm, keep the one with the smallest McClendon difficulty (strict <: the first minimum).
+    `algorithm` is one name or a per-maze list of names (test(new=True)'s random choice); `dim` is
+    one size or a list (maze k gets dim[k % len], as make_env / evaluate assign them). The
+    candidates are GPU-generated (Philox) and scored on the GPU in one launch (mz_difficulty_batch,
+    one workgroup per maze; host mz_difficulty for the mazes it declines).
+    Returns (grids uint8 [n, D, D], start_goal [n, 4], sizes int [n]) with D = the largest size
+    (a smaller maze in the top-left corner) for evaluate(mazes=...) / load_mazes per size."""
     import numpy as np
     from ..difficulty import difficulty_batch
-    cand = VectorMazeEnv(num_mazes * candidates, dim, enrich=True, device=device,
-                         algorithm=algorithm, seed=seed, done_list=False, pos=False, window=False,
-                         window_bits=False)
-    d = difficulty_batch(cand).reshape(num_mazes, candidates)
+    dims = [dim] if isinstance(dim, int) else list(dim)
+    n, C = int(num_mazes), int(candidates)
+    size_of = [dims[k % len(dims)] for k in range(n)]
+    algo_of = [algorithm] * n if isinstance(algorithm, str) else list(algorithm)
+    if len(algo_of) != n:
+        raise ValueError("one algorithm per maze")
+    cand = VectorMazeEnv(n * C, size_of[0], toroidal=toroidal, enrich=True, device=device,
+                         max_dim=max(dims), algorithm=algo_of[0], seed=seed, done_list=False,
+                         pos=False, window=False, window_bits=False,
+                         generate=len(set(size_of)) == 1 and len(set(algo_of)) == 1)
+    if len(set(size_of)) > 1 or len(set(algo_of)) > 1:
+        groups = {}
+        for k in range(n):
+            groups.setdefault((size_of[k], algo_of[k]), []).extend(range(k * C, k * C + C))
+        for (sz, al), ids in sorted(groups.items()):
+            cand.generate(env_ids=torch.tensor(ids, dtype=torch.int32, device=cand.device),
+                          algorithm=al, dim=sz, seed=seed)
+    d = difficulty_batch(cand).reshape(n, C)
     pick = d.argmin(axis=1)  # first minimum (NaN-free: a log domain error raises on the host)
-    grids = np.zeros((num_mazes, dim, dim), np.uint8)
-    sg = np.zeros((num_mazes, 4), np.int32)
-    for k in range(num_mazes):
-        i = k * candidates + int(pick[k])
+    D = max(dims)
+    grids = np.zeros((n, D, D), np.uint8)
+    sg = np.zeros((n, 4), np.int32)
+    for k in range(n):
+        i = k * C + int(pick[k])
         q = cand.query(i)
-        grids[k] = cand.grid(i)
+        g = cand.grid(i)
+        grids[k, :g.shape[0], :g.shape[1]] = g
         sg[k] = (q["start_r"], q["start_c"], q["goal_r"], q["goal_c"])
     cand.close()
-    return grids, sg
+    return grids, sg, np.asarray(size_of, np.int32)
+
+
+def load_selected(env, mazes):
+    """Load best_of_mazes' (grids, start_goal[, sizes]) into env instances 0..n-1, one
+    mz_load_mazes call per size."""
+    import numpy as np
+    grids, sg = mazes[0], mazes[1]
+    sizes = mazes[2] if len(mazes) > 2 else np.full(len(grids), grids.shape[1], np.int32)
+    for sz in sorted(set(int(x) for x in sizes)):
+        ids = np.nonzero(sizes == sz)[0].astype(np.int32)
+        env.load_mazes(np.ascontiguousarray(grids[ids, :sz, :sz]), sg[ids], env_ids=ids)
+    env.reset()
+
+
+def steps_done_epsilon(learner, num_mazes):
+    """The reference's test-time epsilon (test() acts through DQNAgent.get_action, dqn_agent.py:
+    104-119: eps = eps_final + (eps_start - eps_final) * exp(-steps_done / decay), steps_done += 1
+    per action, never reset during test): a callable k -> per-maze epsilon after k actions, each
+    evaluation maze k continuing the steps_done (and epsilon decay) of training instance
+    k mod B. Instances run their test episodes side by side here; the reference plays them one
+    after another on one counter."""
+    sd0 = learner.steps_done.detach().float()
+    B = sd0.numel()
+    idx = torch.arange(num_mazes, device=sd0.device) % B
+    sd0 = sd0[idx]
+    dec = learner.eps_decay
+    dec = dec[idx] if torch.is_tensor(dec) else torch.full_like(sd0, float(dec))
+    e0, e1 = float(learner.eps_start), float(learner.eps_final)
+
+    def eps(k):
+        return e1 + (e0 - e1) * torch.exp(-(sd0 + float(k)) / dec)
+    eps.start_mean = float((e1 + (e0 - e1) * torch.exp(-sd0 / dec)).mean())
+    return eps
 
 
 @torch.no_grad()
 def evaluate(learner, num_mazes, dim, algorithm="r-prim", seed=0x7E57, eps=0.0, toroidal=False,
              device=None, max_vector_steps=None, mazes=None):
     """Fraction of `num_mazes` fresh mazes solved in one episode (terminated before truncation).
-    `dim` may be a list of sizes (instance i gets dim[i % len]). `mazes` = (grids, start_goal)
-    to play instead of generated ones (e.g. best_of_mazes: the reference's best-of-6 selection)."""
+    `dim` may be a list of sizes (instance i gets dim[i % len]). `mazes` = best_of_mazes' output
+    to play instead of generated ones (the reference's best-of-6 selection). `eps` is a number or
+    a callable k -> per-maze epsilon tensor for the k-th action (steps_done_epsilon)."""
     bits = getattr(learner, "supports_bits", False)
-    env = make_env(num_mazes, dim, toroidal=toroidal, algorithm=algorithm, seed=seed,
+    algo0 = algorithm if isinstance(algorithm, str) else "r-prim"
+    env = make_env(num_mazes, dim, toroidal=toroidal, algorithm=algo0, seed=seed,
                    device=device, done_list=False, pos=False, window=not bits, window_bits=True)
     if mazes is not None:
-        env.load_mazes(*mazes)
-        env.reset()
+        load_selected(env, mazes)
     dim = max(dim) if not isinstance(dim, int) else dim
     finished = torch.zeros(num_mazes, dtype=torch.bool, device=env.device)
     won = torch.zeros(num_mazes, dtype=torch.bool, device=env.device)
@@ -242,7 +305,7 @@ def evaluate(learner, num_mazes, dim, algorithm="r-prim", seed=0x7E57, eps=0.0, 
     k = 0
     while k < limit:
         greedy = learner.greedy(env.obs6, env.window, env.window_bits)
-        acts = env.act(eps=eps, greedy=greedy, seed=seed, counter=k)
+        acts = env.act(eps=eps(k) if callable(eps) else eps, greedy=greedy, seed=seed, counter=k)
         acts = torch.where(finished, torch.full_like(acts, -1), acts)
         env.step(acts)
         term = env.terminated.bool()

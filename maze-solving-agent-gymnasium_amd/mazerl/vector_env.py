@@ -23,6 +23,12 @@ def _ptr(t):
     return None if t is None else t.data_ptr()
 
 
+def bank_seed(env_seed):
+    """The maze bank's Philox seed for an env seeded `env_seed` (0xBA4C0000 for the default env
+    seed; distinct per shard because env seeds are 0x5EED0000 + the shard's first instance id)."""
+    return (0xBA4C0000 + (int(env_seed) - 0x5EED0000) * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+
+
 class VectorMazeEnv:
     def __init__(self, num_envs, maze_dim, toroidal=False, enrich=True, device=None,
                  max_dim=None, algorithm="r-prim", seed=0x5EED0000, generate=True,
@@ -242,14 +248,18 @@ class VectorMazeEnv:
 
     # ---------------------------------------------------------------------------------------
     # Maze bank: winners' new mazes are generated ahead of time, in bulk, on a side stream.
-    def enable_bank(self, slots=None, swap_every=8, algorithms=None, seed=0xBA4C0000, dims=None):
+    def enable_bank(self, slots=None, swap_every=8, algorithms=None, seed=None, dims=None):
         """Two banks of `slots` mazes per algorithm (size maze_dim, or per size of `dims` — the
         variable-size envs): reset_done(regen_won=True) consumes the active one; every
         `swap_every` such calls the banks swap and the retired one is refilled on a side stream
         (ordered after the launches that consumed it; the main stream waits for a refill only
-        when that bank comes back). Default slots: B / 8 (split over the sizes, >= 16 each)."""
+        when that bank comes back). Default slots: B / 8 (split over the sizes, >= 16 each).
+        Default seed: derived from the env's seed, which carries the shard's first global
+        instance id, so the ranks of a data-parallel run draw different replacement mazes."""
         if self._bank is not None:
             return
+        if seed is None:
+            seed = bank_seed(self.seed)
         dims = [self.maze_dim] if dims is None else sorted({int(d) for d in dims})
         K = int(slots or max(64 // len(dims) if len(dims) > 1 else 64,
                              self.num_envs // 8 // len(dims), 16))
@@ -339,6 +349,11 @@ class VectorMazeEnv:
             raise ValueError("maze bank mismatch: call enable_bank() with the saved geometry "
                              "(or not at all) before load_state_dict()")
         blob = sd["device_state"].to(device=self.device, dtype=torch.uint8).contiguous()
+        if self._bank is not None:  # a refill still running on the side stream would overwrite
+            main = torch.cuda.current_stream(self.device)  # the loaded bank slots
+            for ev in self._bank["ready"]:
+                if ev is not None:
+                    main.wait_event(ev)
         N.check(self.lib.mz_state_load(self._h, blob.data_ptr(), blob.numel(), self._stream()))
         for k, v in sd["outputs"].items():
             dst = getattr(self, k, None)

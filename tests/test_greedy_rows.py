@@ -126,7 +126,8 @@ def test_best_of_mazes_picks_the_easiest_candidate():
     from mazerl.difficulty import maze_difficulty
     from mazerl.trainers.vector_trainer import best_of_mazes
     n, dim, c = 5, 21, 6
-    grids, sg = best_of_mazes(n, dim, "dfs", seed=77, device="cuda:0", candidates=c)
+    grids, sg, sizes = best_of_mazes(n, dim, "dfs", seed=77, device="cuda:0", candidates=c)
+    assert sizes.tolist() == [dim] * n
     ref = VectorMazeEnv(n * c, dim, enrich=True, device="cuda:0", algorithm="dfs", seed=77)
     for k in range(n):
         ds = []
@@ -144,6 +145,49 @@ def test_best_of_mazes_picks_the_easiest_candidate():
     env.reset()
     for k in range(n):
         assert np.array_equal(env.grid(k), grids[k])
+    env.close()
+
+
+def test_best_of_mazes_mixed_algorithms_toroidal_variable_sizes():
+    """test(new=True)'s per-maze random algorithm (off_policy_trainer.py:231-233) and the toroidal
+    variable-size envs (toroidal_maze_env.py:40-54): each maze's 6 candidates share its size and
+    algorithm; the pick is the first minimum of the difficulty of the bordered maze (the host
+    restatement here, candidates regenerated one by one); evaluate() loads and plays them."""
+    import numpy as np
+    import torch
+    from mazerl import VectorMazeEnv
+    from mazerl.difficulty import toroidal_difficulty
+    from mazerl.trainers.vector_trainer import best_of_mazes, load_selected, maze_algorithms
+    n, c, dims = 6, 6, [17, 21, 25]
+    algos = maze_algorithms(n, seed=5)
+    assert algos == maze_algorithms(n, seed=5) and set(algos) <= {"r-prim", "prim&kill", "dfs"}
+    grids, sg, sizes = best_of_mazes(n, dims, algos, seed=91, device="cuda:0", candidates=c,
+                                     toroidal=True)
+    assert sizes.tolist() == [dims[k % 3] for k in range(n)]
+    ref = VectorMazeEnv(n * c, 17, toroidal=True, enrich=True, device="cuda:0", max_dim=25,
+                        generate=False, done_list=False)
+    for k in range(n):
+        ds = []
+        for j in range(c):
+            i = k * c + j
+            ref.generate(env_ids=torch.tensor([i], dtype=torch.int32, device="cuda:0"),
+                         algorithm=algos[k], dim=int(sizes[k]), seed=91)
+            q = ref.query(i)
+            assert q["n"] == sizes[k]
+            ds.append(toroidal_difficulty(ref.grid(i), (q["start_r"], q["start_c"]),
+                                          (q["goal_r"], q["goal_c"])))
+        j = int(np.argmin(ds))
+        q = ref.query(k * c + j)
+        m = int(sizes[k])
+        assert np.array_equal(grids[k, :m, :m], ref.grid(k * c + j))
+        assert tuple(sg[k]) == (q["start_r"], q["start_c"], q["goal_r"], q["goal_c"])
+    ref.close()
+    env = VectorMazeEnv(n, 17, toroidal=True, enrich=True, device="cuda:0", max_dim=25,
+                        generate=False, done_list=False)
+    load_selected(env, (grids, sg, sizes))
+    for k in range(n):
+        m = int(sizes[k])
+        assert np.array_equal(env.grid(k), grids[k, :m, :m])
     env.close()
 
 

@@ -42,10 +42,9 @@ def test_native_complexity_matches_reference(fx):
         d, c = C.c_double(), C.c_double()
         N.check(L.mz_maze_complexity(g.ctypes.data, g.shape[0], g.shape[1], *m["start"], *m["goal"],
                                      C.byref(d), C.byref(c)))
-        # bit-exact on 119 of the 120 mazes; the float sums follow networkx's order, the one
-        # remaining value differs in the last bit (as mz_difficulty, tests/test_difficulty.py)
-        assert abs(c.value - ref["complexity"]) <= math.ulp(ref["complexity"]), (m["n"], m["seed"])
-        assert abs(d.value - ref["difficulty"]) <= math.ulp(ref["difficulty"]), (m["n"], m["seed"])
+        # bit-exact: the hallway sums follow the networkx subgraph views' set order
+        assert c.value == ref["complexity"], (m["n"], m["seed"])
+        assert d.value == ref["difficulty"], (m["n"], m["seed"])
         checked += 1
     assert checked >= 100
 

@@ -242,7 +242,7 @@ def test_episode_finish_matches_reference_returns_advantages():
     fill = check(first, 0)
     assert int(tr.pool_fill) == fill == sum(n for n in lens if n > 1) == int(tr.pool_total)
     wins = sum(float(fx["ppo.pool.rewards"][off[k + 1] - 1]) == 1.0 for k in range(E))
-    assert tr.stats.tolist() == [E, wins, sum(n == 1 for n in lens)]
+    assert tr.stats.tolist() == [E, wins, sum(n == 1 for n in lens), 0]
     second = [(3, 6), (0, 9), (7, 4), (10, 2)]  # instance order differs from fixture order
     round_(second)
     end = check(sorted(second), fill)
