@@ -248,7 +248,8 @@ def config_legs(a, dev, rank=0, world=1):
     out = {}
     legs = [x for x in a.config_legs.split(",") if x]
     if "cfg4" in legs:
-        log("config 4 leg (DDQN, mixed 81x81)")
+        if rank == 0:
+            log("config 4 leg (DDQN, mixed 81x81)")
         B, dim = a.cfg4_envs, 81
         algo = ((torch.arange(B) + rank * B) % 3).to(torch.uint8)
         env = VectorMazeEnv(B, dim, enrich=True, device=dev, algorithm=algo,
@@ -282,7 +283,8 @@ def config_legs(a, dev, rank=0, world=1):
         out["cfg4"] = rec
         del tr, L
     if "cfg5" in legs:
-        log("config 5 leg (PPO, toroidal 17..79)")
+        if rank == 0:
+            log("config 5 leg (PPO, toroidal 17..79)")
         B = a.cfg5_envs
         dims = list(range(17, 80, 2))
         env = make_env(B, dims, toroidal=True, algorithm="r-prim", seed=0x5EED0000 + rank * B,
@@ -377,19 +379,30 @@ def _free_port():
 
 def launch(n, argv, timeout, environ=None, script=None):
     """Start N child processes of this script (subprocess, never exec: the parent has not touched
-    the GPU and stays a plain supervisor), rank 0's stdout inherited (its JSON line is the
-    output), the other ranks' stdout on stderr. If any rank fails or the deadline passes, every
-    rank's process group is killed and the exit status is non-zero. Returns the exit status."""
+    the GPU and stays a plain supervisor). Rank 0's stdout is relayed: JSON object lines to stdout
+    (the bench line), anything else (e.g. the communication library's own banners) to stderr; the
+    other ranks' stdout goes to stderr. If any rank fails or the deadline passes, every rank's
+    process group is killed and the exit status is non-zero. Returns the exit status."""
     import signal
     import subprocess
+    import threading
     environ = dict(os.environ if environ is None else environ)
     port = int(environ.get("MASTER_PORT") or _free_port())
     script = script or os.path.abspath(__file__)
     procs = []
     for r, env in enumerate(launch_plan(n, environ, port)):
         procs.append(subprocess.Popen([sys.executable, "-u", script] + list(argv), env=env,
-                                      stdout=None if r == 0 else sys.stderr.fileno(),
-                                      start_new_session=True))
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(),
+                                      start_new_session=True, text=True))
+
+    def relay(stream):
+        for line in stream:
+            dst = sys.stdout if line.lstrip().startswith("{") else sys.stderr
+            dst.write(line)
+            dst.flush()
+
+    reader = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
+    reader.start()
     deadline = time.monotonic() + timeout
     rc = 0
     while True:
@@ -418,6 +431,7 @@ def launch(n, argv, timeout, environ=None, script=None):
             t0 = time.monotonic()
             while any(p.poll() is None for p in procs) and time.monotonic() - t0 < wait:
                 time.sleep(0.1)
+    reader.join(timeout=5.0)
     return rc
 
 

@@ -366,12 +366,16 @@ int mz_maze_complexity(const uint8_t* grid_host, int32_t h, int32_t w, int32_t s
  * base_maze_env.py:84-95, maze_complexity_evaluation.py:38-329). For the listed instances
  * (env_ids_dev NULL = all B): out_dev [n][2] float64 = {prod, sum}, the reference's product
  * prod_b (C_b + 1) * C_0 and sum sum_b C_b + C_0 BEFORE math.log (the caller takes the log with
- * the C library, as the reference: difficulty = log(prod), complexity = log(sum)); status_dev
- * [n] int32: 0 ok, 1 not a perfect maze (cycles / unreachable squares), 2 outside the kernel's
- * cases (open border squares, straight goal square, all solution points junctions, more points
- * than the LDS plan holds), 3 invalid (start == goal, bad id, log domain), 4 toroidal — the caller
- * computes every nonzero-status maze with mz_difficulty. Asynchronous on `stream`.
- * Returns MZ_EINVAL_SHAPE when the handle's pitch exceeds the kernel's LDS plan (P > 92). */
+ * the C library, as the reference: difficulty = log(prod), complexity = log(sum)), each hallway
+ * summed in the order networkx's subgraph view iterates its CPython set (bit-exact with the
+ * reference); a toroidal handle's maze is scored as its bordered (N + 2)^2 maze with start / goal
+ * shifted by +1, as the reference scores it (off_policy_trainer.py:194-196). status_dev [n]
+ * int32: 0 ok, 1 not a perfect maze (cycles / unreachable squares), 2 outside the kernel's cases
+ * (open border squares, straight goal square, all solution points junctions, more points than
+ * the LDS plan holds, a hallway of more than 63 view nodes), 3 invalid (start == goal, bad id,
+ * log domain) — the caller computes every nonzero-status maze with mz_difficulty (toroidal: on
+ * the bordered grid). Asynchronous on `stream`. Returns MZ_EINVAL_SHAPE when the evaluated grid's
+ * pitch exceeds the kernel's LDS plan (P > 92; toroidal P > 85). */
 int mz_difficulty_batch(mz_handle* h, const int32_t* env_ids_dev, int32_t n, double* out_dev,
                         int32_t* status_dev, void* stream);
 

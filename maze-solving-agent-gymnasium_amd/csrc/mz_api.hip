@@ -782,7 +782,7 @@ int mz_difficulty_batch(mz_handle* h, const int32_t* env_ids_dev, int32_t n, dou
   if (!env_ids_dev) n = h->d.B;
   if (n < 0 || (!env_ids_dev && n > h->d.B)) return fail(MZ_EINVAL, "n out of range");
   int mm = 0;
-  if (mz_mcclendon_lds(h->d.P, &mm) > 160 * 1024)
+  if (mz_mcclendon_lds(h->d.P, h->d.toroidal != 0, &mm) > 160 * 1024)
     return fail(MZ_EINVAL_SHAPE, "maze pitch beyond the difficulty kernel's LDS plan");
   DeviceGuard g(h->cfg.device);
   MZ_HIP(mz_launch_mcclendon(h->d, env_ids_dev, n, out_dev, status_dev,

@@ -9,7 +9,7 @@
 #include "mz_common.h"
 
 // out[i] = {prod, sum} of instance ids[i] (ids null: i); status[i] 0 ok, 1 not a tree, 2 outside
-// the kernel's cases (host restatement), 3 invalid, 4 toroidal
-size_t mz_mcclendon_lds(int P, int* mm);
+// the kernel's cases (host restatement), 3 invalid. Toroidal handles: the bordered maze.
+size_t mz_mcclendon_lds(int P, bool toroidal, int* mm);
 hipError_t mz_launch_mcclendon(const MzDev& d, const int32_t* ids, int n, double* out,
                                int32_t* status, hipStream_t s);

@@ -1,4 +1,4 @@
-// mz_mcclendon.hip — McClendon maze difficulty on the GPU, one 256-thread workgroup per maze.
+// mz_mcclendon.hip — McClendon maze difficulty on the GPU, one 1,024-thread workgroup per maze.
 //
 // The reference (lib/maze_difficulty_evaluation/maze_complexity_evaluation.py:38-329) builds a
 // networkx graph G of "points" (turns and junctions along the solution path and along the path
@@ -22,11 +22,23 @@
 //               links), numbered by their first node in node order as nx.connected_components
 //               yields them; the junctions a hallway takes follow the reference's loop and its
 //               break (:210-214) per node; each hallway lies in exactly one branch;
-//   sums        every hallway's edge terms sorted into the subgraph's edge order and summed
-//               serially, the branch sums and the final product in the reference's order.
+//   sums        every hallway's edge terms in the order networkx 3.4's subgraph view reports them
+//               (G.subgraph(all_nodes), :217-218, read by get_edge_attributes :283-295): the
+//               view iterates show_nodes' CPython set when it holds fewer than half of G's nodes
+//               (FilterAdjacency), so one wave per hallway rebuilds the sets the reference builds
+//               — _plain_bfs's `seen` (BFS in the adjacency order of G.copy()), set(component),
+//               adjacent_split_points, the union, show_nodes' set — as CPython 3.10 set tables
+//               held in the wave's registers (WSet: one slot per lane and register, <= 128
+//               slots), then walks the final table and sums in that order; the branch sums and
+//               the final product follow the reference's order.
+// Toroidal handles are scored as the reference scores them: the bordered (N + 2)^2 maze, the
+// crop inside a wall ring with start / goal shifted by +1 (gen_maze_no_border, maze_generation.
+// py:49-51; off_policy_trainer.py:194-196) — a perfect maze whose distance field to the goal comes
+// from a bit-parallel BFS over 128-bit rows here (the handle's cell words hold torus distances).
 // Output per maze: the product and the sum before the log (prod_b (C_b + 1) * C_0 and
 // sum_b C_b + C_0); the caller takes math.log (glibc, as the reference) of both. Non-tree mazes
-// and mazes beyond the LDS budget report a status and are left to the host restatement.
+// and mazes beyond the LDS / register budgets report a status and are left to the host
+// restatement (csrc/mz_difficulty.hip, the same orders).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -36,7 +48,10 @@
 
 namespace {
 
-constexpr int T = 256;
+#ifndef MZ_MC_T
+#define MZ_MC_T 1024  // 16 waves: hallways in flight per CU (256: 28 -> 12 ms per 6,000 81x81 mazes)
+#endif
+constexpr int T = MZ_MC_T;  // threads per maze workgroup
 constexpr int WAVE = 64;
 constexpr uint16_t NONE = 0xFFFF;
 constexpr uint8_t F_OPEN = 1, F_POINT = 2, F_SOL = 4, F_JUNC = 8, F_DEAD = 16;
@@ -91,11 +106,139 @@ __device__ inline int block_excl(int v, int* wsum, int* total) {
 __device__ inline int dir_dr(int k) { return k == 0 ? -1 : (k == 1 ? 1 : 0); }
 __device__ inline int dir_dc(int k) { return k == 2 ? -1 : (k == 3 ? 1 : 0); }
 
+// ---- CPython 3.10 set table for int keys (hash(n) == n), held by one wave -------------------
+// Objects/setobject.c: probe i = hash & mask, then the 9 following slots when i + 9 <= mask, then
+// perturb >>= 5, i = (5 i + 1 + perturb) & mask; add() inserts at the first empty slot and resizes
+// to used * 4 when fill * 5 >= mask * 3; a resize re-inserts in old table order (insert_clean);
+// set(s) / s.union(t) / s.update(t) merge (set_merge); no deletions, so no dummies (oracle/
+// pyset.py restates the same and is checked against the interpreter). Slot j lives in lane j & 63
+// of v0 (j < 64) or v1; a slot holds key << 16 | node; occupancy is a wave-uniform 128-bit mask.
+constexpr uint32_t WS_EMPTY = 0xFFFFFFFFu;
+struct WSet {
+  uint32_t v0, v1;
+  uint64_t o0, o1;
+  int mask, fill, used;
+  bool small;  // still the 8-slot smalltable
+};
+__device__ inline void ws_init(WSet& s) {
+  s.v0 = s.v1 = WS_EMPTY;
+  s.o0 = s.o1 = 0;
+  s.mask = 7;
+  s.fill = s.used = 0;
+  s.small = true;
+}
+__device__ inline bool ws_occ(const WSet& s, int j) {
+  return j < 64 ? ((s.o0 >> j) & 1) : ((s.o1 >> (j - 64)) & 1);
+}
+// the first empty slot of key's probe sequence (the key is known to be absent)
+__device__ inline int ws_free_slot(const WSet& s, uint32_t key) {
+  uint32_t perturb = key;
+  int i = (int)(key & (uint32_t)s.mask);
+  for (;;) {
+    const int last = i + 9 <= s.mask ? i + 9 : i;
+    for (int j = i; j <= last; ++j)
+      if (!ws_occ(s, j)) return j;
+    perturb >>= 5;
+    i = (int)(((uint32_t)i * 5u + 1u + perturb) & (uint32_t)s.mask);
+  }
+}
+__device__ inline void ws_put(WSet& s, int j, uint32_t val) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  if (j < 64) {
+    if (lane == j) s.v0 = val;
+    s.o0 |= 1ull << j;
+  } else {
+    if (lane == j - 64) s.v1 = val;
+    s.o1 |= 1ull << (j - 64);
+  }
+}
+__device__ inline uint32_t ws_get(const WSet& s, int j) {
+  return j < 64 ? (uint32_t)__shfl((int)s.v0, j) : (uint32_t)__shfl((int)s.v1, j - 64);
+}
+// next occupied slot after j (table order), -1 at the end
+__device__ inline int ws_next(const WSet& s, int j) {
+  ++j;
+  if (j < 64) {
+    const uint64_t m = j ? s.o0 & ~((1ull << j) - 1) : s.o0;
+    if (m) return __ffsll((long long)m) - 1;
+    j = 64;
+  }
+  if (j < 128) {
+    const int b = j - 64;
+    const uint64_t m = b ? s.o1 & ~((1ull << b) - 1) : s.o1;
+    if (m) return 64 + __ffsll((long long)m) - 1;
+  }
+  return -1;
+}
+// slot of key, -1 if absent
+__device__ inline int ws_find(const WSet& s, uint32_t key) {
+  const uint64_t m0 = __ballot((s.v0 >> 16) == key), m1 = __ballot((s.v1 >> 16) == key);
+  if (m0) return __ffsll((long long)m0) - 1;
+  if (m1) return 64 + __ffsll((long long)m1) - 1;
+  return -1;
+}
+// set_table_resize; false beyond the wave's 128 slots
+__device__ inline bool ws_resize(WSet& s, int minused) {
+  int ns = 8;
+  while (ns <= minused) ns <<= 1;
+  if (ns == 8 && s.small) return true;
+  if (ns > 128) return false;
+  WSet n;
+  ws_init(n);
+  n.mask = ns - 1;
+  n.small = ns == 8;
+  for (int j = ws_next(s, -1); j >= 0; j = ws_next(s, j)) {
+    const uint32_t v = ws_get(s, j);
+    ws_put(n, ws_free_slot(n, v >> 16), v);
+  }
+  n.fill = n.used = s.used;
+  s = n;
+  return true;
+}
+// set_add_entry: 1 added, 0 present, -1 beyond the budget
+__device__ inline int ws_add(WSet& s, uint32_t key, uint32_t node) {
+  if (ws_find(s, key) >= 0) return 0;
+  ws_put(s, ws_free_slot(s, key), (key << 16) | node);
+  s.fill += 1;
+  s.used += 1;
+  if (s.fill * 5 >= s.mask * 3 && !ws_resize(s, s.used > 50000 ? s.used * 2 : s.used * 4)) return -1;
+  return 1;
+}
+// dst = set(src) (set_merge into an empty set)
+__device__ inline bool ws_copy(WSet& dst, const WSet& src) {
+  ws_init(dst);
+  if (src.used == 0) return true;
+  if (src.used * 5 >= dst.mask * 3 && !ws_resize(dst, src.used * 2)) return false;
+  if (dst.mask == src.mask) {
+    dst = src;
+    return true;
+  }
+  for (int j = ws_next(src, -1); j >= 0; j = ws_next(src, j)) {
+    const uint32_t v = ws_get(src, j);
+    ws_put(dst, ws_free_slot(dst, v >> 16), v);
+  }
+  dst.fill = dst.used = src.used;
+  return true;
+}
+// dst.update(src) for a non-empty dst (set_merge: one resize first, then set_add_entry)
+__device__ inline bool ws_merge(WSet& dst, const WSet& src) {
+  if (src.used == 0) return true;
+  if ((dst.fill + src.used) * 5 >= dst.mask * 3 && !ws_resize(dst, (dst.used + src.used) * 2))
+    return false;
+  for (int j = ws_next(src, -1); j >= 0; j = ws_next(src, j)) {
+    const uint32_t v = ws_get(src, j);
+    if (ws_add(dst, v >> 16, v & 0xFFFFu) < 0) return false;
+  }
+  return true;
+}
+
+typedef unsigned __int128 u128;
+
 __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, int n, int MM,
                                                  double* out, int32_t* status) {
   extern __shared__ __align__(16) unsigned char lds[];
   __shared__ int wsum[T / WAVE];
-  __shared__ int s_bad, s_nsol, s_noff, s_nent, s_open, s_edges, s_Hn, s_Bn;
+  __shared__ int s_bad, s_nsol, s_noff, s_open, s_edges, s_Hn, s_Bn;
   const int i = blockIdx.x;
   if (i >= n) return;
   const int e = ids ? ids[i] : i;
@@ -103,21 +246,36 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
     if (threadIdx.x == 0) { out[2 * i] = out[2 * i + 1] = 0.0; status[i] = code; }
   };
   if (e < 0 || e >= d.B) { fail(3); return; }
-  if (d.toroidal) { fail(4); return; }  // the reference's evaluation is euclidean
-  const int P = d.P, NNP = P * P;
+  const bool tor = d.toroidal;
+  const int P = d.P, Pb = tor ? P + 2 : P, NNP = Pb * Pb;
   const uint32_t m0 = d.meta0[e], m1 = d.meta1[e];
-  const int N = m0 & 0xFF, sr = (m0 >> 16) & 0xFF, sc = m0 >> 24;
-  const int gr = m1 & 0xFF, gc = (m1 >> 8) & 0xFF;
+  // the evaluated grid: the maze itself, or a toroidal crop inside its wall ring (+1 shift)
+  const int Nm = m0 & 0xFF, N = tor ? Nm + 2 : Nm, o = tor ? 1 : 0;
+  const int sr = ((m0 >> 16) & 0xFF) + o, sc = (m0 >> 24) + o;
+  const int gr = (m1 & 0xFF) + o, gc = ((m1 >> 8) & 0xFF) + o;
   const int NN = N * N, start = sr * N + sc, goal = gr * N + gc;
-  const uint32_t* cw = d.cells + (size_t)e * NNP;
+  const uint32_t* cw = d.cells + (size_t)e * P * P;
   auto cell = [&](int q) -> uint32_t { const int r = q / N; return cw[r * P + (q - r * N)]; };
+  auto sq_open = [&](int q) -> bool {
+    if (!tor) return (cell(q) & MZ_CELL_OPEN) != 0;
+    const int r = q / N, c = q - r * N;
+    return r >= 1 && r <= Nm && c >= 1 && c <= Nm && (cw[(r - 1) * P + (c - 1)] & MZ_CELL_OPEN);
+  };
 
   // ---- LDS: square region (phase 1) aliased by the node-phase arrays (phase 2) ---------------
   uint16_t* gp = reinterpret_cast<uint16_t*>(lds);                 // [NNP] parent toward the goal
   uint16_t* pos = gp + NNP;                                          // [NNP] node position
   uint32_t* fst = reinterpret_cast<uint32_t*>(pos + NNP);          // [NNP] first dead-end rank
   uint8_t* fl = reinterpret_cast<uint8_t*>(fst + NNP);              // [NNP] flags
-  const size_t sq_bytes = ((size_t)NNP * 9 + 16 + 15) & ~(size_t)15, ph2_bytes = (size_t)MM * 36;
+  // toroidal: the bordered grid's distance field to the goal and the BFS rows
+  const size_t tor_off = ((size_t)NNP * 9 + 16 + 15) & ~(size_t)15;
+  uint16_t* tdist = reinterpret_cast<uint16_t*>(lds + tor_off);     // [NNP]
+  u128* rO = reinterpret_cast<u128*>(lds + tor_off + (((size_t)NNP * 2 + 15) & ~(size_t)15));
+  u128* rV = rO + Pb;
+  u128* rF = rV + Pb;                                                // [2][Pb] frontiers
+  const size_t sq_bytes = tor ? tor_off + (((size_t)NNP * 2 + 15) & ~(size_t)15) + 64 * (size_t)Pb
+                              : tor_off,
+               ph2_bytes = (size_t)MM * 36;
   unsigned char* nb = lds + (sq_bytes > ph2_bytes ? sq_bytes : ph2_bytes);  // node region
   uint64_t* keys = reinterpret_cast<uint64_t*>(nb);                  // [MM] sort buffer
   uint16_t* nsq = reinterpret_cast<uint16_t*>(keys + MM);            // [MM] node -> square
@@ -141,23 +299,71 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
   double* Cb = Ch + MM;                                              // [MM] branch complexity
 
   if (threadIdx.x == 0) {
-    s_bad = 0; s_nsol = 0; s_noff = 0; s_nent = 0; s_open = 0; s_edges = 0; s_Hn = 0; s_Bn = 0;
+    s_bad = 0; s_nsol = 0; s_noff = 0; s_open = 0; s_edges = 0; s_Hn = 0; s_Bn = 0;
   }
-  if (N < 3 || N > P || start == goal) { fail(3); return; }
+  if (N < 3 || N > Pb || start == goal) { fail(3); return; }
+  if (tor && N > 128) { fail(2); return; }  // the BFS rows are 128-bit
   // ---- A. squares: open, parent toward the goal, points, junctions -------------------------
   for (int q = threadIdx.x; q < NN; q += T) {
     gp[q] = NONE;
     pos[q] = NONE;
     fst[q] = 0xFFFFFFFFu;
-    fl[q] = (cell(q) & MZ_CELL_OPEN) ? F_OPEN : 0;
+    fl[q] = sq_open(q) ? F_OPEN : 0;
   }
+  if (tor) {
+    // distances to the goal on the bordered grid: BFS over 128-bit rows (a level = shift / or /
+    // and-not of the frontier rows), one row per thread, no wrap (the ring is wall)
+    for (int q = threadIdx.x; q < NN; q += T) tdist[q] = 0xFFFF;
+    for (int y = threadIdx.x; y < N; y += T) {
+      u128 ob = 0;
+      for (int x = 0; x < N; ++x)
+        if (sq_open(y * N + x)) ob |= (u128)1 << x;
+      const u128 g = y == gr ? (u128)1 << gc : (u128)0;
+      rO[y] = ob;
+      rV[y] = g;
+      rF[y] = g;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) tdist[goal] = 0;
+    int cur = 0;
+    for (int level = 1;; ++level) {
+      const u128* Fc = rF + cur * Pb;
+      u128* Fn = rF + (cur ^ 1) * Pb;
+      int any = 0;
+      for (int y = threadIdx.x; y < N; y += T) {
+        const u128 f = Fc[y];
+        u128 reach = f | (f << 1) | (f >> 1);
+        if (y > 0) reach |= Fc[y - 1];
+        if (y + 1 < N) reach |= Fc[y + 1];
+        u128 nw = reach & rO[y] & ~rV[y];
+        Fn[y] = nw;
+        if (nw) {
+          any = 1;
+          rV[y] |= nw;
+          while (nw) {
+            const uint64_t lo = (uint64_t)nw, hi = (uint64_t)(nw >> 64);
+            const int x = lo ? __ffsll((long long)lo) - 1 : 64 + __ffsll((long long)hi) - 1;
+            tdist[y * N + x] = (uint16_t)level;
+            nw &= nw - 1;
+          }
+        }
+      }
+      if (!__syncthreads_or(any)) break;
+      cur ^= 1;
+    }
+  }
+  auto sq_dist = [&](int q) -> int {  // BFS distance to the goal (MZ_CELL_D_MASK: unreachable)
+    if (!tor) return (int)(cell(q) & MZ_CELL_D_MASK);
+    const int v = tdist[q];
+    return v < (int)MZ_CELL_D_MASK ? v : (int)MZ_CELL_D_MASK;
+  };
   __syncthreads();
   {
     int n_open = 0, n_edges = 0, bad = 0;
     for (int q = threadIdx.x; q < NN; q += T) {
       if (!(fl[q] & F_OPEN)) continue;
       const int r = q / N, c = q - r * N;
-      const int D = (int)(cell(q) & MZ_CELL_D_MASK);
+      const int D = sq_dist(q);
       if (D >= (int)MZ_CELL_D_MASK) bad = 1;  // unreachable from the goal
       // open squares on the border (the host restatement's neighbour count reads past the grid)
       if (r == 0 || c == 0 || r == N - 1 || c == N - 1) bad |= 2;
@@ -168,7 +374,7 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
         nbo[k] = rr >= 0 && rr < N && cc >= 0 && cc < N && (fl[rr * N + cc] & F_OPEN);
         if (nbo[k]) {
           ++deg;
-          if (D > 0 && (int)(cell(rr * N + cc) & MZ_CELL_D_MASK) == D - 1) gp[q] = (uint16_t)(rr * N + cc);
+          if (D > 0 && sq_dist(rr * N + cc) == D - 1) gp[q] = (uint16_t)(rr * N + cc);
         }
       }
       n_open += 1;
@@ -255,7 +461,7 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
   for (int q = threadIdx.x; q < NN; q += T) {
     if ((fl[q] & F_POINT) && !(fl[q] & F_SOL)) {
       const int k = atomicAdd(&s_noff, 1);
-      const uint32_t D = cell(q) & MZ_CELL_D_MASK;
+      const uint32_t D = (uint32_t)sq_dist(q);
       if (fst[q] > 0x3FFFu) s_bad = 2;  // no dead end below it
       if (k < MM)
         keys[k] = ((uint64_t)(fst[q] & 0x3FFFu) << 28) | ((uint64_t)(8191u - D) << 15) | (uint64_t)q;
@@ -278,7 +484,7 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
   for (int v = threadIdx.x; v < M; v += T) {
     const int q = nsq[v], r = q / N, c = q - r * N;
     const bool sol = fl[q] & F_SOL;
-    const uint32_t Dq = cell(q) & MZ_CELL_D_MASK;
+    const uint32_t Dq = (uint32_t)sq_dist(q);
     int deg = 0, par = NONE, pard = 0, succ = NONE, succd = 0;
     int ch[4], chd[4], chf[4], nch = 0;
     for (int k = 0; k < 4; ++k) {
@@ -296,7 +502,7 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
       const int u = pos[y];
       bool is_par, is_succ = false;
       if (sol) {
-        const uint32_t Dy0 = cell(y0) & MZ_CELL_D_MASK;
+        const uint32_t Dy0 = (uint32_t)sq_dist(y0);
         is_par = (fl[y0] & F_SOL) && Dy0 == Dq + 1;
         is_succ = (fl[y0] & F_SOL) && y0 == gp[q];
       } else {
@@ -405,62 +611,190 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
   for (int v = threadIdx.x; v < M; v += T) bid[v] = br[v] != NONE ? pref[bmin[br[v]]] : NONE;
   __syncthreads();
   const int Hn = s_Hn, Bn = s_Bn;
-  // ---- G. hallway edges in the subgraph's edge order (lower-position end, then its adjacency
-  // index): every member scans its adjacency with the reference's junction rule and break
-  for (int m = threadIdx.x; m < M; m += T) {
-    if (!in_h(m)) continue;
-    const uint64_t h = hid[m];
-    const int na = adjn[m];
-    bool jstop = false;  // the reference's break (:213-214): no junction after a solution one
-    for (int k = 0; k < na; ++k) {
-      const int u = adjp[4 * m + k], du = adjd[4 * m + k];
-      int v = -1, kk = 0;
-      if (in_h(u)) {
-        if (m < u) { v = m; kk = k; }
-      } else if ((nfl[u] & N_JUNC) && !jstop) {
-        if (m < u) { v = m; kk = k; }
-        else {
-          v = u;
-          for (int j = 0; j < adjn[u]; ++j)
-            if (adjp[4 * u + j] == m) kk = j;
+  // ---- G. hallway complexities, one wave per hallway (extract_hallways :186-221,
+  // complexity_of_hallway :286-296) ---------------------------------------------------------
+  // member lists grouped by hallway id (the phase-F roots / minima are dead now)
+  uint16_t* hlist = hr;     // [M] members, grouped by hallway
+  uint32_t* hstart = hmin;  // [Hn + 2] first member of hallway h
+  uint32_t* hcur = bmin;    // [Hn + 2] counts, then scatter cursors
+  if (Hn + 2 > MM) { fail(2); return; }
+  for (int h = threadIdx.x; h <= Hn + 1; h += T) hcur[h] = 0;
+  __syncthreads();
+  for (int v = threadIdx.x; v < M; v += T)
+    if (hid[v]) atomicAdd(&hcur[hid[v]], 1u);
+  __syncthreads();
+  {
+    int carry = 0;
+    for (int h0 = 0; h0 <= Hn + 1; h0 += T) {
+      const int h = h0 + threadIdx.x;
+      const int c = (h >= 1 && h <= Hn) ? (int)hcur[h] : 0;
+      int tot;
+      const int ex = carry + block_excl(c, wsum, &tot);
+      __syncthreads();
+      if (h <= Hn + 1) hstart[h] = (uint32_t)ex;
+      carry += tot;
+      __syncthreads();
+    }
+  }
+  for (int h = threadIdx.x; h <= Hn + 1; h += T) hcur[h] = hstart[h];
+  __syncthreads();
+  for (int v = threadIdx.x; v < M; v += T)
+    if (hid[v]) hlist[atomicAdd(&hcur[hid[v]], 1u)] = (uint16_t)v;
+  __syncthreads();
+  {
+    const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
+    auto key_of = [&](int v) -> uint32_t {  // cantor_pairing((r, c)) (:7-20), also its hash
+      const int q = nsq[v], r = q / N, c = q - r * N;
+      return (uint32_t)((r + c) * (r + c + 1) / 2 + c);
+    };
+    auto wave_sum = [&](int x) {
+      for (int k = WAVE / 2; k; k >>= 1) x += __shfl_xor(x, k);
+      return x;
+    };
+    auto wave_min = [&](int x) {
+      for (int k = WAVE / 2; k; k >>= 1) x = min(x, __shfl_xor(x, k));
+      return x;
+    };
+    for (int h = 1 + wid; h <= Hn; h += T / WAVE) {
+      const int b0 = (int)hstart[h], nc = (int)hstart[h + 1] - b0;
+      // adjacent_split_points (:208-214): each member's junction neighbours up to and including
+      // the first solution junction (the reference's break); in a tree each such junction
+      // neighbours one member only
+      int na_l = 0, f_l = 0x7FFFFFFF;
+      for (int i = lane; i < nc; i += WAVE) {
+        const int m = hlist[b0 + i];
+        f_l = min(f_l, m);
+        for (int k = 0; k < adjn[m]; ++k) {
+          const int u = adjp[4 * m + k];
+          if (nfl[u] & N_JUNC) {
+            ++na_l;
+            if (nfl[u] & N_SOL) break;
+          }
         }
-        if (nfl[u] & N_SOL) jstop = true;
       }
-      if (v >= 0) {
-        const int slot = atomicAdd(&s_nent, 1);
-        if (slot < MM)
-          keys[slot] = (h << 48) | ((uint64_t)v << 20) | ((uint64_t)kk << 16) | (uint64_t)du;
-      }
-    }
-  }
-  __syncthreads();
-  const int nent = s_nent;
-  if (nent > MM || Hn + 1 > MM) { fail(2); return; }
-  const int S2 = next_pow2(nent > 1 ? nent : 2);
-  for (int k = nent + threadIdx.x; k < S2; k += T) keys[k] = ~0ull;
-  for (int h = threadIdx.x; h <= Hn; h += T) pref[h] = NONE;  // segment start per hallway
-  __syncthreads();
-  bitonic(keys, S2);
-  for (int k = threadIdx.x; k < nent; k += T) {
-    const int h = (int)(keys[k] >> 48);
-    if (k == 0 || (int)(keys[k - 1] >> 48) != h) pref[h] = (uint16_t)k;
-  }
-  __syncthreads();
-  // C_h = D_h * sum(1 / (2 d)) in edge order (sum() starts from int 0: 0 + t = t)
-  for (int h = 1 + threadIdx.x; h <= Hn; h += T) {
-    double s = 0.0;
-    long D = 0;
-    const int k0 = pref[h];
-    if (k0 != NONE) {
-      for (int k = k0; k < nent && (int)(keys[k] >> 48) == h; ++k) {
-        const int dd = (int)(keys[k] & 0xFFFFu);
+      const int nasp = wave_sum(na_l);
+      double sum = 0.0;
+      long D = 0;
+      int nterm = 0;
+      auto add_term = [&](int dd) {  // sum() from int 0 (0 + t = t), then left to right
         const double t = __ddiv_rn(1.0, __dmul_rn(2.0, (double)dd));
-        s = k == k0 ? t : __dadd_rn(s, t);
+        sum = nterm ? __dadd_rn(sum, t) : t;
         D += dd;
+        ++nterm;
+      };
+      bool ok = true;
+      if (nc + nasp <= 3) {
+        // <= 3 view nodes, <= 2 edges: their sum does not depend on the order
+        for (int i = 0; i < nc; ++i) {
+          const int m = hlist[b0 + i];
+          bool jstop = false;
+          for (int k = 0; k < adjn[m]; ++k) {
+            const int u = adjp[4 * m + k];
+            if (in_h(u)) {
+              if (u > m) add_term(adjd[4 * m + k]);
+            } else if ((nfl[u] & N_JUNC) && !jstop) {
+              add_term(adjd[4 * m + k]);
+              if (nfl[u] & N_SOL) jstop = true;
+            }
+          }
+        }
+      } else if (nc + nasp > 63) {
+        ok = false;  // beyond the wave's 128-slot tables: the host restatement
+      } else {
+        // _plain_bfs (nx.connected_components on temp_graph = G.copy() minus split / solution
+        // points, :194-201): BFS from the member first in node order, each node's neighbours in
+        // the copy's adjacency order — earlier neighbours by position, then later ones in G's
+        // order — into `seen` (a set built by add())
+        const int first = wave_min(f_l);
+        WSet S1, S2;
+        ws_init(S1);
+        uint32_t qv = 0;  // BFS queue: entry i in lane i
+        int qn = 0;
+        auto push = [&](int v) {
+          if (lane == qn) qv = (uint32_t)v;
+          ++qn;
+        };
+        ok = ws_add(S1, key_of(first), (uint32_t)first) >= 0;
+        push(first);
+        for (int hd = 0; hd < qn && ok; ++hd) {
+          const int x = __shfl((int)qv, hd);
+          const int na = adjn[x];
+          int ord[4], no = 0;
+          for (int k = 0; k < na; ++k) {  // earlier neighbours, ascending
+            const int u = adjp[4 * x + k];
+            if (u >= x) continue;
+            int j = no++;
+            while (j > 0 && ord[j - 1] > u) { ord[j] = ord[j - 1]; --j; }
+            ord[j] = u;
+          }
+          for (int k = 0; k < na; ++k) {
+            const int u = adjp[4 * x + k];
+            if (u > x) ord[no++] = u;
+          }
+          for (int k = 0; k < no && ok; ++k) {
+            const int u = ord[k];
+            if (!in_h(u)) continue;
+            const int r = ws_add(S1, key_of(u), (uint32_t)u);
+            if (r < 0) ok = false;
+            else if (r == 1) push(u);
+          }
+        }
+        ok = ok && ws_copy(S2, S1);  // set(component_nodes) (:205)
+        // adjacent_split_points, filled in that set's order
+        ws_init(S1);
+        for (int j = ws_next(S2, -1); j >= 0 && ok; j = ws_next(S2, j)) {
+          const int m = (int)(ws_get(S2, j) & 0xFFFFu);
+          for (int k = 0; k < adjn[m]; ++k) {
+            const int u = adjp[4 * m + k];
+            if (nfl[u] & N_JUNC) {
+              if (ws_add(S1, key_of(u), (uint32_t)u) < 0) ok = false;
+              if (nfl[u] & N_SOL) break;
+            }
+          }
+        }
+        // all_nodes = component_nodes.union(adjacent_split_points) (:217): the copy of a
+        // dummy-free set has its layout, then the merge
+        ok = ok && ws_merge(S2, S1);
+        // show_nodes(nbunch_iter(all_nodes)).nodes: a set built by add() in all_nodes' order
+        ws_init(S1);
+        for (int j = ws_next(S2, -1); j >= 0 && ok; j = ws_next(S2, j)) {
+          const uint32_t v = ws_get(S2, j);
+          if (ws_add(S1, v >> 16, v & 0xFFFFu) < 0) ok = false;
+        }
+        if (ok && 2 * S1.used < M) {
+          // FilterAdjacency iterates the set; EdgeDataView reports (n, u) for u in G's adjacency
+          // order of n, inside the view, not yet iterated
+          for (int j = ws_next(S1, -1); j >= 0; j = ws_next(S1, j)) {
+            const int n = (int)(ws_get(S1, j) & 0xFFFFu);
+            for (int k = 0; k < adjn[n]; ++k)
+              if (ws_find(S1, key_of(adjp[4 * n + k])) > j) add_term(adjd[4 * n + k]);
+          }
+        } else if (ok) {
+          // the view holds at least half of G: G's node order (position)
+          int last = -1;
+          for (int c = 0; c < S1.used; ++c) {
+            int cand = 0x7FFFFFFF;
+            if (S1.v0 != WS_EMPTY && (int)(S1.v0 & 0xFFFFu) > last) cand = (int)(S1.v0 & 0xFFFFu);
+            if (S1.v1 != WS_EMPTY && (int)(S1.v1 & 0xFFFFu) > last)
+              cand = min(cand, (int)(S1.v1 & 0xFFFFu));
+            const int n = wave_min(cand);
+            for (int k = 0; k < adjn[n]; ++k) {
+              const int u = adjp[4 * n + k];
+              if (u > n && ws_find(S1, key_of(u)) >= 0) add_term(adjd[4 * n + k]);
+            }
+            last = n;
+          }
+        }
+      }
+      if (!ok) {
+        if (lane == 0) s_bad = 2;
+      } else if (lane == 0) {
+        Ch[h] = __dmul_rn((double)D, sum);
       }
     }
-    Ch[h] = __dmul_rn((double)D, s);
   }
+  __syncthreads();
+  if (s_bad) { fail(2); return; }
   // hallway 0: the solution branch, edges in path order
   if (threadIdx.x == 0) {
     double s = 0.0;
@@ -514,12 +848,15 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
 
 }  // namespace
 
-size_t mz_mcclendon_lds(int P, int* mm) {
-  const int cells = ((P - 1) / 2) * ((P - 1) / 2) + 4;
+size_t mz_mcclendon_lds(int P, bool toroidal, int* mm) {
+  const int Pb = toroidal ? P + 2 : P;  // a toroidal maze is scored on its bordered grid
+  const int cells = ((Pb - 1) / 2) * ((Pb - 1) / 2) + 4;
   int MM = 16;
   while (MM < cells) MM <<= 1;
   *mm = MM;
-  const size_t sq = ((size_t)P * P * 9 + 16 + 15) & ~(size_t)15;
+  const size_t NNP = (size_t)Pb * Pb;
+  size_t sq = (NNP * 9 + 16 + 15) & ~(size_t)15;
+  if (toroidal) sq += ((NNP * 2 + 15) & ~(size_t)15) + 64 * (size_t)Pb;  // distances + BFS rows
   const size_t node = (size_t)MM * (8 + 2 + 8 + 8 + 2 + 2 + 2 + 1 + 1);
   const size_t ph2 = (size_t)MM * (2 * 6 + 4 * 2 + 8 * 2);
   return (sq > ph2 ? sq : ph2) + node;
@@ -529,7 +866,7 @@ hipError_t mz_launch_mcclendon(const MzDev& d, const int32_t* ids, int n, double
                                int32_t* status, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   int MM = 0;
-  const size_t bytes = mz_mcclendon_lds(d.P, &MM);
+  const size_t bytes = mz_mcclendon_lds(d.P, d.toroidal != 0, &MM);
   if (bytes > 160 * 1024) return hipErrorInvalidValue;
   if (bytes > 65536) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mcclendon),

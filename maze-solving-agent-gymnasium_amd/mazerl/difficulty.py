@@ -25,8 +25,9 @@ def toroidal_difficulty(grid, start, goal):
 
 def difficulty_batch(env, env_ids=None, complexity=False):
     """McClendon difficulty (and complexity) of resident mazes of a VectorMazeEnv, one GPU
-    workgroup per maze (mz_difficulty_batch, csrc/mz_mcclendon.hip); mazes the kernel leaves
-    to the host (nonzero status: cycles, open border squares, ...) go through mz_difficulty.
+    workgroup per maze (mz_difficulty_batch, csrc/mz_mcclendon.hip; a toroidal maze scored as its
+    bordered maze, as the reference scores it); mazes the kernel leaves to the host (nonzero
+    status: cycles, open border squares, very long hallways, ...) go through mz_difficulty.
     Returns float64 numpy [n] (or ([n], [n]) with complexity) — math.log of the kernel's
     product / sum, the C library's log as the reference's math.log."""
     import math
@@ -57,7 +58,7 @@ def difficulty_batch(env, env_ids=None, complexity=False):
         q = env.query(e)
         g = env.grid(e)
         s, t = (q["start_r"], q["start_c"]), (q["goal_r"], q["goal_c"])
-        if stat[i] == 4:
+        if env.toroidal:
             d[i] = toroidal_difficulty(g, s, t)
             c[i] = toroidal_complexity(g, s, t)
         else:

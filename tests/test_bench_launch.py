@@ -63,6 +63,7 @@ def test_launch_relays_rank0_json_line(tmp_path):
     p = _run_launcher(tmp_path, """
         import json, os
         r, w = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+        print(f"[lib] rank {r} banner on stdout", flush=True)
         print(json.dumps({"rank": r, "world": w, "port": os.environ["MASTER_PORT"]}) if r == 0
               else f"rank {r} stdout", flush=True)
     """, 3)
@@ -72,6 +73,7 @@ def test_launch_relays_rank0_json_line(tmp_path):
     rec = json.loads(lines[0])
     assert rec["rank"] == 0 and rec["world"] == 3 and int(rec["port"]) > 0
     assert "rank 1 stdout" in p.stderr and "rank 2 stdout" in p.stderr
+    assert "[lib] rank 0 banner on stdout" in p.stderr  # rank 0's non-JSON lines go to stderr
 
 
 def test_launch_stops_every_rank_when_one_fails(tmp_path):

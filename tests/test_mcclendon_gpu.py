@@ -2,12 +2,15 @@
 and the host restatement (mz_difficulty / mz_maze_complexity, maze_complexity_evaluation.py:38-329).
 
 - the 24 reference 81x81 mazes of gen_euclid.npz: difficulty and complexity equal the values the
-  reference's ComplexityEvaluation computed (tests/golden/difficulty81.npz, rel 1e-15 as
-  tests/test_difficulty.py) and the host restatement's bit for bit;
-- every golden euclidean maze of 15..81 squares and 1,152 GPU-generated mazes (3 algorithms x 6 sizes):
-  status 0 and bit-exact with the host restatement;
-- the kernel's declines: a maze with a cycle (status 1), toroidal instances (status 4); the
-  Python wrapper computes those on the host, equal to the host calls.
+  reference's ComplexityEvaluation computed (tests/golden/difficulty81.npz) and the host
+  restatement's, bit for bit (hallway sums in networkx's subgraph-view set order);
+- every golden euclidean maze of 15..81 squares, the toroidal golden mazes (scored on their
+  bordered grid, as the reference scores them) and tests/golden/mcclendon.npz: status 0 and
+  bit-exact with the reference's values and the host restatement;
+- 1,152 GPU-generated euclidean and 768 toroidal mazes (3 algorithms x sizes): bit-exact with the
+  host restatement;
+- the kernel's declines: a maze with a cycle (status 1); the Python wrapper computes it on the
+  host, equal to the host call.
 """
 import math
 
@@ -60,15 +63,11 @@ def test_reference_81x81_values(mods):
     pw, st = _raw(mods, env)
     assert (st == 0).all(), st
     d, c = D.difficulty_batch(env, complexity=True)
-    exact = 0
     for k, m in enumerate(ms):
         hd, hc = D.maze_complexity(m["grid"], m["start"], m["goal"])
         assert d[k] == hd and c[k] == hc, (k, d[k], hd, c[k], hc)  # bit-exact vs the host
         assert d[k] == math.log(pw[k, 0])
-        assert d[k] == pytest.approx(float(z["difficulty"][k]), rel=1e-15, abs=0)
-        assert c[k] == pytest.approx(float(z["complexity"][k]), rel=1e-15, abs=0)
-        exact += d[k] == z["difficulty"][k]
-    assert exact >= 20
+        assert d[k] == z["difficulty"][k] and c[k] == z["complexity"][k], k  # and the reference
     env.close()
 
 
@@ -82,7 +81,75 @@ def test_golden_euclidean_mazes_bit_exact_with_host(mods):
     for k, m in enumerate(ms):
         assert (d[k], c[k]) == D.maze_complexity(m["grid"], m["start"], m["goal"]), k
         if not math.isnan(m["difficulty"]):
-            assert d[k] == pytest.approx(m["difficulty"], rel=1e-15, abs=0)
+            assert d[k] == m["difficulty"], k
+    env.close()
+
+
+def test_golden_toroidal_mazes_on_the_gpu(mods):
+    """Toroidal handles: the kernel scores the bordered maze (wall ring, start / goal + 1) —
+    status 0, == the reference's gen_maze_no_border difficulty and the host restatement."""
+    _, _, D, _ = mods
+    ms = [m for m in G.mazes("gen_toroid.npz") if m["n"] >= 17]
+    env = _loaded(mods, ms, toroidal=True)
+    _, st = _raw(mods, env)
+    assert (st == 0).all(), np.nonzero(st)[0]
+    d, c = D.difficulty_batch(env, complexity=True)
+    for k, m in enumerate(ms):
+        assert d[k] == D.toroidal_difficulty(m["grid"], m["start"], m["goal"]), k
+        assert c[k] == D.toroidal_complexity(m["grid"], m["start"], m["goal"]), k
+        if not math.isnan(m["difficulty"]):
+            assert d[k] == m["difficulty"], k
+    env.close()
+
+
+def test_set_order_fixture_on_the_gpu(mods):
+    """tests/golden/mcclendon.npz (228 reference mazes, euclidean 9..61 and re-bordered toroidal
+    9..41): the euclidean ones of >= 15 squares in a euclidean handle, the toroidal ones cropped
+    back into a toroidal handle — GPU == the reference's difficulty and complexity."""
+    _, _, D, _ = mods
+    z = G.load("mcclendon.npz")
+    eu, to = [], []
+    for i in range(len(z["n"])):
+        n = int(z["n"][i])
+        m = dict(grid=z["grid"][i, :n, :n], start=tuple(int(x) for x in z["start"][i]),
+                 goal=tuple(int(x) for x in z["goal"][i]), difficulty=float(z["difficulty"][i]),
+                 complexity=float(z["complexity"][i]), n=n)
+        if math.isnan(m["difficulty"]):
+            continue
+        if z["toroidal"][i]:
+            if n - 2 >= 17:
+                to.append(dict(m, grid=m["grid"][1:-1, 1:-1], n=n - 2,
+                               start=(m["start"][0] - 1, m["start"][1] - 1),
+                               goal=(m["goal"][0] - 1, m["goal"][1] - 1)))
+        elif n >= 15:
+            eu.append(m)
+    assert len(eu) >= 100 and len(to) >= 40
+    for ms, tor in ((eu, False), (to, True)):
+        env = _loaded(mods, ms, toroidal=tor)
+        _, st = _raw(mods, env)
+        assert (st == 0).all(), (tor, np.nonzero(st)[0])
+        d, c = D.difficulty_batch(env, complexity=True)
+        for k, m in enumerate(ms):
+            assert d[k] == m["difficulty"] and c[k] == m["complexity"], (tor, k, m["n"])
+        env.close()
+
+
+@pytest.mark.parametrize("algo", ["r-prim", "dfs", "prim&kill"])
+def test_generated_toroidal_mazes_bit_exact_with_host(mods, algo):
+    _, _, D, _ = mods
+    from mazerl.trainers.vector_trainer import make_env
+    dims = [17, 29, 41, 53, 65, 79, 23, 35]
+    n = 32 * len(dims)
+    env = make_env(n, dims, toroidal=True, algorithm=algo, seed=0x70D1FF, device="cuda:0",
+                   done_list=False)
+    pw, st = _raw(mods, env)
+    assert (st == 0).all(), np.nonzero(st)[0]
+    d, c = D.difficulty_batch(env, complexity=True)
+    for i in range(n):
+        q = env.query(i)
+        g, s, t = env.grid(i), (q["start_r"], q["start_c"]), (q["goal_r"], q["goal_c"])
+        h = (D.toroidal_difficulty(g, s, t), D.toroidal_complexity(g, s, t))
+        assert (d[i], c[i]) == h, (i, q["n"], d[i], c[i], h)
     env.close()
 
 
@@ -119,14 +186,6 @@ def test_declined_mazes_fall_back_to_the_host(mods):
     d = D.difficulty_batch(env)
     assert d[0] == D.maze_difficulty(g, cyc["start"], cyc["goal"])
     assert d[1] == D.maze_difficulty(ms[1]["grid"], ms[1]["start"], ms[1]["goal"])
-    env.close()
-    tor = [m for m in G.mazes("gen_toroid.npz") if m["n"] >= 15][:3]
-    env = _loaded(mods, tor, toroidal=True)
-    _, st = _raw(mods, env)
-    assert (st == 4).all()
-    d = D.difficulty_batch(env)
-    for k, m in enumerate(tor):
-        assert d[k] == D.toroidal_difficulty(m["grid"], m["start"], m["goal"])
     env.close()
 
 
