@@ -13,7 +13,7 @@ import torch
 
 from .distributed import GradAllReduce, allreduce_sum, broadcast_params, init_from_env
 from .trainers.ppo_trainer import VectorPPOTrainer
-from .trainers.vector_trainer import evaluate, make_env
+from .trainers.vector_trainer import best_of_mazes, evaluate, make_env
 
 
 def main(argv=None):
@@ -64,12 +64,18 @@ def main(argv=None):
     if rank == 0:
         rate, k = evaluate(tr, a.eval_mazes, dims, a.algo, seed=0x7E570000, eps=0.0, toroidal=True,
                            device=dev)
+        # new mazes as the reference's toroidal env picks them: the easiest of 6 by the McClendon
+        # difficulty of the bordered maze (toroidal_maze_env.py:40-54), scored on the GPU
+        mz6 = best_of_mazes(a.eval_mazes, dims, a.algo, seed=0x7E580000, device=dev, toroidal=True)
+        rate6, _ = evaluate(tr, a.eval_mazes, dims, a.algo, seed=0x7E580000, eps=0.0,
+                            toroidal=True, device=dev, mazes=mz6)
         print(json.dumps({"config": "ppo toroidal variable", "envs_per_gpu": a.envs, "n_gpus": world,
                           "dims": [dims[0], dims[-1]], "vector_steps": a.steps, "train_seconds": secs,
                           "train_env_steps_per_s": a.envs * a.steps * world / secs,
                           "episodes": int(st[0]), "wins": int(st[1]), "updates": tr.updates,
-                          "acting": "f32 (ActorCriticNet.act as the reference)",
-                          "win_rate_greedy": rate, "eval_steps": k}), flush=True)
+                          "seed": a.seed, "acting": "f32 (ActorCriticNet.act as the reference)",
+                          "win_rate_greedy": rate, "win_rate_greedy_best_of_6": rate6,
+                          "eval_mazes": a.eval_mazes, "eval_steps": k}), flush=True)
     env.close()
 
 
