@@ -554,8 +554,11 @@ int mz_qact_prepare(const float* fc1_w_dev, const float* fc2_w_dev, uint16_t* w1
  * [32][3][3][3] / bias, fc1 bias [1024], fc2 bias [512], fc3 weight [4][512] / bias [4] f32;
  * relu: 1 for DDQN's second activation (ReLU), 0 for DQN's LeakyReLU; drop_p > 0: DDQN's
  * train-mode Dropout after the conv activation (counter hash of seed / counter, row, feature).
- * h1_dev: workspace [n][1024] f32. Outputs: greedy_dev[instance] = first argmax (int64; NaN as
- * torch.argmax), q_out_dev [n][4] f32 (either may be NULL). No host synchronisation. */
+ * h1_dev: workspace of mz_qact_workspace_floats(n) f32 (fc1's output rows [n][1024], then the
+ * conv stem's bf16 hi / lo feature tiles: the stem runs once per 64 rows, k_qconv, and fc1 reads
+ * them, k_qfc1). Outputs: greedy_dev[instance] = first argmax (int64; NaN as torch.argmax),
+ * q_out_dev [n][4] f32 (either may be NULL). No host synchronisation. */
+int64_t mz_qact_workspace_floats(int32_t n);
 int mz_qact(const uint32_t* bits_dev, const float* obs6_dev, const int32_t* rows_dev,
             const int32_t* count_dev, int32_t n, const float* conv_w_dev, const float* conv_b_dev,
             const uint16_t* w1_hi_dev, const uint16_t* w1_lo_dev, const float* b1_dev,

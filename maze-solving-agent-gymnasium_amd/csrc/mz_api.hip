@@ -1087,6 +1087,8 @@ int mz_qact_prepare(const float* fc1_w_dev, const float* fc2_w_dev, uint16_t* w1
   return MZ_OK;
 }
 
+int64_t mz_qact_workspace_floats(int32_t n) { return n > 0 ? mz_qact_ws_floats(n) : 0; }
+
 int mz_qact(const uint32_t* bits_dev, const float* obs6_dev, const int32_t* rows_dev,
             const int32_t* count_dev, int32_t n, const float* conv_w_dev, const float* conv_b_dev,
             const uint16_t* w1_hi_dev, const uint16_t* w1_lo_dev, const float* b1_dev,

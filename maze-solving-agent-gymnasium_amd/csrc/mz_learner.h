@@ -114,6 +114,7 @@ struct MzQAct {
   int64_t* greedy; float* q_out;             // greedy[inst] = argmax; q_out [n][4] (nullable)
 };
 int mz_qact_row_tiles(int n);
+int64_t mz_qact_ws_floats(int n);
 hipError_t mz_launch_qact(const MzQAct& q, int relu, hipStream_t s);
 hipError_t mz_launch_qact_prepare(const float* w1, const float* w2, uint16_t* w1h, uint16_t* w1l,
                                   uint16_t* w2h, uint16_t* w2l, hipStream_t s);

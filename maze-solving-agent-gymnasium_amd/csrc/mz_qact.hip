@@ -123,6 +123,170 @@ __device__ inline void mfma_x3(const frag_ab (&ah)[I], const frag_ab (&al)[I], c
                                                           acc[i][j], 0, 0, 0);
 }
 
+// ---- the conv stem (shared by k_qact1 and k_qconv) --------------------------------------------
+// LDS tables and the tile's window rows: lut (8 patch bits -> 8 bf16), spread (8 bits -> bits at
+// 3i), wb (the rows' window bits), crow (column-interleaved padded window rows). Two barriers.
+__device__ inline void conv_tables(const MzQAct& q, int r0, int nr, int tid, int nthr, uint4* lut,
+                                   uint32_t* spread, uint64_t* crow, uint32_t* wb) {
+  for (int i = tid; i < 256; i += nthr) {
+    uint32_t v[4], sp = 0;
+    for (int p = 0; p < 4; ++p)
+      v[p] = (((i >> (2 * p)) & 1) ? 0x3F80u : 0u) | (((i >> (2 * p + 1)) & 1) ? 0x3F800000u : 0u);
+    lut[i] = make_uint4(v[0], v[1], v[2], v[3]);
+    for (int k = 0; k < 8; ++k) sp |= ((uint32_t)(i >> k) & 1u) << (3 * k);
+    spread[i] = sp;
+  }
+  for (int i = tid; i < RT1 * 22; i += nthr) {
+    const int r = i / 22, k = i - r * 22;
+    uint32_t v = 0;
+    if (r < nr) {
+      const int inst = q.rows ? q.rows[r0 + r] : r0 + r;
+      v = q.bits[(size_t)inst * 22 + k];
+    }
+    wb[i] = v;
+  }
+  for (int r = tid; r < RT1; r += nthr) {
+    crow[r * PR] = 0ull;
+    crow[r * PR + 16] = 0ull;
+  }
+  __syncthreads();
+  // window row y of every channel -> one column-interleaved row (col c at bits 3(c+1) + ch)
+  for (int i = tid; i < RT1 * 15; i += nthr) {
+    const int r = i / 15, y = i - r * 15;
+    uint64_t cr = 0;
+    for (int ch = 0; ch < 3; ++ch) {
+      const int f0 = ch * 225 + y * 15, j = f0 >> 5;
+      const uint64_t v = ((uint64_t)wb[r * 22 + j + 1] << 32) | wb[r * 22 + j];
+      const uint32_t row = (uint32_t)(v >> (f0 & 31)) & 0x7FFFu;
+      const uint64_t sp = (uint64_t)spread[row & 0xFF] | ((uint64_t)spread[row >> 8] << 24);
+      cr |= sp << (3 + ch);
+    }
+    crow[r * PR + y + 1] = cr;
+  }
+  __syncthreads();
+}
+
+// this lane's conv B operands, hi and lo: W[c][k] for k = 8 g4 + j, c = 2 c16 (even) and 2 c16 + 1
+// (odd); K order 9 ky + 3 kx + ch (the interleaved rows), torch's [c][ch][ky][kx]
+struct ConvW {
+  frag_ab be_h, be_l, bo_h, bo_l;
+  float bias_e, bias_o;
+};
+__device__ inline ConvW conv_weights(const MzQAct& q, int g4, int c16) {
+  ConvW cw;
+  for (int j = 0; j < 8; ++j) {
+    const int k = 8 * g4 + j;
+    const int ky = k / 9, kx = (k % 9) / 3, ch = k % 3;
+    const int wi = ch * 9 + ky * 3 + kx;
+    const float we = k < 27 ? q.conv_w[(2 * c16) * 27 + wi] : 0.0f;
+    const float wo = k < 27 ? q.conv_w[(2 * c16 + 1) * 27 + wi] : 0.0f;
+    const float weh = bf16_round(we), woh = bf16_round(wo);
+    cw.be_h[j] = static_cast<__bf16>(weh);
+    cw.be_l[j] = static_cast<__bf16>(we - weh);
+    cw.bo_h[j] = static_cast<__bf16>(woh);
+    cw.bo_l[j] = static_cast<__bf16>(wo - woh);
+  }
+  cw.bias_e = q.conv_b[2 * c16];
+  cw.bias_o = q.conv_b[2 * c16 + 1];
+  return cw;
+}
+
+// dropout streams (DDQN): one xorshift32 stream per (row, channel pair) — this lane's rows
+// 4 (TPWv w + tt) + g4, pair c16 — seeded lowbias32(lowbias32(key ^ lowbias32(row)) ^ pair) | 1,
+// four draws per pooled position in chunk order
+template <int TPWv>
+__device__ inline void drop_seeds(const MzQAct& q, int r0, int w, int g4, int c16, uint32_t (&rs)[4]) {
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt) rs[tt] = 0u;
+#pragma unroll
+  for (int tt = 0; tt < TPWv; ++tt) {
+    const uint32_t row = (uint32_t)(r0 + 4 * (TPWv * w + tt) + g4);
+    rs[tt] = lowbias32(lowbias32(q.key ^ lowbias32(row)) ^ (uint32_t)c16) | 1u;
+  }
+}
+
+// conv chunk c (pooled position c) of this wave's TPWv conv tiles (tile t: instances 4t .. 4t + 3;
+// the MFMA's A row of this lane = c16: instance 4t + c16 / 4, position c16 % 4 of its 2x2 pooling
+// window): LeakyReLU, DDQN's dropout, 2x2 max-pool, split into bf16 hi / lo. Out: for each tile
+// tt, row il[tt] of the 64-row block, channels 2 c16 and 2 c16 + 1 packed as hi[tt] / lo[tt].
+template <bool DROP, int TPWv>
+__device__ inline void conv_chunk_vals(const MzQAct& q, int c, int w, int g4, int c16,
+                                       const uint4* lut, const uint64_t* crow, const ConvW& cw,
+                                       uint32_t (&rs)[4], int (&il)[TPWv], uint32_t (&hi)[TPWv],
+                                       uint32_t (&lo)[TPWv]) {
+  const int py = c / 7, px = c - py * 7;
+  frag_ab a[TPWv];
+#pragma unroll
+  for (int tt = 0; tt < TPWv; ++tt) {
+    const int inst = 4 * (TPWv * w + tt) + (c16 >> 2), pos = c16 & 3;
+    const int y = 2 * py + (pos >> 1), xx = 2 * px + (pos & 1);
+    const uint64_t* cr = crow + inst * PR + y;
+    const uint32_t p = ((uint32_t)(cr[0] >> (3 * xx)) & 0x1FFu) |
+                       (((uint32_t)(cr[1] >> (3 * xx)) & 0x1FFu) << 9) |
+                       (((uint32_t)(cr[2] >> (3 * xx)) & 0x1FFu) << 18);
+    a[tt] = __builtin_bit_cast(frag_ab, lut[(p >> (8 * g4)) & 0xFFu]);
+  }
+  frag_cd e[TPWv], o[TPWv];
+#pragma unroll
+  for (int tt = 0; tt < TPWv; ++tt) {
+    e[tt] = frag_cd{cw.bias_e, cw.bias_e, cw.bias_e, cw.bias_e};
+    o[tt] = frag_cd{cw.bias_o, cw.bias_o, cw.bias_o, cw.bias_o};
+  }
+#pragma unroll
+  for (int tt = 0; tt < TPWv; ++tt) {
+    e[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tt], cw.be_h, e[tt], 0, 0, 0);
+    o[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tt], cw.bo_h, o[tt], 0, 0, 0);
+  }
+#pragma unroll
+  for (int tt = 0; tt < TPWv; ++tt) {
+    e[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tt], cw.be_l, e[tt], 0, 0, 0);
+    o[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tt], cw.bo_l, o[tt], 0, 0, 0);
+  }
+#pragma unroll
+  for (int tt = 0; tt < TPWv; ++tt) {
+    // lane: pooled output of instance 4t + g4, channels 2 c16 (e) and 2 c16 + 1 (o);
+    // registers = the 4 positions of its 2x2 window
+    il[tt] = 4 * (TPWv * w + tt) + g4;
+    float ve, vo;
+    if (DROP) {
+      // MaxPool(Dropout(LeakyReLU(x))) = scale * leaky(max_r x'_r), x'_r = x_r kept, 0 dropped
+      // (leaky(0) = 0; leaky and the scale are monotonic): the 4 draws of this chunk from the
+      // lane's stream, low half -> even channel, high half -> odd
+      float me = 0.0f, mo = 0.0f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        uint32_t x = rs[tt];
+        x ^= x << 13;
+        x ^= x >> 17;
+        x ^= x << 5;
+        rs[tt] = x;
+        const float xe = (x & 0xFFFFu) >= q.drop_thresh ? e[tt][r] : 0.0f;
+        const float xo = (x >> 16) >= q.drop_thresh ? o[tt][r] : 0.0f;
+        me = r ? fmaxf(me, xe) : xe;
+        mo = r ? fmaxf(mo, xo) : xo;
+      }
+      ve = leaky(me) * q.drop_scale;
+      vo = leaky(mo) * q.drop_scale;
+    } else {
+      ve = leaky(fmaxf(fmaxf(e[tt][0], e[tt][1]), fmaxf(e[tt][2], e[tt][3])));
+      vo = leaky(fmaxf(fmaxf(o[tt][0], o[tt][1]), fmaxf(o[tt][2], o[tt][3])));
+    }
+    split2(ve, vo, hi[tt], lo[tt]);
+  }
+}
+
+// the obs6 chunk (features 1568..1573, then zeros) of row r, k pair k2 / 2: packed hi / lo
+__device__ inline void obs_vals(const MzQAct& q, int r0, int nr, int r, int k2, uint32_t& hi,
+                                uint32_t& lo) {
+  float v0 = 0.0f, v1 = 0.0f;
+  if (r < nr && k2 < 6) {
+    const int inst = q.rows ? q.rows[r0 + r] : r0 + r;
+    v0 = q.obs6[(size_t)inst * 6 + k2];
+    v1 = q.obs6[(size_t)inst * 6 + k2 + 1];
+  }
+  split2(v0, v1, hi, lo);
+}
+
 // ---- k_qact1 -------------------------------------------------------------------------------
 template <bool DROP>
 __global__ __launch_bounds__(T1) __attribute__((amdgpu_waves_per_eu(2, 2)))
@@ -146,69 +310,10 @@ void k_qact1(MzQAct q, int row_tiles) {
   if (r0 >= m) return;
   const int nr = min(RT1, m - r0);
 
-  for (int i = tid; i < 256; i += T1) {
-    uint32_t v[4], sp = 0;
-    for (int p = 0; p < 4; ++p)
-      v[p] = (((i >> (2 * p)) & 1) ? 0x3F80u : 0u) | (((i >> (2 * p + 1)) & 1) ? 0x3F800000u : 0u);
-    lut[i] = make_uint4(v[0], v[1], v[2], v[3]);
-    for (int k = 0; k < 8; ++k) sp |= ((uint32_t)(i >> k) & 1u) << (3 * k);
-    spread[i] = sp;
-  }
-  for (int i = tid; i < RT1 * 22; i += T1) {
-    const int r = i / 22, k = i - r * 22;
-    uint32_t v = 0;
-    if (r < nr) {
-      const int inst = q.rows ? q.rows[r0 + r] : r0 + r;
-      v = q.bits[(size_t)inst * 22 + k];
-    }
-    wb[i] = v;
-  }
-  for (int r = tid; r < RT1; r += T1) {
-    crow[r * PR] = 0ull;
-    crow[r * PR + 16] = 0ull;
-  }
-  __syncthreads();
-  // window row y of every channel -> one column-interleaved row (col c at bits 3(c+1) + ch)
-  for (int i = tid; i < RT1 * 15; i += T1) {
-    const int r = i / 15, y = i - r * 15;
-    uint64_t cr = 0;
-    for (int ch = 0; ch < 3; ++ch) {
-      const int f0 = ch * 225 + y * 15, j = f0 >> 5;
-      const uint64_t v = ((uint64_t)wb[r * 22 + j + 1] << 32) | wb[r * 22 + j];
-      const uint32_t row = (uint32_t)(v >> (f0 & 31)) & 0x7FFFu;
-      const uint64_t sp = (uint64_t)spread[row & 0xFF] | ((uint64_t)spread[row >> 8] << 24);
-      cr |= sp << (3 + ch);
-    }
-    crow[r * PR + y + 1] = cr;
-  }
-
-  // conv B operands, hi and lo: lane holds W[c][k] for k = 8 g4 + j, c = 2 c16 (even) and
-  // 2 c16 + 1 (odd); K order 9 ky + 3 kx + ch (the interleaved rows), torch's [c][ch][ky][kx]
-  frag_ab be_h, be_l, bo_h, bo_l;
-  for (int j = 0; j < 8; ++j) {
-    const int k = 8 * g4 + j;
-    const int ky = k / 9, kx = (k % 9) / 3, ch = k % 3;
-    const int wi = ch * 9 + ky * 3 + kx;
-    const float we = k < 27 ? q.conv_w[(2 * c16) * 27 + wi] : 0.0f;
-    const float wo = k < 27 ? q.conv_w[(2 * c16 + 1) * 27 + wi] : 0.0f;
-    const float weh = bf16_round(we), woh = bf16_round(wo);
-    be_h[j] = static_cast<__bf16>(weh);
-    be_l[j] = static_cast<__bf16>(we - weh);
-    bo_h[j] = static_cast<__bf16>(woh);
-    bo_l[j] = static_cast<__bf16>(wo - woh);
-  }
-  const float bias_e = q.conv_b[2 * c16], bias_o = q.conv_b[2 * c16 + 1];
-  // dropout streams (DDQN): one xorshift32 stream per (row, channel pair) — this lane's rows
-  // 4 (4w + tt) + g4, pair c16 — seeded lowbias32(lowbias32(key ^ lowbias32(row)) ^ pair) | 1,
-  // four draws per pooled position in chunk order
-  uint32_t rs[4] = {0u, 0u, 0u, 0u};
-  if (DROP) {
-#pragma unroll
-    for (int tt = 0; tt < TPW; ++tt) {
-      const uint32_t row = (uint32_t)(r0 + 4 * (TPW * w + tt) + g4);
-      rs[tt] = lowbias32(lowbias32(q.key ^ lowbias32(row)) ^ (uint32_t)c16) | 1u;
-    }
-  }
+  conv_tables(q, r0, nr, tid, T1, lut, spread, crow, wb);
+  const ConvW cw = conv_weights(q, g4, c16);
+  uint32_t rs[4];
+  if (DROP) drop_seeds<TPW>(q, r0, w, g4, c16, rs);
 
   // fc1 tile of this wave: rows 16 i, columns nt * NT1 + 64 cq + 16 j
   const int cq = w;
@@ -228,9 +333,6 @@ void k_qact1(MzQAct q, int row_tiles) {
                                                       0, NT1 * K1 * 2, 0x00020000);
   const int boff = (cq * 4 * 64 + lane) * 16;  // bytes within a chunk's QW1 x 4 KB
   auto load_b = [&](int c, uint4* dh, uint4* dl) {
-#ifdef MZ_QPROBE_NO_BLOAD
-    if (c > 0) return;
-#endif
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int off = boff + c * (QW1 * 4 * 64 * 16) + j * (64 * 16);
@@ -238,86 +340,18 @@ void k_qact1(MzQAct q, int row_tiles) {
       dl[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs_l, off, 0, 0));
     }
   };
-  __syncthreads();  // crow complete
 
-  // stage 1 — the A tile of conv chunk c (pooled position c) into A[c & 1]: conv tiles 4w .. 4w + 3
-  // (tile t: instances 4t .. 4t + 3); A row of this lane = c16: instance 4t + c16 / 4, position
-  // c16 % 4 of its 2x2 pooling window
+  // stage 1 — the A tile of conv chunk c (pooled position c) into A[c & 1]
   auto conv_chunk = [&](int c) {
-    const int py = c / 7, px = c - py * 7;
+    int il[TPW];
+    uint32_t hi[TPW], lo[TPW];
+    conv_chunk_vals<DROP, TPW>(q, c, w, g4, c16, lut, crow, cw, rs, il, hi, lo);
     uint16_t* Ah = A[c & 1][0];
     uint16_t* Al = A[c & 1][1];
-    frag_ab a[TPW];
 #pragma unroll
     for (int tt = 0; tt < TPW; ++tt) {
-      const int inst = 4 * (TPW * w + tt) + (c16 >> 2), pos = c16 & 3;
-      const int y = 2 * py + (pos >> 1), xx = 2 * px + (pos & 1);
-      const uint64_t* cr = crow + inst * PR + y;
-      const uint32_t p = ((uint32_t)(cr[0] >> (3 * xx)) & 0x1FFu) |
-                         (((uint32_t)(cr[1] >> (3 * xx)) & 0x1FFu) << 9) |
-                         (((uint32_t)(cr[2] >> (3 * xx)) & 0x1FFu) << 18);
-#ifdef MZ_QACT_VALU_LUT
-      // the 8 patch bits of this lane's K slice -> 8 bf16 (0 / 1.0) in registers
-      const uint32_t by = (p >> (8 * g4)) & 0xFFu;
-      uint4 v;
-      v.x = __umul24((by & 1u) | (((by >> 1) & 1u) << 16), 0x3F80u);
-      v.y = __umul24(((by >> 2) & 1u) | (((by >> 3) & 1u) << 16), 0x3F80u);
-      v.z = __umul24(((by >> 4) & 1u) | (((by >> 5) & 1u) << 16), 0x3F80u);
-      v.w = __umul24(((by >> 6) & 1u) | (((by >> 7) & 1u) << 16), 0x3F80u);
-      a[tt] = __builtin_bit_cast(frag_ab, v);
-#else
-      a[tt] = __builtin_bit_cast(frag_ab, lut[(p >> (8 * g4)) & 0xFFu]);
-#endif
-    }
-    frag_cd e[TPW], o[TPW];
-#pragma unroll
-    for (int tt = 0; tt < TPW; ++tt) {
-      e[tt] = frag_cd{bias_e, bias_e, bias_e, bias_e};
-      o[tt] = frag_cd{bias_o, bias_o, bias_o, bias_o};
-    }
-#pragma unroll
-    for (int tt = 0; tt < TPW; ++tt) {
-      e[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tt], be_h, e[tt], 0, 0, 0);
-      o[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tt], bo_h, o[tt], 0, 0, 0);
-    }
-#pragma unroll
-    for (int tt = 0; tt < TPW; ++tt) {
-      e[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tt], be_l, e[tt], 0, 0, 0);
-      o[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[tt], bo_l, o[tt], 0, 0, 0);
-    }
-#pragma unroll
-    for (int tt = 0; tt < TPW; ++tt) {
-      // lane: pooled output of instance 4t + g4, channels 2 c16 (e) and 2 c16 + 1 (o);
-      // registers = the 4 positions of its 2x2 window
-      const int il = 4 * (TPW * w + tt) + g4;
-      float ve, vo;
-      if (DROP) {
-        // MaxPool(Dropout(LeakyReLU(x))) = scale * leaky(max_r x'_r), x'_r = x_r kept, 0
-        // dropped (leaky(0) = 0; leaky and the scale are monotonic): the 4 draws of this chunk
-        // from the lane's stream, low half -> even channel, high half -> odd
-        float me = 0.0f, mo = 0.0f;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          uint32_t x = rs[tt];
-          x ^= x << 13;
-          x ^= x >> 17;
-          x ^= x << 5;
-          rs[tt] = x;
-          const float xe = (x & 0xFFFFu) >= q.drop_thresh ? e[tt][r] : 0.0f;
-          const float xo = (x >> 16) >= q.drop_thresh ? o[tt][r] : 0.0f;
-          me = r ? fmaxf(me, xe) : xe;
-          mo = r ? fmaxf(mo, xo) : xo;
-        }
-        ve = leaky(me) * q.drop_scale;
-        vo = leaky(mo) * q.drop_scale;
-      } else {
-        ve = leaky(fmaxf(fmaxf(e[tt][0], e[tt][1]), fmaxf(e[tt][2], e[tt][3])));
-        vo = leaky(fmaxf(fmaxf(o[tt][0], o[tt][1]), fmaxf(o[tt][2], o[tt][3])));
-      }
-      uint32_t hi, lo;
-      split2(ve, vo, hi, lo);
-      reinterpret_cast<uint32_t*>(Ah + il * AST)[c16] = hi;
-      reinterpret_cast<uint32_t*>(Al + il * AST)[c16] = lo;
+      reinterpret_cast<uint32_t*>(Ah + il[tt] * AST)[c16] = hi[tt];
+      reinterpret_cast<uint32_t*>(Al + il[tt] * AST)[c16] = lo[tt];
     }
   };
   // stage 1 of the last chunk: features 1568..1573 = obs6, then zeros
@@ -326,14 +360,8 @@ void k_qact1(MzQAct q, int row_tiles) {
     uint16_t* Al = A[(NCH - 1) & 1][1];
     for (int i = tid; i < RT1 * 16; i += T1) {
       const int r = i >> 4, k2 = (i & 15) * 2;
-      float v0 = 0.0f, v1 = 0.0f;
-      if (r < nr && k2 < 6) {
-        const int inst = q.rows ? q.rows[r0 + r] : r0 + r;
-        v0 = q.obs6[(size_t)inst * 6 + k2];
-        v1 = q.obs6[(size_t)inst * 6 + k2 + 1];
-      }
       uint32_t hi, lo;
-      split2(v0, v1, hi, lo);
+      obs_vals(q, r0, nr, r, k2, hi, lo);
       reinterpret_cast<uint32_t*>(Ah + r * AST)[k2 >> 1] = hi;
       reinterpret_cast<uint32_t*>(Al + r * AST)[k2 >> 1] = lo;
     }
@@ -410,6 +438,153 @@ void k_qact1(MzQAct q, int row_tiles) {
 
   // epilogue: h1 = LeakyReLU(acc + b1) as f32 rows (list order); lane: column 16 j + c16 of the
   // wave's tile, rows 16 i + 4 g4 + reg
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = col0 + 16 * j + c16;
+    const float bb = q.b1[col];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * i + 4 * g4 + r;
+        if (row < nr) q.h1[(size_t)(r0 + row) * N1 + col] = leaky(acc[i][j][r] + bb);
+      }
+  }
+}
+
+// ---- the split forward: k_qconv (the conv stem once per 64-row tile) + k_qfc1 ----------------
+// k_qact1 recomputes the conv stem (and DDQN's dropout draws) in each of its NTL1 = 4 output-tile
+// workgroups of a row tile. The split computes it once: k_qconv writes each row tile's A chunks —
+// exactly the hi / lo bf16 values k_qact1 puts in LDS — to a workspace after h1, feature tiles
+// [row tile][chunk][hi, lo][64 rows][32] (8 KB per tile and chunk, 400 KB per tile), and k_qfc1
+// runs k_qact1's fc1 loop with each chunk's A tile staged from there through LDS (one 16-B load
+// of hi and of lo per thread per chunk). Same values, same MFMA order: the same Q values bit for
+// bit.
+constexpr int FT_CHUNK = 2 * RT1 * 32;  // uint16 per (tile, chunk)
+
+template <bool DROP>
+__global__ __launch_bounds__(T1) void k_qconv(MzQAct q, int row_tiles, uint16_t* __restrict__ feat) {
+  __shared__ uint4 lut[256];
+  __shared__ uint32_t spread[256];
+  __shared__ uint64_t crow[RT1 * PR];
+  __shared__ uint32_t wb[RT1 * 22];
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1);
+  const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);
+  const int g4 = lane >> 4, c16 = lane & 15;
+  const int rt = blockIdx.x;
+  if (rt >= row_tiles) return;
+  const int m = q.count ? min(q.n, *q.count) : q.n;
+  const int r0 = rt * RT1;
+  if (r0 >= m) return;
+  const int nr = min(RT1, m - r0);
+  conv_tables(q, r0, nr, tid, T1, lut, spread, crow, wb);
+  const ConvW cw = conv_weights(q, g4, c16);
+  uint32_t rs[4];
+  if (DROP) drop_seeds<TPW>(q, r0, w, g4, c16, rs);
+  uint16_t* ft = feat + (size_t)rt * NCH * FT_CHUNK;
+  for (int c = 0; c < NCH - 1; ++c) {
+    int il[TPW];
+    uint32_t hi[TPW], lo[TPW];
+    conv_chunk_vals<DROP, TPW>(q, c, w, g4, c16, lut, crow, cw, rs, il, hi, lo);
+    uint32_t* fh = reinterpret_cast<uint32_t*>(ft + (size_t)c * FT_CHUNK);
+    uint32_t* fl = fh + RT1 * 16;
+#pragma unroll
+    for (int tt = 0; tt < TPW; ++tt) {
+      fh[il[tt] * 16 + c16] = hi[tt];
+      fl[il[tt] * 16 + c16] = lo[tt];
+    }
+  }
+  uint32_t* fh = reinterpret_cast<uint32_t*>(ft + (size_t)(NCH - 1) * FT_CHUNK);
+  for (int i = tid; i < RT1 * 16; i += T1) {
+    const int r = i >> 4, k2 = (i & 15) * 2;
+    uint32_t hi, lo;
+    obs_vals(q, r0, nr, r, k2, hi, lo);
+    fh[i] = hi;
+    fh[RT1 * 16 + i] = lo;
+  }
+}
+
+__global__ __launch_bounds__(T1) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void k_qfc1(MzQAct q, int row_tiles, const uint16_t* __restrict__ feat) {
+  __shared__ __align__(16) uint16_t A[2][2][RT1 * AST];  // [buffer][hi, lo][row][k]
+  static_assert(RT1 * 32 / 8 == T1, "one 16-B A load per thread and half-tile");
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1);
+  const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);
+  const int g4 = lane >> 4, c16 = lane & 15;
+  const int b = blockIdx.x, x = b & 7;
+  const int nt = x / XPT, rt = (b >> 3) * XPT + (x % XPT);
+  if (rt >= row_tiles) return;
+  const int m = q.count ? min(q.n, *q.count) : q.n;
+  const int r0 = rt * RT1;
+  if (r0 >= m) return;
+  const int nr = min(RT1, m - r0);
+  const int cq = w;
+  const int col0 = nt * NT1 + cq * 64;
+  frag_cd acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = frag_cd{0.0f, 0.0f, 0.0f, 0.0f};
+  uint4 bh[4], bl[4], nbh[4], nbl[4];
+  const auto rs_h = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(q.w1h) + (size_t)nt * NT1 * K1,
+                                                      0, NT1 * K1 * 2, 0x00020000);
+  const auto rs_l = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(q.w1l) + (size_t)nt * NT1 * K1,
+                                                      0, NT1 * K1 * 2, 0x00020000);
+  const int boff = (cq * 4 * 64 + lane) * 16;
+  auto load_b = [&](int c, uint4* dh, uint4* dl) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int off = boff + c * (QW1 * 4 * 64 * 16) + j * (64 * 16);
+      dh[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs_h, off, 0, 0));
+      dl[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs_l, off, 0, 0));
+    }
+  };
+  // A staging: thread tid <-> 16-B piece tid of the chunk's hi and lo halves (row tid / 4, k
+  // octet tid % 4)
+  const uint4* fsrc = reinterpret_cast<const uint4*>(feat + (size_t)rt * NCH * FT_CHUNK);
+  const int ar = tid >> 2, ao = (tid & 3) * 8;
+  uint4 va_h, va_l;
+  auto load_a = [&](int c) {
+    va_h = fsrc[(size_t)c * (FT_CHUNK / 8) + tid];
+    va_l = fsrc[(size_t)c * (FT_CHUNK / 8) + T1 + tid];
+  };
+  auto store_a = [&](int buf) {
+    *reinterpret_cast<uint4*>(A[buf][0] + ar * AST + ao) = va_h;
+    *reinterpret_cast<uint4*>(A[buf][1] + ar * AST + ao) = va_l;
+  };
+  frag_ab ah[4], al[4];
+  auto fc1_read = [&](int c) {
+    const uint16_t* Ah = A[c & 1][0];
+    const uint16_t* Al = A[c & 1][1];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 16 * i + c16;
+      ah[i] = __builtin_bit_cast(frag_ab, *reinterpret_cast<const uint4*>(Ah + r * AST + 8 * g4));
+      al[i] = __builtin_bit_cast(frag_ab, *reinterpret_cast<const uint4*>(Al + r * AST + 8 * g4));
+    }
+  };
+  load_b(0, bh, bl);
+  load_a(0);
+  store_a(0);
+  __syncthreads();
+  static_assert(NCH % 2 == 0, "loop unrolled by two");
+  for (int c = 0; c < NCH; c += 2) {
+    load_a(c + 1);
+    load_b(c + 1, nbh, nbl);
+    fc1_read(c);
+    mfma_x3(ah, al, bh, bl, acc);
+    store_a(1);
+    __syncthreads();
+    if (c + 2 < NCH) {
+      load_a(c + 2);
+      load_b(c + 2, bh, bl);
+    }
+    fc1_read(c + 1);
+    mfma_x3(ah, al, nbh, nbl, acc);
+    if (c + 2 < NCH) store_a(0);
+    __syncthreads();
+  }
+  // epilogue: as k_qact1
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int col = col0 + 16 * j + c16;
@@ -657,15 +832,35 @@ __global__ __launch_bounds__(256) void k_qact_prep2(const float* __restrict__ w2
 
 int mz_qact_row_tiles(int n) { return (n + RT1 - 1) / RT1; }
 
+// the workspace mz_qact takes: h1 [n][1024] f32, then the split forward's feature tiles
+int64_t mz_qact_ws_floats(int n) {
+  const int64_t rt = (n + RT1 - 1) / RT1;
+  return (int64_t)n * N1 + rt * NCH * FT_CHUNK / 2;
+}
+
+// MZ_QACT_FUSED=1 at build time: k_qact1 (conv recomputed per output tile) instead of the split
+#ifndef MZ_QACT_FUSED
+#define MZ_QACT_FUSED 0
+#endif
+
 hipError_t mz_launch_qact(const MzQAct& q, int relu, hipStream_t s) {
   if (q.n <= 0) return hipSuccess;
   const int rt = (q.n + RT1 - 1) / RT1;
   // 8 workgroups per XPT row tiles: XCD x takes output tile x / XPT of row tile XPT k + x % XPT
   const int blocks1 = 8 * ((rt + XPT - 1) / XPT);
-  if (q.drop_thresh)
-    hipLaunchKernelGGL(k_qact1<true>, dim3(blocks1), dim3(T1), 0, s, q, rt);
-  else
-    hipLaunchKernelGGL(k_qact1<false>, dim3(blocks1), dim3(T1), 0, s, q, rt);
+  if (MZ_QACT_FUSED) {
+    if (q.drop_thresh)
+      hipLaunchKernelGGL(k_qact1<true>, dim3(blocks1), dim3(T1), 0, s, q, rt);
+    else
+      hipLaunchKernelGGL(k_qact1<false>, dim3(blocks1), dim3(T1), 0, s, q, rt);
+  } else {
+    uint16_t* feat = reinterpret_cast<uint16_t*>(q.h1 + (size_t)q.n * N1);
+    if (q.drop_thresh)
+      hipLaunchKernelGGL(k_qconv<true>, dim3(rt), dim3(T1), 0, s, q, rt, feat);
+    else
+      hipLaunchKernelGGL(k_qconv<false>, dim3(rt), dim3(T1), 0, s, q, rt, feat);
+    hipLaunchKernelGGL(k_qfc1, dim3(blocks1), dim3(T1), 0, s, q, rt, feat);
+  }
   const int blocks2 = (q.n + RT2 - 1) / RT2;
   if (relu)
     hipLaunchKernelGGL(k_qact2<true>, dim3(blocks2), dim3(512), 0, s, q);

@@ -45,7 +45,8 @@ EXPORTS = ["mz_last_error", "mz_device_count", "mz_create", "mz_destroy", "mz_lo
            "mz_replay_gather", "mz_host_alloc", "mz_host_free", "mz_q_front_rows", "mz_greedy_rows",
            "mz_trainer_tick", "mz_greedy_scatter", "mz_head_bf16", "mz_replay_push",
            "mz_replay_sample_idx", "mz_q_loss", "mz_q_loss_backward", "mz_adamw_groups",
-           "mz_ppo_act", "mz_ppo_scan", "mz_ppo_finish", "mz_ppo_head_loss", "mz_qact_prepare", "mz_qact"]
+           "mz_ppo_act", "mz_ppo_scan", "mz_ppo_finish", "mz_ppo_head_loss", "mz_qact_prepare", "mz_qact",
+           "mz_qact_workspace_floats"]
 
 _lib = None
 
@@ -125,6 +126,8 @@ def load(build_if_missing=True):
                                   C.c_int32, vp, vp]
     L.mz_stem_backward.argtypes = [vp, vp, vp, C.c_int32, C.c_int32, C.c_float, vp, vp, vp, vp]
     L.mz_stem_workspace_floats.argtypes = [C.c_int32]
+    L.mz_qact_workspace_floats.argtypes = [C.c_int32]
+    L.mz_qact_workspace_floats.restype = C.c_int64
     L.mz_leaky_relu_bf16.argtypes = [vp, C.c_int64, C.c_float, vp]
     L.mz_colsum_f32.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, vp, vp]
     L.mz_replay_gather.argtypes = [vp, C.c_int32, C.c_int64] + [vp] * 11

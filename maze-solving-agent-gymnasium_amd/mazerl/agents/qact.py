@@ -5,11 +5,13 @@ never leave train mode, so DDQN's Dropout(0.2) is active when acting — SURVEY 
 acting head (agents/fused.py FusedQ) picked the f32 argmax on 99.4 % of real trainer states
 (profiles/r03c_acting_precision.json). `QAct` runs the whole forward in two HIP launches with
 every GEMM operand split into bf16 hi + lo and each product summed as hi*hi + hi*lo + lo*hi in f32
-(~2^-16 relative), the conv stem computed from the window bits inside fc1's K loop:
+(~2^-16 relative), the conv stem computed from the window bits once per 64 rows into bf16 hi / lo
+feature tiles that fc1's K loop reads:
 
   mz_qact_prepare  fc1 / fc2 weights -> hi / lo bf16 images (after every weight change)
   mz_qact          Q values of the listed rows (row count read on the device) and the argmax
-                   scattered to the listed instances — no host synchronisation
+                   scattered to the listed instances — no host synchronisation (three launches:
+                   conv stem, fc1, fc2 + fc3 + argmax)
 
 Interface as FusedQ (invalidate / refresh / __call__) plus `rows_greedy` for the greedy-row list.
 """
@@ -73,8 +75,9 @@ class QAct:
         assert bits.dtype == torch.int32 and bits.shape[1] == 22 and bits.is_contiguous()
         obs6 = obs6.contiguous()
         assert obs6.dtype == torch.float32 and obs6.shape == (bits.shape[0], 6)
-        if self.h1 is None or self.h1.shape[0] < n:
-            self.h1 = torch.empty(max(n, 1), N1, dtype=torch.float32, device=bits.device)
+        ws = int(self.lib.mz_qact_workspace_floats(max(n, 1)))  # h1 rows + conv feature tiles
+        if self.h1 is None or self.h1.numel() < ws:
+            self.h1 = torch.empty(ws, dtype=torch.float32, device=bits.device)
         p = float(self.dropout.p) if (self.dropout is not None and self.dropout.training) else 0.0
         cw, cb = self.conv.weight.detach().contiguous(), self.conv.bias.detach().contiguous()
         l0, l1, l2 = self.lin

@@ -13,7 +13,7 @@ HEADER = os.path.join(ROOT, "include", "mazerl.h")
 
 def declared():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(mz_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^(?:int|int64_t|const char\*)\s+(mz_\w+)\s*\(", txt, re.M)))
 
 
 def test_header_declares_api():
