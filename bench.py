@@ -82,6 +82,9 @@ def parse(argv=None):
     ap.add_argument("--train-steps", type=int, default=2400,
                     help="DDQN vector steps for the win-rate half of the metric (0 = skip)")
     ap.add_argument("--eval-mazes", type=int, default=1000)
+    ap.add_argument("--curriculum-steps", type=int, default=2400,
+                    help="DDQN vector steps of the curriculum leg (the reference's change_algorithm "
+                         "training, evaluated under its test(new=True) protocol; 0 = skip)")
     # learner: one update of 1,024 per vector step. Sweep at 2,400 vector steps (training env
     # steps/s, greedy win-rate): 256: 58.0 M, 96.0 % / 512: 54.4 M, 95.0-96.0 % / 1,024: 50.6-
     # 50.8 M, 96.2-96.4 % / 2,048: 40.4 M, 96.5 % / 4,096: 30.4 M, 96.2 % — the win-rate is on its
@@ -139,8 +142,7 @@ def win_rate(a, dev, rank=0, world=1):
     from mazerl import VectorMazeEnv
     from mazerl.agents.dqn import VectorDQNLearner
     from mazerl.distributed import GradAllReduce, broadcast_params
-    from mazerl.trainers.vector_trainer import (VectorOffPolicyTrainer, best_of_mazes, evaluate,
-                                                maze_algorithms, steps_done_epsilon)
+    from mazerl.trainers.vector_trainer import VectorOffPolicyTrainer, best_of_mazes, evaluate
     env = VectorMazeEnv(a.envs, a.dim, enrich=True, device=dev, algorithm=a.algo,
                         seed=0xA11CE + rank * a.envs, done_list=False, window=False,
                         window_bits=True)  # acting reads the bits
@@ -175,21 +177,16 @@ def win_rate(a, dev, rank=0, world=1):
     t6 = time.perf_counter() - t6  # 6 x eval_mazes candidates generated + McClendon on the GPU
     g6, _ = evaluate(L, n, a.dim, a.algo, seed=0x7E580000, eps=0.0, device=dev, mazes=mz6)
     e6, _ = evaluate(L, n, a.dim, a.algo, seed=0x7E580000, eps=0.1, device=dev, mazes=mz6)
-    algos = maze_algorithms(n, seed=0x7E590000)
-    mzr = best_of_mazes(n, a.dim, algos, seed=0x7E590000, device=dev)
-    gr, _ = evaluate(L, n, a.dim, seed=0x7E590000, eps=0.0, device=dev, mazes=mzr)
-    sde = steps_done_epsilon(L, n)
-    er, kr = evaluate(L, n, a.dim, seed=0x7E590000, eps=sde, device=dev, mazes=mzr)
+    proto = reference_protocol(L, n, a.dim, dev, 0x7E590000)
+    proto["training"] = "r-prim only (BASELINE configs[2])"
     return {"greedy": g, "eps_0.1": e, "greedy_best_of_6": g6, "eps_0.1_best_of_6": e6,
-            "new_mazes_reference_protocol": {
-                "greedy": gr, "eps_from_steps_done": er,
-                "eps_start_mean": sde.start_mean, "eps_decay": decay,
-                "algorithms": {x: algos.count(x) for x in sorted(set(algos))},
-                "note": "test(num, new=True): per maze random.choice(ALGOS) + best-of-6 by McClendon "
-                        "difficulty; eps_from_steps_done acts through get_action's epsilon with each "
-                        "maze continuing a training instance's steps_done (episodes side by side "
-                        "here, one after another in the reference); the reference's 99.6 % was "
-                        "measured at 41x41 after 125 single-env episodes (README.md)"},
+            "new_mazes_reference_protocol": dict(proto, note=(
+                "test(num, new=True): per maze random.choice(ALGOS) + best-of-6 by McClendon "
+                "difficulty; eps_from_steps_done acts through get_action's epsilon with each maze "
+                "continuing a training instance's steps_done (episodes side by side here, one "
+                "after another in the reference); the reference's 99.6 % was measured at 41x41 "
+                "after 125 single-env episodes with its change_algorithm curriculum (README.md); "
+                "see curriculum_leg for the curriculum-trained learner")),
             "eval_mazes": n, "variant": "ddqn",
             "ranks": world, "train_vector_steps": a.train_steps + 20,
             "train_seconds_steady": round(secs, 3),
@@ -212,15 +209,65 @@ def win_rate(a, dev, rank=0, world=1):
                     "steps_done)"}
 
 
+def curriculum_leg(a, dev, rank=0, world=1):
+    """The reference's own training protocol for its "new mazes" number: DDQN trained with
+    NeuralOffPolicyTrainer.change_algorithm (off_policy_trainer.py:302-310, per instance here:
+    prim&kill mazes from an instance's 5th win, dfs from its 10th, epsilon_decay x3 / x4), same
+    net, learner and instance count as the win-rate leg, then test(new=True)'s protocol
+    (reference_protocol). With N ranks every rank trains its shard with the gradient all-reduce."""
+    import torch
+    import torch.distributed as dist
+    from mazerl import VectorMazeEnv
+    from mazerl.agents.dqn import VectorDQNLearner
+    from mazerl.distributed import GradAllReduce, broadcast_params
+    from mazerl.trainers.vector_trainer import VectorOffPolicyTrainer
+    env = VectorMazeEnv(a.envs, a.dim, enrich=True, device=dev, algorithm="r-prim",
+                        seed=0xC0CC0000 + rank * a.envs, done_list=False, window=False,
+                        window_bits=True)
+    decay = ((a.dim - 1) * (a.dim - 1) // 2) * 5 / 40.0
+    L = VectorDQNLearner(a.envs, dev, variant="ddqn", lr=1e-3, eps_start=0.95, eps_final=0.1,
+                         eps_decay=decay, gamma=0.7, batch_size=a.batch, capacity=2_000_000,
+                         updates_per_step=a.updates_per_step, target_every=a.target_every,
+                         allreduce=GradAllReduce() if world > 1 else None, overlap=bool(a.overlap),
+                         greedy_rows=bool(a.greedy_rows), acting=a.acting, seed=1)
+    if world > 1:
+        broadcast_params(L.source)
+        L.target.load_state_dict(L.source.state_dict())
+    tr = VectorOffPolicyTrainer(env, L, seed=11 + 7919 * rank, curriculum=True)
+    tr.train(20)
+    if world > 1:
+        dist.barrier()
+    secs = tr.train(a.curriculum_steps)
+    if world > 1:
+        t = torch.tensor([secs], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        secs = float(t.item())
+    algo_mix = (torch.bincount(tr.algo.long(), minlength=3).tolist()
+                if getattr(tr, "algo", None) is not None else None)  # ids: ALGOS (vector_env.py)
+    env.close()
+    if rank != 0:
+        return None
+    log("curriculum-leg evaluation")
+    out = reference_protocol(L, a.eval_mazes, a.dim, dev, 0x7E5D0000)
+    out.update({"training": "change_algorithm curriculum (r-prim -> prim&kill at 5 wins -> dfs at "
+                            "10 wins, per instance)",
+                "train_vector_steps": a.curriculum_steps + 20,
+                "train_env_steps_per_s": a.envs * a.curriculum_steps * world / secs,
+                "instances_per_algorithm_at_end": (dict(zip(["r-prim", "dfs", "prim&kill"], algo_mix))
+                                                   if algo_mix else None),
+                "eval_mazes": a.eval_mazes})
+    return out
+
+
 def config_legs(a, dev, rank=0, world=1):
     """BASELINE configs 4 and 5 at the bench's N (north_star's 8-GPU configs; per rank the share of
     the 8-GPU job: 8,192 and 4,096 instances), each trained for a fixed number of vector steps
     between a barrier + synchronize on each side, whole-node env steps/s = all ranks' env steps /
     the max-over-ranks time; rank 0 then evaluates:
       cfg4  DDQN on 8,192 mixed dfs / r-prim / prim&kill 81x81 mazes per rank (algo = global
-            instance id mod 3, SURVEY §8d), source-net gradients all-reduced over RCCL per update;
-            win-rates under the reference's test(new=True) protocol (mixed algorithms, best-of-6,
-            greedy and epsilon from steps_done);
+            instance id mod 3), 4 updates of 512 per vector step, source-net gradients
+            all-reduced over RCCL per update; win-rates under the reference's test(new=True)
+            protocol (mixed algorithms, best-of-6, greedy and epsilon from steps_done);
       cfg5  PPO on 4,096 toroidal mazes of sizes 17..79 per rank (instance i: 17 + 2 (i mod 32)),
             gradients all-reduced per minibatch; greedy win-rate on fresh mazes as generated and on
             best-of-6 mazes (toroidal_maze_env.py:40-54: difficulty of the bordered maze)."""
@@ -231,7 +278,7 @@ def config_legs(a, dev, rank=0, world=1):
     from mazerl.distributed import GradAllReduce, broadcast_params
     from mazerl.trainers.ppo_trainer import VectorPPOTrainer
     from mazerl.trainers.vector_trainer import (VectorOffPolicyTrainer, best_of_mazes, evaluate,
-                                                make_env, maze_algorithms, steps_done_epsilon)
+                                                make_env)
 
     def timed_train(tr, steps):
         torch.cuda.synchronize()
@@ -256,10 +303,13 @@ def config_legs(a, dev, rank=0, world=1):
                             seed=0x5EED0000 + rank * B, done_list=False, window=False, window_bits=True)
         env.set_algorithm(algo)
         decay = ((dim - 1) * (dim - 1) // 2) * 5 / 40.0
+        # 4 updates of 512 per vector step: at 8,192 instances one update of 2,048 (the same
+        # samples) did not learn in 600 vector steps (0 wins vs 92.3 % greedy,
+        # profiles/r04f_cfg4.jsonl)
         L = VectorDQNLearner(B, dev, variant="ddqn", lr=1e-3, eps_start=0.95, eps_final=0.1,
-                             eps_decay=decay, gamma=0.7, batch_size=2048, capacity=2_000_000,
-                             target_every=13, allreduce=GradAllReduce() if world > 1 else None,
-                             overlap=True, seed=0)
+                             eps_decay=decay, gamma=0.7, batch_size=512, updates_per_step=4,
+                             capacity=2_000_000, target_every=13,
+                             allreduce=GradAllReduce() if world > 1 else None, overlap=True, seed=0)
         if world > 1:
             broadcast_params(L.source)
             L.target.load_state_dict(L.source.state_dict())
@@ -270,16 +320,11 @@ def config_legs(a, dev, rank=0, world=1):
         rec = {"envs_per_gpu": B, "grid": dim, "algo": "mixed (global id mod 3)",
                "vector_steps": a.cfg4_steps, "seconds": round(secs, 3),
                "env_steps_per_s": B * a.cfg4_steps * world / secs, "updates": L.n_updates,
-               "batch": 2048, "grad_allreduce": (dist.get_backend() if world > 1 else None)}
+               "batch": 512, "updates_per_vector_step": 4, "grad_allreduce": (dist.get_backend() if world > 1 else None)}
         if rank == 0:
-            n = a.cfg_eval_mazes
-            algos = maze_algorithms(n, seed=0x7E5A0000)
-            mz = best_of_mazes(n, dim, algos, seed=0x7E5A0000, device=dev)
-            rec["win_rate_reference_protocol_greedy"], _ = evaluate(
-                L, n, dim, seed=0x7E5A0000, eps=0.0, device=dev, mazes=mz)
-            rec["win_rate_reference_protocol_eps_from_steps_done"], _ = evaluate(
-                L, n, dim, seed=0x7E5A0000, eps=steps_done_epsilon(L, n), device=dev, mazes=mz)
-            rec["eval_mazes"] = n
+            rec["win_rate_reference_protocol"] = reference_protocol(L, a.cfg_eval_mazes, dim, dev,
+                                                                    0x7E5A0000)
+            rec["eval_mazes"] = a.cfg_eval_mazes
         out["cfg4"] = rec
         del tr, L
     if "cfg5" in legs:
@@ -312,6 +357,26 @@ def config_legs(a, dev, rank=0, world=1):
             rec["eval_mazes"] = n
         out["cfg5"] = rec
         del tr
+    return out
+
+
+def reference_protocol(L, n, dim, dev, seed):
+    """NeuralOffPolicyTrainer.test(n, new=True) (off_policy_trainer.py:228-263) for learner L: per
+    maze random.choice(ALGOS) and a best-of-6 maze of that algorithm, acting greedy and through
+    get_action's epsilon from steps_done (dqn_agent.py:104-119); rates overall and per algorithm."""
+    import numpy as np
+    from mazerl.trainers.vector_trainer import (best_of_mazes, evaluate, maze_algorithms,
+                                                steps_done_epsilon)
+    algos = maze_algorithms(n, seed=seed)
+    mz = best_of_mazes(n, dim, algos, seed=seed, device=dev)
+    sde = steps_done_epsilon(L, n)
+    out = {"eps_start_mean": sde.start_mean,
+           "algorithms": {x: algos.count(x) for x in sorted(set(algos))}}
+    for name, eps in (("greedy", 0.0), ("eps_from_steps_done", sde)):
+        rate, _, won = evaluate(L, n, dim, seed=seed, eps=eps, device=dev, mazes=mz, return_won=True)
+        out[name] = rate
+        out[name + "_by_algorithm"] = {x: float(np.mean([w for w, al in zip(won, algos) if al == x]))
+                                       for x in sorted(set(algos))}
     return out
 
 
@@ -743,6 +808,12 @@ def main():
         if rank == 0:
             out["win_rate"] = wr
             out["q_head"] = q_head(dev, B)
+    if a.curriculum_steps > 0:
+        if rank == 0:
+            log("DDQN curriculum leg (the reference's new-maze protocol)")
+        cl = curriculum_leg(a, dev, rank, world)
+        if rank == 0:
+            out["curriculum_leg"] = cl
     if a.config_legs:
         cl = config_legs(a, dev, rank, world)
         if rank == 0:

@@ -375,7 +375,7 @@ int mz_maze_complexity(const uint8_t* grid_host, int32_t h, int32_t w, int32_t s
  * the LDS plan holds, a hallway of more than 63 view nodes), 3 invalid (start == goal, bad id,
  * log domain) — the caller computes every nonzero-status maze with mz_difficulty (toroidal: on
  * the bordered grid). Asynchronous on `stream`. Returns MZ_EINVAL_SHAPE when the evaluated grid's
- * pitch exceeds the kernel's LDS plan (P > 92; toroidal P > 85). */
+ * pitch exceeds the kernel's LDS plan (P > 92; toroidal P > 87). */
 int mz_difficulty_batch(mz_handle* h, const int32_t* env_ids_dev, int32_t n, double* out_dev,
                         int32_t* status_dev, void* stream);
 

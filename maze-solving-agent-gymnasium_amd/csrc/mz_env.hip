@@ -710,20 +710,20 @@ __global__ __launch_bounds__(WAVE) void k_bank_fill(MzDev bd, const int* head, i
 // then resets the done instances of its share of them cooperatively, one after another — waves
 // with nothing to do exit at once, no device list or counter is involved. With regen, instances
 // whose last step terminated first get a new maze (win -> update_maze,
-// off_policy_trainer.py:190-202). MZ_RD_SPLIT waves may share a 64-instance group (each resets
-// the done instances of 64 / MZ_RD_SPLIT of its lanes) to shorten the longest chain of resets;
-// inside training the launch's time is mostly waiting for CU slots beside the acting and update
-// kernels, and one wave per group measured best (68.3 / 68.5 vs 67.0 / 67.4 M env steps/s with 4,
-// profiles/r03_adamw_qw8_rd1/train.jsonl).
-#ifndef MZ_RD_SPLIT
-#define MZ_RD_SPLIT 1
-#endif
+// off_policy_trainer.py:190-202). `split` waves share a 64-instance group (each resets the done
+// instances of 64 / split of its lanes), so that the launch has >= ~1,024 waves: a reset is a
+// chain of ~10 dependent global round trips, and a wave runs its share's resets one after
+// another. At 65,536 instances (1,024 groups) split = 1 — inside training the launch's time
+// is mostly waiting for CU slots beside the acting and update kernels, and one wave per group
+// measured best there (68.3 / 68.5 vs 67.0 / 67.4 M env steps/s with 4,
+// profiles/r03_adamw_qw8_rd1/train.jsonl); config 2's 4,096 instances (64 groups) spent 218 us
+// per vector step here with one wave per group (profiles/r04f_cfg2_train_streams.json).
 template <bool TOR, bool ENRICH>
 __global__ __launch_bounds__(WAVE) void k_reset_done(MzDev d, int regen, uint64_t seed,
-                                                     uint32_t epoch, MzOut o) {
+                                                     uint32_t epoch, MzOut o, int split) {
   extern __shared__ __align__(16) uint8_t lds[];
   __shared__ __align__(16) uint32_t wsh[32];
-  const int grp = blockIdx.x / MZ_RD_SPLIT, part = blockIdx.x - grp * MZ_RD_SPLIT;
+  const int grp = blockIdx.x / split, part = blockIdx.x - grp * split;
   const int lane = threadIdx.x, e = grp * WAVE + lane;
   const bool done = e < d.B && ((d.posw[e] >> 20) & 1u);
   const bool win = regen && done && d.last_term[e];  // gets a new maze (loaded once, coalesced)
@@ -740,7 +740,7 @@ __global__ __launch_bounds__(WAVE) void k_reset_done(MzDev d, int regen, uint64_
       pend &= ~m;
     }
   }
-  constexpr int SH = WAVE / MZ_RD_SPLIT;
+  const int SH = WAVE / split;
   const unsigned long long share = (~0ull >> (WAVE - SH)) << (part * SH);
   unsigned long long bal = __ballot(done) & share;
   while (bal) {
@@ -1011,7 +1011,10 @@ hipError_t mz_launch_reset_list(const MzDev& d, const int32_t* idx, int32_t* cou
 
 hipError_t mz_launch_reset_done(const MzDev& d, int regen, uint64_t seed, uint32_t epoch,
                                 const MzOut& o, hipStream_t s) {
-  const int blocks = (d.B + WAVE - 1) / WAVE * MZ_RD_SPLIT;  // MZ_RD_SPLIT waves per 64 instances
+  const int groups = (d.B + WAVE - 1) / WAVE;
+  int split = 1;  // waves per 64-instance group: >= 1,024 waves in the launch
+  while (split < WAVE && groups * split < 1024) split <<= 1;
+  const int blocks = groups * split;
   size_t lds = 0;
   hipError_t ae = hipSuccess;
   if (regen && d.bk_K) {  // the winners' bank slots, in instance order (k_bank_count / k_bank_scan)
@@ -1028,7 +1031,7 @@ hipError_t mz_launch_reset_done(const MzDev& d, int regen, uint64_t seed, uint32
       if (ae != hipSuccess) return ae;                                                        \
     }                                                                                         \
     hipLaunchKernelGGL((k_reset_done<T, E>), dim3(blocks), dim3(WAVE), lds, s, d, regen, seed, \
-                       epoch, o);                                                             \
+                       epoch, o, split);                                                      \
   } while (0)
   if (d.toroidal) { if (d.enrich) MZ_RD(true, true); else MZ_RD(true, false); }
   else { if (d.enrich) MZ_RD(false, true); else MZ_RD(false, false); }

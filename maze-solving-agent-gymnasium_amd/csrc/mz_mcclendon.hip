@@ -34,7 +34,8 @@
 // Toroidal handles are scored as the reference scores them: the bordered (N + 2)^2 maze, the
 // crop inside a wall ring with start / goal shifted by +1 (gen_maze_no_border, maze_generation.
 // py:49-51; off_policy_trainer.py:194-196) — a perfect maze whose distance field to the goal comes
-// from a bit-parallel BFS over 128-bit rows here (the handle's cell words hold torus distances).
+// from a bit-parallel BFS over 128-bit rows held in one wave's registers here (the handle's cell
+// words hold torus distances).
 // Output per maze: the product and the sum before the log (prod_b (C_b + 1) * C_0 and
 // sum_b C_b + C_0); the caller takes math.log (glibc, as the reference) of both. Non-tree mazes
 // and mazes beyond the LDS / register budgets report a status and are left to the host
@@ -267,14 +268,10 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
   uint16_t* pos = gp + NNP;                                          // [NNP] node position
   uint32_t* fst = reinterpret_cast<uint32_t*>(pos + NNP);          // [NNP] first dead-end rank
   uint8_t* fl = reinterpret_cast<uint8_t*>(fst + NNP);              // [NNP] flags
-  // toroidal: the bordered grid's distance field to the goal and the BFS rows
+  // toroidal: the bordered grid's distance field to the goal
   const size_t tor_off = ((size_t)NNP * 9 + 16 + 15) & ~(size_t)15;
   uint16_t* tdist = reinterpret_cast<uint16_t*>(lds + tor_off);     // [NNP]
-  u128* rO = reinterpret_cast<u128*>(lds + tor_off + (((size_t)NNP * 2 + 15) & ~(size_t)15));
-  u128* rV = rO + Pb;
-  u128* rF = rV + Pb;                                                // [2][Pb] frontiers
-  const size_t sq_bytes = tor ? tor_off + (((size_t)NNP * 2 + 15) & ~(size_t)15) + 64 * (size_t)Pb
-                              : tor_off,
+  const size_t sq_bytes = tor ? tor_off + (((size_t)NNP * 2 + 15) & ~(size_t)15) : tor_off,
                ph2_bytes = (size_t)MM * 36;
   unsigned char* nb = lds + (sq_bytes > ph2_bytes ? sq_bytes : ph2_bytes);  // node region
   uint64_t* keys = reinterpret_cast<uint64_t*>(nb);                  // [MM] sort buffer
@@ -312,44 +309,63 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
   }
   if (tor) {
     // distances to the goal on the bordered grid: BFS over 128-bit rows (a level = shift / or /
-    // and-not of the frontier rows), one row per thread, no wrap (the ring is wall)
+    // and-not of the frontier rows), no wrap (the ring is wall), by ONE wave with the rows in
+    // registers — lane l holds rows l and 64 + l, the neighbour rows come by lane shuffles — so a
+    // level costs no barrier (a dfs maze has ~3,000 levels; a workgroup barrier per level made
+    // this BFS the kernel's longest phase)
     for (int q = threadIdx.x; q < NN; q += T) tdist[q] = 0xFFFF;
-    for (int y = threadIdx.x; y < N; y += T) {
-      u128 ob = 0;
-      for (int x = 0; x < N; ++x)
-        if (sq_open(y * N + x)) ob |= (u128)1 << x;
-      const u128 g = y == gr ? (u128)1 << gc : (u128)0;
-      rO[y] = ob;
-      rV[y] = g;
-      rF[y] = g;
-    }
     __syncthreads();
-    if (threadIdx.x == 0) tdist[goal] = 0;
-    int cur = 0;
-    for (int level = 1;; ++level) {
-      const u128* Fc = rF + cur * Pb;
-      u128* Fn = rF + (cur ^ 1) * Pb;
-      int any = 0;
-      for (int y = threadIdx.x; y < N; y += T) {
-        const u128 f = Fc[y];
-        u128 reach = f | (f << 1) | (f >> 1);
-        if (y > 0) reach |= Fc[y - 1];
-        if (y + 1 < N) reach |= Fc[y + 1];
-        u128 nw = reach & rO[y] & ~rV[y];
-        Fn[y] = nw;
-        if (nw) {
-          any = 1;
-          rV[y] |= nw;
-          while (nw) {
-            const uint64_t lo = (uint64_t)nw, hi = (uint64_t)(nw >> 64);
-            const int x = lo ? __ffsll((long long)lo) - 1 : 64 + __ffsll((long long)hi) - 1;
-            tdist[y * N + x] = (uint16_t)level;
-            nw &= nw - 1;
-          }
+    if (threadIdx.x < WAVE) {
+      const int lane = threadIdx.x;
+      auto row_open = [&](int y) -> u128 {
+        u128 ob = 0;
+        if (y < N)
+          for (int x = 0; x < N; ++x)
+            if (sq_open(y * N + x)) ob |= (u128)1 << x;
+        return ob;
+      };
+      const u128 O0 = row_open(lane), O1 = row_open(64 + lane);
+      u128 F0 = lane == gr ? (u128)1 << gc : (u128)0;
+      u128 F1 = 64 + lane == gr ? (u128)1 << gc : (u128)0;
+      u128 V0 = F0, V1 = F1;
+      if (lane == 0) tdist[goal] = 0;
+      auto shfl128 = [&](u128 v, int src) -> u128 {
+        u128 r = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          r |= (u128)(uint32_t)__shfl((int)(uint32_t)(v >> (32 * k)), src) << (32 * k);
+        return r;
+      };
+      auto mark = [&](u128 nw, int y, int level) {
+        while (nw) {
+          const uint64_t lo = (uint64_t)nw, hi = (uint64_t)(nw >> 64);
+          const int x = lo ? __ffsll((long long)lo) - 1 : 64 + __ffsll((long long)hi) - 1;
+          tdist[y * N + x] = (uint16_t)level;
+          nw &= nw - 1;
         }
+      };
+      for (int level = 1;; ++level) {
+        // row y - 1 of row lane: lane - 1's row 0 part (lane 0: none); of row 64 + lane: lane - 1's
+        // row 1 part (lane 0: lane 63's row 0 part). Row y + 1 of row lane: lane + 1's row 0 part
+        // (lane 63: lane 0's row 1 part); of row 64 + lane: lane + 1's row 1 part (lane 63: none)
+        const u128 a0 = shfl128(F0, (lane + WAVE - 1) & (WAVE - 1));
+        const u128 a1 = shfl128(F1, (lane + WAVE - 1) & (WAVE - 1));
+        const u128 b0 = shfl128(F0, (lane + 1) & (WAVE - 1));
+        const u128 b1 = shfl128(F1, (lane + 1) & (WAVE - 1));
+        const u128 up0 = lane == 0 ? (u128)0 : a0;
+        const u128 up1 = lane == 0 ? a0 : a1;  // lane 0: row 63 = lane 63's row 0 part
+        const u128 dn0 = lane == WAVE - 1 ? b1 : b0;  // lane 63: row 64 = lane 0's row 1 part
+        const u128 dn1 = lane == WAVE - 1 ? (u128)0 : b1;
+        const u128 n0 = (F0 | (F0 << 1) | (F0 >> 1) | up0 | dn0) & O0 & ~V0;
+        const u128 n1 = (F1 | (F1 << 1) | (F1 >> 1) | up1 | dn1) & O1 & ~V1;
+        V0 |= n0;
+        V1 |= n1;
+        F0 = n0;
+        F1 = n1;
+        mark(n0, lane, level);
+        mark(n1, 64 + lane, level);
+        if (!__any((n0 | n1) != 0)) break;
       }
-      if (!__syncthreads_or(any)) break;
-      cur ^= 1;
     }
   }
   auto sq_dist = [&](int q) -> int {  // BFS distance to the goal (MZ_CELL_D_MASK: unreachable)
@@ -856,7 +872,7 @@ size_t mz_mcclendon_lds(int P, bool toroidal, int* mm) {
   *mm = MM;
   const size_t NNP = (size_t)Pb * Pb;
   size_t sq = (NNP * 9 + 16 + 15) & ~(size_t)15;
-  if (toroidal) sq += ((NNP * 2 + 15) & ~(size_t)15) + 64 * (size_t)Pb;  // distances + BFS rows
+  if (toroidal) sq += (NNP * 2 + 15) & ~(size_t)15;  // the distance field
   const size_t node = (size_t)MM * (8 + 2 + 8 + 8 + 2 + 2 + 2 + 1 + 1);
   const size_t ph2 = (size_t)MM * (2 * 6 + 4 * 2 + 8 * 2);
   return (sq > ph2 ? sq : ph2) + node;

@@ -287,11 +287,13 @@ def steps_done_epsilon(learner, num_mazes):
 
 @torch.no_grad()
 def evaluate(learner, num_mazes, dim, algorithm="r-prim", seed=0x7E57, eps=0.0, toroidal=False,
-             device=None, max_vector_steps=None, mazes=None):
+             device=None, max_vector_steps=None, mazes=None, return_won=False):
     """Fraction of `num_mazes` fresh mazes solved in one episode (terminated before truncation).
     `dim` may be a list of sizes (instance i gets dim[i % len]). `mazes` = best_of_mazes' output
     to play instead of generated ones (the reference's best-of-6 selection). `eps` is a number or
-    a callable k -> per-maze epsilon tensor for the k-th action (steps_done_epsilon)."""
+    a callable k -> per-maze epsilon tensor for the k-th action (steps_done_epsilon).
+    Returns (rate, vector steps) or, with return_won, (rate, vector steps, won bool [n] on the
+    host)."""
     bits = getattr(learner, "supports_bits", False)
     algo0 = algorithm if isinstance(algorithm, str) else "r-prim"
     env = make_env(num_mazes, dim, toroidal=toroidal, algorithm=algo0, seed=seed,
@@ -316,4 +318,6 @@ def evaluate(learner, num_mazes, dim, algorithm="r-prim", seed=0x7E57, eps=0.0, 
             break
     rate = float(won.float().mean())
     env.close()
+    if return_won:
+        return rate, k, won.cpu().numpy()
     return rate, k
