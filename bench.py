@@ -82,6 +82,10 @@ def parse(argv=None):
     ap.add_argument("--train-steps", type=int, default=2400,
                     help="DDQN vector steps for the win-rate half of the metric (0 = skip)")
     ap.add_argument("--eval-mazes", type=int, default=1000)
+    ap.add_argument("--curriculum-envs", type=int, default=4096)
+    ap.add_argument("--curriculum-dim", type=int, default=41)
+    ap.add_argument("--curriculum-updates", type=int, default=4)
+    ap.add_argument("--curriculum-batch", type=int, default=1024)
     ap.add_argument("--curriculum-steps", type=int, default=2400,
                     help="DDQN vector steps of the curriculum leg (the reference's change_algorithm "
                          "training, evaluated under its test(new=True) protocol; 0 = skip)")
@@ -210,24 +214,30 @@ def win_rate(a, dev, rank=0, world=1):
 
 
 def curriculum_leg(a, dev, rank=0, world=1):
-    """The reference's own training protocol for its "new mazes" number: DDQN trained with
-    NeuralOffPolicyTrainer.change_algorithm (off_policy_trainer.py:302-310, per instance here:
-    prim&kill mazes from an instance's 5th win, dfs from its 10th, epsilon_decay x3 / x4), same
-    net, learner and instance count as the win-rate leg, then test(new=True)'s protocol
-    (reference_protocol). With N ranks every rank trains its shard with the gradient all-reduce."""
+    """The reference's own protocol for its "new mazes" number (README: 99.6 % for DDQN at 41x41):
+    DDQN trained with NeuralOffPolicyTrainer.change_algorithm (off_policy_trainer.py:302-310, per
+    instance here: prim&kill mazes from an instance's 5th win, dfs from its 10th, epsilon_decay
+    x3 / x4) at the reference example's 41x41 grid (training_examples/euclidean_mazes/
+    costant_sizes/test_ddqn.py:20-27; its epsilon_decay ((N-1)^2 // 2) * 5), then test(new=True)'s
+    protocol (reference_protocol). The reference trains one update of 128 per env step; here
+    --curriculum-envs instances with --curriculum-updates updates of --curriculum-batch per
+    vector step (default 4,096 x 4 x 1,024: one sample per env step). With N ranks every rank
+    trains its shard with the gradient all-reduce."""
     import torch
     import torch.distributed as dist
     from mazerl import VectorMazeEnv
     from mazerl.agents.dqn import VectorDQNLearner
     from mazerl.distributed import GradAllReduce, broadcast_params
     from mazerl.trainers.vector_trainer import VectorOffPolicyTrainer
-    env = VectorMazeEnv(a.envs, a.dim, enrich=True, device=dev, algorithm="r-prim",
-                        seed=0xC0CC0000 + rank * a.envs, done_list=False, window=False,
+    B, dim = a.curriculum_envs, a.curriculum_dim
+    env = VectorMazeEnv(B, dim, enrich=True, device=dev, algorithm="r-prim",
+                        seed=0xC0CC0000 + rank * B, done_list=False, window=False,
                         window_bits=True)
-    decay = ((a.dim - 1) * (a.dim - 1) // 2) * 5 / 40.0
-    L = VectorDQNLearner(a.envs, dev, variant="ddqn", lr=1e-3, eps_start=0.95, eps_final=0.1,
-                         eps_decay=decay, gamma=0.7, batch_size=a.batch, capacity=2_000_000,
-                         updates_per_step=a.updates_per_step, target_every=a.target_every,
+    decay = ((dim - 1) * (dim - 1) // 2) * 5
+    L = VectorDQNLearner(B, dev, variant="ddqn", lr=1e-3, eps_start=0.95, eps_final=0.1,
+                         eps_decay=decay, gamma=0.7, batch_size=a.curriculum_batch,
+                         capacity=2_000_000, updates_per_step=a.curriculum_updates,
+                         target_every=a.target_every,
                          allreduce=GradAllReduce() if world > 1 else None, overlap=bool(a.overlap),
                          greedy_rows=bool(a.greedy_rows), acting=a.acting, seed=1)
     if world > 1:
@@ -248,11 +258,13 @@ def curriculum_leg(a, dev, rank=0, world=1):
     if rank != 0:
         return None
     log("curriculum-leg evaluation")
-    out = reference_protocol(L, a.eval_mazes, a.dim, dev, 0x7E5D0000)
+    out = reference_protocol(L, a.eval_mazes, dim, dev, 0x7E5D0000)
     out.update({"training": "change_algorithm curriculum (r-prim -> prim&kill at 5 wins -> dfs at "
                             "10 wins, per instance)",
+                "grid": dim, "envs_per_gpu": B, "epsilon_decay": decay,
+                "updates_per_vector_step": a.curriculum_updates, "batch": a.curriculum_batch,
                 "train_vector_steps": a.curriculum_steps + 20,
-                "train_env_steps_per_s": a.envs * a.curriculum_steps * world / secs,
+                "train_env_steps_per_s": B * a.curriculum_steps * world / secs,
                 "instances_per_algorithm_at_end": (dict(zip(["r-prim", "dfs", "prim&kill"], algo_mix))
                                                    if algo_mix else None),
                 "eval_mazes": a.eval_mazes})
