@@ -12,9 +12,11 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 export PYTHONPATH="$GRAFT_REPO_ROOT/maze-solving-agent-gymnasium_amd:$PYTHONPATH"
 O=gpurun_out/prof
 mkdir -p $O
-ARGS="--steps 300 --warmup 30 --train-steps 0 --no-cpu-baseline"
+ARGS="--steps 300 --warmup 30 --train-steps 0 --curriculum-steps 0 --config-legs= --no-cpu-baseline"
+# the kernel trace with the bench's captured-graph replays; the counter passes with eager launches
+# (the same k_step launch, one dispatch at a time under counter collection)
 for leg in window bits; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/kt_$leg -o run -- python3 bench.py $ARGS --legs $leg > $O/kt_$leg.log 2>&1
-  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -f csv -d $O/fetch_$leg -o run -- python3 bench.py $ARGS --legs $leg > $O/fetch_$leg.log 2>&1
-  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -f csv -d $O/write_$leg -o run -- python3 bench.py $ARGS --legs $leg > $O/write_$leg.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -f csv -d $O/fetch_$leg -o run -- python3 bench.py $ARGS --graph 0 --legs $leg > $O/fetch_$leg.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -f csv -d $O/write_$leg -o run -- python3 bench.py $ARGS --graph 0 --legs $leg > $O/write_$leg.log 2>&1
 done
