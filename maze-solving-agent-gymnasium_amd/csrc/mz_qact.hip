@@ -191,9 +191,10 @@ __device__ inline ConvW conv_weights(const MzQAct& q, int g4, int c16) {
   return cw;
 }
 
-// dropout streams (DDQN): one xorshift32 stream per (row, channel pair) — this lane's rows
-// 4 (TPWv w + tt) + g4, pair c16 — seeded lowbias32(lowbias32(key ^ lowbias32(row)) ^ pair) | 1,
-// four draws per pooled position in chunk order
+// dropout draws (DDQN): per (row, channel pair, pooled position c) one xorshift32 stream of four
+// draws, seeded lowbias32(base ^ c * 0x9E3779B9) | 1 from the (row, pair) base
+// lowbias32(lowbias32(key ^ lowbias32(row)) ^ pair) | 1 — counter-based, so any chunk can be
+// computed by any workgroup (k_qconv splits a row tile's chunks over several)
 template <int TPWv>
 __device__ inline void drop_seeds(const MzQAct& q, int r0, int w, int g4, int c16, uint32_t (&rs)[4]) {
 #pragma unroll
@@ -250,16 +251,15 @@ __device__ inline void conv_chunk_vals(const MzQAct& q, int c, int w, int g4, in
     float ve, vo;
     if (DROP) {
       // MaxPool(Dropout(LeakyReLU(x))) = scale * leaky(max_r x'_r), x'_r = x_r kept, 0 dropped
-      // (leaky(0) = 0; leaky and the scale are monotonic): the 4 draws of this chunk from the
-      // lane's stream, low half -> even channel, high half -> odd
+      // (leaky(0) = 0; leaky and the scale are monotonic): the 4 draws of this chunk's stream,
+      // low half -> even channel, high half -> odd
       float me = 0.0f, mo = 0.0f;
+      uint32_t x = lowbias32(rs[tt] ^ ((uint32_t)c * 0x9E3779B9u)) | 1u;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        uint32_t x = rs[tt];
         x ^= x << 13;
         x ^= x >> 17;
         x ^= x << 5;
-        rs[tt] = x;
         const float xe = (x & 0xFFFFu) >= q.drop_thresh ? e[tt][r] : 0.0f;
         const float xo = (x >> 16) >= q.drop_thresh ? o[tt][r] : 0.0f;
         me = r ? fmaxf(me, xe) : xe;
@@ -462,8 +462,12 @@ void k_qact1(MzQAct q, int row_tiles) {
 // bit.
 constexpr int FT_CHUNK = 2 * RT1 * 32;  // uint16 per (tile, chunk)
 
+
+// grid: row tiles x `groups` chunk groups (small batches: a row tile's 50 chunks over several
+// workgroups, so that a few thousand rows still fill the chip)
 template <bool DROP>
-__global__ __launch_bounds__(T1) void k_qconv(MzQAct q, int row_tiles, uint16_t* __restrict__ feat) {
+__global__ __launch_bounds__(T1) void k_qconv(MzQAct q, int row_tiles, int groups,
+                                              uint16_t* __restrict__ feat) {
   __shared__ uint4 lut[256];
   __shared__ uint32_t spread[256];
   __shared__ uint64_t crow[RT1 * PR];
@@ -471,18 +475,20 @@ __global__ __launch_bounds__(T1) void k_qconv(MzQAct q, int row_tiles, uint16_t*
   const int tid = threadIdx.x, lane = tid & (WAVE - 1);
   const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);
   const int g4 = lane >> 4, c16 = lane & 15;
-  const int rt = blockIdx.x;
+  const int rt = blockIdx.x / groups, grp = blockIdx.x - rt * groups;
   if (rt >= row_tiles) return;
   const int m = q.count ? min(q.n, *q.count) : q.n;
   const int r0 = rt * RT1;
   if (r0 >= m) return;
   const int nr = min(RT1, m - r0);
+  const int per = (NCH + groups - 1) / groups;
+  const int c0 = grp * per, c1 = min(NCH, c0 + per);
   conv_tables(q, r0, nr, tid, T1, lut, spread, crow, wb);
   const ConvW cw = conv_weights(q, g4, c16);
   uint32_t rs[4];
   if (DROP) drop_seeds<TPW>(q, r0, w, g4, c16, rs);
   uint16_t* ft = feat + (size_t)rt * NCH * FT_CHUNK;
-  for (int c = 0; c < NCH - 1; ++c) {
+  for (int c = c0; c < min(c1, NCH - 1); ++c) {
     int il[TPW];
     uint32_t hi[TPW], lo[TPW];
     conv_chunk_vals<DROP, TPW>(q, c, w, g4, c16, lut, crow, cw, rs, il, hi, lo);
@@ -494,13 +500,15 @@ __global__ __launch_bounds__(T1) void k_qconv(MzQAct q, int row_tiles, uint16_t*
       fl[il[tt] * 16 + c16] = lo[tt];
     }
   }
-  uint32_t* fh = reinterpret_cast<uint32_t*>(ft + (size_t)(NCH - 1) * FT_CHUNK);
-  for (int i = tid; i < RT1 * 16; i += T1) {
-    const int r = i >> 4, k2 = (i & 15) * 2;
-    uint32_t hi, lo;
-    obs_vals(q, r0, nr, r, k2, hi, lo);
-    fh[i] = hi;
-    fh[RT1 * 16 + i] = lo;
+  if (c1 == NCH) {  // the obs6 chunk
+    uint32_t* fh = reinterpret_cast<uint32_t*>(ft + (size_t)(NCH - 1) * FT_CHUNK);
+    for (int i = tid; i < RT1 * 16; i += T1) {
+      const int r = i >> 4, k2 = (i & 15) * 2;
+      uint32_t hi, lo;
+      obs_vals(q, r0, nr, r, k2, hi, lo);
+      fh[i] = hi;
+      fh[RT1 * 16 + i] = lo;
+    }
   }
 }
 
@@ -543,15 +551,6 @@ void k_qfc1(MzQAct q, int row_tiles, const uint16_t* __restrict__ feat) {
   // octet tid % 4)
   const uint4* fsrc = reinterpret_cast<const uint4*>(feat + (size_t)rt * NCH * FT_CHUNK);
   const int ar = tid >> 2, ao = (tid & 3) * 8;
-  uint4 va_h, va_l;
-  auto load_a = [&](int c) {
-    va_h = fsrc[(size_t)c * (FT_CHUNK / 8) + tid];
-    va_l = fsrc[(size_t)c * (FT_CHUNK / 8) + T1 + tid];
-  };
-  auto store_a = [&](int buf) {
-    *reinterpret_cast<uint4*>(A[buf][0] + ar * AST + ao) = va_h;
-    *reinterpret_cast<uint4*>(A[buf][1] + ar * AST + ao) = va_l;
-  };
   frag_ab ah[4], al[4];
   auto fc1_read = [&](int c) {
     const uint16_t* Ah = A[c & 1][0];
@@ -563,25 +562,40 @@ void k_qfc1(MzQAct q, int row_tiles, const uint16_t* __restrict__ feat) {
       al[i] = __builtin_bit_cast(frag_ab, *reinterpret_cast<const uint4*>(Al + r * AST + 8 * g4));
     }
   };
-  load_b(0, bh, bl);
-  load_a(0);
-  store_a(0);
-  __syncthreads();
   static_assert(NCH % 2 == 0, "loop unrolled by two");
+  // A tiles staged through LDS (one 16-B piece of hi and of lo per thread), each loaded into
+  // registers two chunks ahead of its LDS store (slots r0 / r1): all waves read the same 8 KB,
+  // so LDS staging beats per-wave fragment loads (70.7-71.0 vs 73.0-73.4 M env steps/s in
+  // training), and the two-chunk distance beats one (74.5-74.9 vs 73.0-73.4 M; the forward alone
+  // 1.04 vs 1.10 ms at 65,536 rows) — profiles/r04l/ — with the Q values bit for bit the same
+  uint4 r0h, r0l, r1h, r1l;
+  auto ld = [&](int c, uint4& h, uint4& l) {
+    h = fsrc[(size_t)c * (FT_CHUNK / 8) + tid];
+    l = fsrc[(size_t)c * (FT_CHUNK / 8) + T1 + tid];
+  };
+  auto st = [&](int buf, const uint4& h, const uint4& l) {
+    *reinterpret_cast<uint4*>(A[buf][0] + ar * AST + ao) = h;
+    *reinterpret_cast<uint4*>(A[buf][1] + ar * AST + ao) = l;
+  };
+  ld(0, r0h, r0l);
+  st(0, r0h, r0l);
+  ld(1, r1h, r1l);
+  ld(2, r0h, r0l);
+  load_b(0, bh, bl);
+  __syncthreads();
   for (int c = 0; c < NCH; c += 2) {
-    load_a(c + 1);
+    // chunk c in LDS buffer 0; r1 = chunk c + 1, r0 = chunk c + 2
     load_b(c + 1, nbh, nbl);
     fc1_read(c);
     mfma_x3(ah, al, bh, bl, acc);
-    store_a(1);
+    st(1, r1h, r1l);
+    if (c + 3 < NCH) ld(c + 3, r1h, r1l);
     __syncthreads();
-    if (c + 2 < NCH) {
-      load_a(c + 2);
-      load_b(c + 2, bh, bl);
-    }
+    if (c + 2 < NCH) load_b(c + 2, bh, bl);
     fc1_read(c + 1);
     mfma_x3(ah, al, nbh, nbl, acc);
-    if (c + 2 < NCH) store_a(0);
+    if (c + 2 < NCH) st(0, r0h, r0l);
+    if (c + 4 < NCH) ld(c + 4, r0h, r0l);
     __syncthreads();
   }
   // epilogue: as k_qact1
@@ -855,10 +869,12 @@ hipError_t mz_launch_qact(const MzQAct& q, int relu, hipStream_t s) {
       hipLaunchKernelGGL(k_qact1<false>, dim3(blocks1), dim3(T1), 0, s, q, rt);
   } else {
     uint16_t* feat = reinterpret_cast<uint16_t*>(q.h1 + (size_t)q.n * N1);
+    int groups = 1;  // chunk groups per row tile: >= ~512 workgroups (at most 10 chunks apart)
+    while (groups < 5 && rt * groups < 512) ++groups;
     if (q.drop_thresh)
-      hipLaunchKernelGGL(k_qconv<true>, dim3(rt), dim3(T1), 0, s, q, rt, feat);
+      hipLaunchKernelGGL(k_qconv<true>, dim3(rt * groups), dim3(T1), 0, s, q, rt, groups, feat);
     else
-      hipLaunchKernelGGL(k_qconv<false>, dim3(rt), dim3(T1), 0, s, q, rt, feat);
+      hipLaunchKernelGGL(k_qconv<false>, dim3(rt * groups), dim3(T1), 0, s, q, rt, groups, feat);
     hipLaunchKernelGGL(k_qfc1, dim3(blocks1), dim3(T1), 0, s, q, rt, feat);
   }
   const int blocks2 = (q.n + RT2 - 1) / RT2;

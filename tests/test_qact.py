@@ -102,7 +102,8 @@ def _lowbias32(x):
 
 def test_qact_ddqn_dropout_masks():
     """DDQN acts in train mode (Dropout(0.2) after the conv activation): the
-    kernel's keep decisions are a counter hash of (seed, counter, row, feature, 2x2 position);
+    kernel's keep decisions are a counter hash of (seed, counter, row, channel pair, pooled
+    position) feeding a 4-draw xorshift32 stream per 2x2 window;
     rebuilt here, applied to the f32 torch stem (conv -> LeakyReLU -> mask * 1/(1-p) -> MaxPool)
     the Q values agree to the same tolerance, and P(drop) = 13107/65536."""
     from mazerl.agents.nets import QNet
@@ -117,11 +118,13 @@ def test_qact_ddqn_dropout_masks():
     k = (77 * 0x9E3779B97F4A7C15 + 0 * 0xD1B54A32D192ED03 + 1) & (2**64 - 1)
     key = np.uint64((k ^ (k >> 32)) & 0xFFFFFFFF)
     rkey = _lowbias32(key ^ _lowbias32(np.arange(n, dtype=np.uint64)))  # [n]
-    # one xorshift32 stream per (row, channel pair), 4 draws per pooled position in order:
-    # draw r (= 2 dy + dx) -> low half: even channel, high half: odd channel
-    st = _lowbias32(rkey[:, None] ^ np.arange(16, dtype=np.uint64)[None]) | 1  # [n, 16]
+    # per (row, channel pair, pooled position) one xorshift32 stream of 4 draws, seeded from the
+    # (row, pair) base and the position: draw r (= 2 dy + dx) -> low half: even channel, high
+    # half: odd channel
+    base = _lowbias32(rkey[:, None] ^ np.arange(16, dtype=np.uint64)[None]) | 1  # [n, 16]
     keep = np.zeros((n, 49, 32, 2, 2), bool)
     for qi in range(49):
+        st = _lowbias32(base ^ np.uint64((qi * 0x9E3779B9) & 0xFFFFFFFF)) | 1
         for r in range(4):
             st ^= (st << 13) & 0xFFFFFFFF
             st ^= st >> 17
