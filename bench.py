@@ -163,7 +163,7 @@ def win_rate(a, dev, rank=0, world=1):
     tr.train(20)  # warm-up: MIOpen / hipBLASLt first calls
     if world > 1:
         dist.barrier()
-    secs = tr.train(a.train_steps)
+    secs = tr.train(a.train_steps, **progress(rank, "win-rate leg"))
     if world > 1:
         t = torch.tensor([secs], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -247,7 +247,7 @@ def curriculum_leg(a, dev, rank=0, world=1):
     tr.train(20)
     if world > 1:
         dist.barrier()
-    secs = tr.train(a.curriculum_steps)
+    secs = tr.train(a.curriculum_steps, **progress(rank, "curriculum leg"))
     if world > 1:
         t = torch.tensor([secs], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -292,11 +292,11 @@ def config_legs(a, dev, rank=0, world=1):
     from mazerl.trainers.vector_trainer import (VectorOffPolicyTrainer, best_of_mazes, evaluate,
                                                 make_env)
 
-    def timed_train(tr, steps):
+    def timed_train(tr, steps, name):
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
-        secs = tr.train(steps)
+        secs = tr.train(steps, **progress(rank, name))
         if world > 1:
             dist.barrier()
             t = torch.tensor([secs], dtype=torch.float64, device=dev)
@@ -327,7 +327,7 @@ def config_legs(a, dev, rank=0, world=1):
             L.target.load_state_dict(L.source.state_dict())
         tr = VectorOffPolicyTrainer(env, L, seed=7919 * rank)
         tr.train(20)
-        secs = timed_train(tr, a.cfg4_steps)
+        secs = timed_train(tr, a.cfg4_steps, "config 4 leg")
         env.close()
         rec = {"envs_per_gpu": B, "grid": dim, "algo": "mixed (global id mod 3)",
                "vector_steps": a.cfg4_steps, "seconds": round(secs, 3),
@@ -351,7 +351,7 @@ def config_legs(a, dev, rank=0, world=1):
         if world > 1:
             broadcast_params(tr.net)
         tr.train(20)
-        secs = timed_train(tr, a.cfg5_steps)
+        secs = timed_train(tr, a.cfg5_steps, "config 5 leg")
         rec = {"envs_per_gpu": B, "dims": [dims[0], dims[-1]], "toroidal": True,
                "vector_steps": a.cfg5_steps, "seconds": round(secs, 3),
                "env_steps_per_s": B * a.cfg5_steps * world / secs, "updates": tr.updates,
@@ -395,6 +395,15 @@ def reference_protocol(L, n, dim, dev, seed):
 def log(msg):
     """Progress on stderr (the JSON line is the only stdout output)."""
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def progress(rank, name, every=400):
+    """train() keyword arguments for a progress line on rank 0 every `every` vector steps (one
+    stream synchronisation each): long legs keep writing, so a supervisor that takes silence
+    for a hang (and a reader of the log) sees them advance."""
+    if rank != 0:
+        return {}
+    return {"log_every": every, "log": lambda r: log(f"{name}: vector step {r['step']}")}
 
 
 def acting_agreement(L, n=65536):
