@@ -515,7 +515,8 @@ __global__ __launch_bounds__(T1) void k_qconv(MzQAct q, int row_tiles, int group
 __global__ __launch_bounds__(T1) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void k_qfc1(MzQAct q, int row_tiles, const uint16_t* __restrict__ feat) {
   __shared__ __align__(16) uint16_t A[2][2][RT1 * AST];  // [buffer][hi, lo][row][k]
-  static_assert(RT1 * 32 / 8 == T1, "one 16-B A load per thread and half-tile");
+  constexpr int NP = 2 * RT1 * 32 / 8 / T1;  // 16-B pieces of a chunk's A tile per thread
+  static_assert(NP * T1 == 2 * RT1 * 32 / 8, "whole 16-B pieces per thread");
   const int tid = threadIdx.x, lane = tid & (WAVE - 1);
   const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);
   const int g4 = lane >> 4, c16 = lane & 15;
@@ -550,7 +551,6 @@ void k_qfc1(MzQAct q, int row_tiles, const uint16_t* __restrict__ feat) {
   // A staging: thread tid <-> 16-B piece tid of the chunk's hi and lo halves (row tid / 4, k
   // octet tid % 4)
   const uint4* fsrc = reinterpret_cast<const uint4*>(feat + (size_t)rt * NCH * FT_CHUNK);
-  const int ar = tid >> 2, ao = (tid & 3) * 8;
   frag_ab ah[4], al[4];
   auto fc1_read = [&](int c) {
     const uint16_t* Ah = A[c & 1][0];
@@ -564,38 +564,43 @@ void k_qfc1(MzQAct q, int row_tiles, const uint16_t* __restrict__ feat) {
   };
   static_assert(NCH % 2 == 0, "loop unrolled by two");
   // A tiles staged through LDS (one 16-B piece of hi and of lo per thread), each loaded into
-  // registers two chunks ahead of its LDS store (slots r0 / r1): all waves read the same 8 KB,
+  // registers two chunks ahead of its LDS store (slots s0 / s1): all waves read the same 8 KB,
   // so LDS staging beats per-wave fragment loads (70.7-71.0 vs 73.0-73.4 M env steps/s in
   // training), and the two-chunk distance beats one (74.5-74.9 vs 73.0-73.4 M; the forward alone
   // 1.04 vs 1.10 ms at 65,536 rows) — profiles/r04l/ — with the Q values bit for bit the same
-  uint4 r0h, r0l, r1h, r1l;
-  auto ld = [&](int c, uint4& h, uint4& l) {
-    h = fsrc[(size_t)c * (FT_CHUNK / 8) + tid];
-    l = fsrc[(size_t)c * (FT_CHUNK / 8) + T1 + tid];
+  // piece p of a chunk: half p / 256 (hi, lo), row (p % 256) / 4, k octet p % 4; thread tid
+  // takes pieces tid + k T1
+  uint4 s0[NP], s1[NP];
+  auto ld = [&](int c, uint4 (&r)[NP]) {
+#pragma unroll
+    for (int k = 0; k < NP; ++k) r[k] = fsrc[(size_t)c * (FT_CHUNK / 8) + tid + k * T1];
   };
-  auto st = [&](int buf, const uint4& h, const uint4& l) {
-    *reinterpret_cast<uint4*>(A[buf][0] + ar * AST + ao) = h;
-    *reinterpret_cast<uint4*>(A[buf][1] + ar * AST + ao) = l;
+  auto st = [&](int buf, const uint4 (&r)[NP]) {
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const int pc = tid + k * T1, idx = pc & 255;
+      *reinterpret_cast<uint4*>(A[buf][pc >> 8] + (idx >> 2) * AST + (idx & 3) * 8) = r[k];
+    }
   };
-  ld(0, r0h, r0l);
-  st(0, r0h, r0l);
-  ld(1, r1h, r1l);
-  ld(2, r0h, r0l);
+  ld(0, s0);
+  st(0, s0);
+  ld(1, s1);
+  ld(2, s0);
   load_b(0, bh, bl);
   __syncthreads();
   for (int c = 0; c < NCH; c += 2) {
-    // chunk c in LDS buffer 0; r1 = chunk c + 1, r0 = chunk c + 2
+    // chunk c in LDS buffer 0; s1 = chunk c + 1, s0 = chunk c + 2
     load_b(c + 1, nbh, nbl);
     fc1_read(c);
     mfma_x3(ah, al, bh, bl, acc);
-    st(1, r1h, r1l);
-    if (c + 3 < NCH) ld(c + 3, r1h, r1l);
+    st(1, s1);
+    if (c + 3 < NCH) ld(c + 3, s1);
     __syncthreads();
     if (c + 2 < NCH) load_b(c + 2, bh, bl);
     fc1_read(c + 1);
     mfma_x3(ah, al, nbh, nbl, acc);
-    if (c + 2 < NCH) st(0, r0h, r0l);
-    if (c + 4 < NCH) ld(c + 4, r0h, r0l);
+    if (c + 2 < NCH) st(0, s0);
+    if (c + 4 < NCH) ld(c + 4, s0);
     __syncthreads();
   }
   // epilogue: as k_qact1

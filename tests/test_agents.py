@@ -85,3 +85,29 @@ def test_ppo_pool_episode_returns_advantages(fx):
         np.testing.assert_array_equal(R.numpy(), fx["ppo.pool.returns"][sl])
         np.testing.assert_array_equal(A.numpy(), fx["ppo.pool.advantages"][sl])
         assert np.isnan(R.numpy()).all() == (n == 1)
+
+
+def test_ppo_episode_bound_covers_max_steps():
+    """VectorPPOTrainer's record buffers hold L = episode_bound(max_dim, toroidal) steps per
+    instance: more than any episode (max_steps + 1 steps, base_maze_env.py:205-208). On the torus
+    len / CE exceeds 1 for some mazes, so (N-1)^2 + 2 is not a bound there; the oracle's max_steps
+    of generated mazes (17..79 toroidal, 15..81 euclidean, 3 algorithms) stay below L, and the
+    formula's worst case (every open square on the solution) is what L is sized for."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import pyoracle as O
+    from mazerl.trainers.ppo_trainer import episode_bound
+    for tor, sizes in ((True, range(17, 80, 6)), (False, range(15, 82, 6))):
+        L = episode_bound(max(sizes), tor)
+        for n in sizes:
+            for algo in range(3):
+                for s in range(3):
+                    start, goal, g = O.generate(n, algo, 0x5EED + 97 * n + s, toroidal=tor)
+                    assert O.max_steps(g, start, goal, tor) + 1 < L
+        # the formula's worst case at the largest size: len = every open square
+        n = max(sizes)
+        c = ((n + 1) // 2) ** 2 if tor else ((n - 1) // 2) ** 2
+        worst = -(-((n - 1) ** 2 - 1) * (2 * c - 1) // ((n - 1) * ((n - 1) // 2) - 1))
+        assert worst + 1 < L
+    assert episode_bound(79, True) > (79 - 1) ** 2 + 2  # the old bound was short on the torus
