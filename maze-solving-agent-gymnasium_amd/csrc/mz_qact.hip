@@ -461,6 +461,9 @@ void k_qact1(MzQAct q, int row_tiles) {
 // of hi and of lo per thread per chunk). Same values, same MFMA order: the same Q values bit for
 // bit.
 constexpr int FT_CHUNK = 2 * RT1 * 32;  // uint16 per (tile, chunk)
+#ifndef MZ_QFC1_BDIST
+#define MZ_QFC1_BDIST 1  // chunks ahead the fc1 weight fragments are loaded (1 or 2)
+#endif
 
 
 // grid: row tiles x `groups` chunk groups (small batches: a row tile's 50 chunks over several
@@ -586,6 +589,27 @@ void k_qfc1(MzQAct q, int row_tiles, const uint16_t* __restrict__ feat) {
   st(0, s0);
   ld(1, s1);
   ld(2, s0);
+#if MZ_QFC1_BDIST == 2
+  // B fragments two chunks ahead with the same two register sets: chunk c + 2's load is issued
+  // right after chunk c's MFMAs (which read the set at issue)
+  load_b(0, bh, bl);
+  load_b(1, nbh, nbl);
+  __syncthreads();
+  for (int c = 0; c < NCH; c += 2) {
+    fc1_read(c);
+    mfma_x3(ah, al, bh, bl, acc);
+    if (c + 2 < NCH) load_b(c + 2, bh, bl);
+    st(1, s1);
+    if (c + 3 < NCH) ld(c + 3, s1);
+    __syncthreads();
+    fc1_read(c + 1);
+    mfma_x3(ah, al, nbh, nbl, acc);
+    if (c + 3 < NCH) load_b(c + 3, nbh, nbl);
+    if (c + 2 < NCH) st(0, s0);
+    if (c + 4 < NCH) ld(c + 4, s0);
+    __syncthreads();
+  }
+#else
   load_b(0, bh, bl);
   __syncthreads();
   for (int c = 0; c < NCH; c += 2) {
@@ -603,6 +627,7 @@ void k_qfc1(MzQAct q, int row_tiles, const uint16_t* __restrict__ feat) {
     if (c + 4 < NCH) ld(c + 4, s0);
     __syncthreads();
   }
+#endif
   // epilogue: as k_qact1
 #pragma unroll
   for (int j = 0; j < 4; ++j) {

@@ -3,12 +3,12 @@
 # then the 4-rank gloo rehearsal of the whole bench through its own launcher
 set -o pipefail
 out=gpurun_out/r04n; mkdir -p $out
-for lib in default profiles/_bin/lib_qw8.so; do
+for lib in default profiles/_bin/lib_qw8.so profiles/_bin/lib_qb2.so; do
   if [ "$lib" = default ]; then unset MZ_LIB_OVERRIDE; else export MZ_LIB_OVERRIDE=$lib; fi
   timeout -k 10 200 python -u profiles/exp_qact_checksum.py >> $out/checksum.jsonl || exit 1
 done
 for rep in 1 2; do
-  for lib in default profiles/_bin/lib_qw8.so; do
+  for lib in default profiles/_bin/lib_qw8.so profiles/_bin/lib_qb2.so; do
     if [ "$lib" = default ]; then unset MZ_LIB_OVERRIDE; else export MZ_LIB_OVERRIDE=$lib; fi
     timeout -k 10 300 python -u bench.py --legs bits --steps 50 --warmup 5 --no-cpu-baseline --config-legs cfg4 --curriculum-steps 0 --eval-mazes 200 --cfg-eval-mazes 100 > $out/bench_${rep}_$(basename $lib).json 2>> $out/bench.err || exit 1
   done
