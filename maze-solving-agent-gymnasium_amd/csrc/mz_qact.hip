@@ -462,7 +462,7 @@ void k_qact1(MzQAct q, int row_tiles) {
 // bit.
 constexpr int FT_CHUNK = 2 * RT1 * 32;  // uint16 per (tile, chunk)
 #ifndef MZ_QFC1_BDIST
-#define MZ_QFC1_BDIST 1  // chunks ahead the fc1 weight fragments are loaded (1 or 2)
+#define MZ_QFC1_BDIST 2  // chunks ahead the fc1 weight fragments are loaded (1 or 2)
 #endif
 
 
