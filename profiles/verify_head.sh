@@ -7,4 +7,4 @@ O=gpurun_out/$1
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1 &&
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 &&
-timeout -k 10 300 python -u bench.py > $O/bench.json 2> $O/bench.err
+timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err
