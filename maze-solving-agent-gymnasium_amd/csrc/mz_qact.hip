@@ -54,7 +54,7 @@ constexpr int TPW = 16 / QW1;      // conv tiles (4 rows each) per wave
 constexpr int NTL1 = N1 / NT1;     // fc1 output tiles
 constexpr int XPT = 8 / NTL1;      // XCDs per output tile
 constexpr int PR = 17;             // padded window rows per instance
-constexpr int AST = 40;            // LDS A-tile row stride in bf16 (32 + 8: conflict-free b128)
+constexpr int AST = 40;            // k_qact1 LDS A-tile row stride in bf16 (32 + 8; 2-way on b128 reads)
 // k_qact2 rows per workgroup: each wave streams its 256 KB of fc2 hi / lo fragments once per
 // workgroup (2 MB per 64 rows of L2 traffic). 128 rows halve that but need 256 VGPRs with spills:
 // alone no faster (greedy rows 0.466 vs 0.460 ms), inside training 58.2 vs 67.8-68.3 M env steps/s
@@ -63,10 +63,21 @@ constexpr int AST = 40;            // LDS A-tile row stride in bf16 (32 + 8: con
 #define MZ_QACT2_ROWS 64
 #endif
 constexpr int RT2 = MZ_QACT2_ROWS;
+// k_qact2's h1 chunks and fc2 fragments: 1 chunk ahead (the single-buffered loop) or 2. Two ahead
+// is faster alone (k_qact2 MFMA busy 0.43 -> 0.47) and slower inside training: 71.0 / 71.0 vs
+// 75.3 / 74.9 M env steps/s, the same box interleaved (profiles/r04p/)
+#ifndef MZ_QACT2_AHEAD
+#define MZ_QACT2_AHEAD 1
+#endif
 constexpr int MI2 = RT2 / 16;      // k_qact2 row fragments per wave
 
 typedef __attribute__((ext_vector_type(8))) __bf16 frag_ab;
 typedef __attribute__((ext_vector_type(4))) float frag_cd;
+// staging registers as native vectors: HIP's uint4 / float4 structs held across loop iterations
+// in small arrays defeat SROA, and the compiler then moves the arrays to LDS (promote-alloca: each
+// prefetch became a store to LDS behind an s_waitcnt vmcnt(0))
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 __device__ inline uint32_t bf16x2(float lo, float hi) {  // round to nearest even, packed
   uint32_t r;
@@ -461,6 +472,22 @@ void k_qact1(MzQAct q, int row_tiles) {
 // of hi and of lo per thread per chunk). Same values, same MFMA order: the same Q values bit for
 // bit.
 constexpr int FT_CHUNK = 2 * RT1 * 32;  // uint16 per (tile, chunk)
+
+// LDS A tiles of k_qfc1 / k_qact2: 64-B rows (32 bf16), the 16-B octets of row r permuted by
+// oct ^ h((r >> 2) & 3), h = {0, 3, 2, 1}. The MFMA operand read (ds_read_b128, lane -> row
+// 16 i + lane % 16, octet lane / 16) then hits 16 distinct 16-B bank slots in each of its four
+// lane groups ({0-3, 12-15, 20-27}, ...: MI355X_MICROARCH.md, LDS), and the row-major stores stay
+// conflict-free; k_qact1's padded 80-B rows (AST) were 2-way on every operand read.
+#ifndef MZ_QA_SWZ
+#define MZ_QA_SWZ 1
+#endif
+#if MZ_QA_SWZ
+constexpr int ARS = 32;  // A-tile row stride (bf16)
+__device__ inline int a_off(int r, int oct) { return r * ARS + 8 * (oct ^ ((4 - ((r >> 2) & 3)) & 3)); }
+#else
+constexpr int ARS = AST;
+__device__ inline int a_off(int r, int oct) { return r * ARS + 8 * oct; }
+#endif
 #ifndef MZ_QFC1_BDIST
 #define MZ_QFC1_BDIST 2  // chunks ahead the fc1 weight fragments are loaded (1 or 2)
 #endif
@@ -517,7 +544,7 @@ __global__ __launch_bounds__(T1) void k_qconv(MzQAct q, int row_tiles, int group
 
 __global__ __launch_bounds__(T1) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void k_qfc1(MzQAct q, int row_tiles, const uint16_t* __restrict__ feat) {
-  __shared__ __align__(16) uint16_t A[2][2][RT1 * AST];  // [buffer][hi, lo][row][k]
+  __shared__ __align__(16) uint16_t A[2][2][RT1 * ARS];  // [buffer][hi, lo][row][k]
   constexpr int NP = 2 * RT1 * 32 / 8 / T1;  // 16-B pieces of a chunk's A tile per thread
   static_assert(NP * T1 == 2 * RT1 * 32 / 8, "whole 16-B pieces per thread");
   const int tid = threadIdx.x, lane = tid & (WAVE - 1);
@@ -553,7 +580,7 @@ void k_qfc1(MzQAct q, int row_tiles, const uint16_t* __restrict__ feat) {
   };
   // A staging: thread tid <-> 16-B piece tid of the chunk's hi and lo halves (row tid / 4, k
   // octet tid % 4)
-  const uint4* fsrc = reinterpret_cast<const uint4*>(feat + (size_t)rt * NCH * FT_CHUNK);
+  const u32x4* fsrc = reinterpret_cast<const u32x4*>(feat + (size_t)rt * NCH * FT_CHUNK);
   frag_ab ah[4], al[4];
   auto fc1_read = [&](int c) {
     const uint16_t* Ah = A[c & 1][0];
@@ -561,8 +588,8 @@ void k_qfc1(MzQAct q, int row_tiles, const uint16_t* __restrict__ feat) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = 16 * i + c16;
-      ah[i] = __builtin_bit_cast(frag_ab, *reinterpret_cast<const uint4*>(Ah + r * AST + 8 * g4));
-      al[i] = __builtin_bit_cast(frag_ab, *reinterpret_cast<const uint4*>(Al + r * AST + 8 * g4));
+      ah[i] = __builtin_bit_cast(frag_ab, *reinterpret_cast<const uint4*>(Ah + a_off(r, g4)));
+      al[i] = __builtin_bit_cast(frag_ab, *reinterpret_cast<const uint4*>(Al + a_off(r, g4)));
     }
   };
   static_assert(NCH % 2 == 0, "loop unrolled by two");
@@ -573,43 +600,54 @@ void k_qfc1(MzQAct q, int row_tiles, const uint16_t* __restrict__ feat) {
   // 1.04 vs 1.10 ms at 65,536 rows) — profiles/r04l/ — with the Q values bit for bit the same
   // piece p of a chunk: half p / 256 (hi, lo), row (p % 256) / 4, k octet p % 4; thread tid
   // takes pieces tid + k T1
-  uint4 s0[NP], s1[NP];
-  auto ld = [&](int c, uint4 (&r)[NP]) {
+  u32x4 s0[NP], s1[NP];
+  auto ld = [&](int c, u32x4 (&r)[NP]) {
 #pragma unroll
     for (int k = 0; k < NP; ++k) r[k] = fsrc[(size_t)c * (FT_CHUNK / 8) + tid + k * T1];
   };
-  auto st = [&](int buf, const uint4 (&r)[NP]) {
+  auto st = [&](int buf, const u32x4 (&r)[NP]) {
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
       const int pc = tid + k * T1, idx = pc & 255;
-      *reinterpret_cast<uint4*>(A[buf][pc >> 8] + (idx >> 2) * AST + (idx & 3) * 8) = r[k];
+      *reinterpret_cast<u32x4*>(A[buf][pc >> 8] + a_off(idx >> 2, idx & 3)) = r[k];
     }
   };
   ld(0, s0);
   st(0, s0);
-  ld(1, s1);
-  ld(2, s0);
 #if MZ_QFC1_BDIST == 2
   // B fragments two chunks ahead with the same two register sets: chunk c + 2's load is issued
-  // right after chunk c's MFMAs (which read the set at issue)
+  // right after chunk c's MFMAs (which read the set at issue). The prologue issues its loads in
+  // the loop's order (A c + 1, B c, A c + 2, B c + 1; sched_barrier keeps the compiler from
+  // regrouping them): s_waitcnt counts are merged over the loop's entry and back edge, and a
+  // prologue order with the A tiles last made every iteration wait for all but 2 loads
+  ld(1, s1);
+  __builtin_amdgcn_sched_barrier(0);
   load_b(0, bh, bl);
+  __builtin_amdgcn_sched_barrier(0);
+  ld(2, s0);
+  __builtin_amdgcn_sched_barrier(0);
   load_b(1, nbh, nbl);
   __syncthreads();
   for (int c = 0; c < NCH; c += 2) {
     fc1_read(c);
     mfma_x3(ah, al, bh, bl, acc);
-    if (c + 2 < NCH) load_b(c + 2, bh, bl);
+    // loads past the last chunk re-read chunk NCH - 1 (unused): unconditional loads keep the
+    // compiler's s_waitcnt counts exact across the loop (a conditional load made it wait for
+    // every load in flight, vmcnt(0), before the first MFMA of each iteration)
+    load_b(min(c + 2, NCH - 1), bh, bl);
     st(1, s1);
-    if (c + 3 < NCH) ld(c + 3, s1);
+    ld(min(c + 3, NCH - 1), s1);
     __syncthreads();
     fc1_read(c + 1);
     mfma_x3(ah, al, nbh, nbl, acc);
-    if (c + 3 < NCH) load_b(c + 3, nbh, nbl);
-    if (c + 2 < NCH) st(0, s0);
-    if (c + 4 < NCH) ld(c + 4, s0);
+    load_b(min(c + 3, NCH - 1), nbh, nbl);
+    st(0, s0);  // (the last iteration's store fills a buffer no one reads again)
+    ld(min(c + 4, NCH - 1), s0);
     __syncthreads();
   }
 #else
+  ld(1, s1);
+  ld(2, s0);
   load_b(0, bh, bl);
   __syncthreads();
   for (int c = 0; c < NCH; c += 2) {
@@ -646,7 +684,7 @@ void k_qfc1(MzQAct q, int row_tiles, const uint16_t* __restrict__ feat) {
 // ---- k_qact2 -------------------------------------------------------------------------------
 template <bool RELU>
 __global__ __launch_bounds__(512) void k_qact2(MzQAct q) {
-  __shared__ __align__(16) uint16_t A[2][2][RT2 * AST];
+  __shared__ __align__(16) uint16_t A[2][2][RT2 * ARS];
   __shared__ float part[8][RT2][4];
   const int tid = threadIdx.x, lane = tid & (WAVE - 1);
   const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);
@@ -660,13 +698,13 @@ __global__ __launch_bounds__(512) void k_qact2(MzQAct q) {
   // A chunk c (32 columns of h1 for the RT2 rows): thread -> (rows tid / 8 + 64 u, 4 columns)
   constexpr int AU = RT2 / 64;
   const int ar = tid >> 3, ak = (tid & 7) * 4;
-  struct AV { float4 v[AU]; };
+  struct AV { f32x4 v[AU]; };
   auto load_a = [&](int c) -> AV {
     AV a;
 #pragma unroll
     for (int u = 0; u < AU; ++u)
-      a.v[u] = ar + 64 * u >= nr ? make_float4(0.f, 0.f, 0.f, 0.f)
-                                 : *reinterpret_cast<const float4*>(q.h1 + (size_t)(r0 + ar + 64 * u) * N1 + 32 * c + ak);
+      // rows past the count re-read the last row (their results are not stored): no branch
+      a.v[u] = *reinterpret_cast<const f32x4*>(q.h1 + (size_t)(r0 + min(ar + 64 * u, nr - 1)) * N1 + 32 * c + ak);
     return a;
   };
   auto store_a = [&](int buf, const AV& a) {
@@ -675,8 +713,9 @@ __global__ __launch_bounds__(512) void k_qact2(MzQAct q) {
       uint32_t h0, l0, h1, l1;
       split2(a.v[u].x, a.v[u].y, h0, l0);
       split2(a.v[u].z, a.v[u].w, h1, l1);
-      uint32_t* ph = reinterpret_cast<uint32_t*>(A[buf][0] + (ar + 64 * u) * AST + ak);
-      uint32_t* pl = reinterpret_cast<uint32_t*>(A[buf][1] + (ar + 64 * u) * AST + ak);
+      const int o = a_off(ar + 64 * u, ak >> 3) + (ak & 7);
+      uint32_t* ph = reinterpret_cast<uint32_t*>(A[buf][0] + o);
+      uint32_t* pl = reinterpret_cast<uint32_t*>(A[buf][1] + o);
       ph[0] = h0; ph[1] = h1;
       pl[0] = l0; pl[1] = l1;
     }
@@ -702,6 +741,47 @@ __global__ __launch_bounds__(512) void k_qact2(MzQAct q) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = frag_cd{0.0f, 0.0f, 0.0f, 0.0f};
   constexpr int NC2 = N1 / 32;
+  auto chunk_mfma = [&](int buf, const uint4 (&b_h)[4], const uint4 (&b_l)[4]) {
+    const uint16_t* Ah = A[buf][0];
+    const uint16_t* Al = A[buf][1];
+#pragma unroll
+    for (int h = 0; h < MI2; h += 4) {  // four row fragments at a time (register pressure)
+      frag_ab ah[4], al[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 16 * (h + i) + c16;
+        ah[i] = __builtin_bit_cast(frag_ab, *reinterpret_cast<const uint4*>(Ah + a_off(r, g4)));
+        al[i] = __builtin_bit_cast(frag_ab, *reinterpret_cast<const uint4*>(Al + a_off(r, g4)));
+      }
+      mfma_x3<4>(ah, al, b_h, b_l, *reinterpret_cast<frag_cd(*)[4][4]>(&acc[h]));
+    }
+  };
+#if MZ_QACT2_AHEAD == 2
+  // h1 chunks loaded two chunks ahead of their LDS store (s1 / s0), the fc2 fragments two chunks
+  // ahead in two register sets, each load issued right after the MFMAs that free its registers
+  static_assert(NC2 % 2 == 0, "loop unrolled by two");
+  store_a(0, load_a(0));
+  AV s1 = load_a(1);  // the loop's load order (as k_qfc1's prologue)
+  __builtin_amdgcn_sched_barrier(0);
+  load_b(0, bh, bl);
+  __builtin_amdgcn_sched_barrier(0);
+  AV s0 = load_a(2);
+  __builtin_amdgcn_sched_barrier(0);
+  load_b(1, nbh, nbl);
+  __syncthreads();
+  for (int c = 0; c < NC2; c += 2) {
+    chunk_mfma(0, bh, bl);
+    load_b(min(c + 2, NC2 - 1), bh, bl);  // unconditional, clamped: as k_qfc1
+    store_a(1, s1);
+    s1 = load_a(min(c + 3, NC2 - 1));
+    __syncthreads();
+    chunk_mfma(1, nbh, nbl);
+    load_b(min(c + 3, NC2 - 1), nbh, nbl);
+    store_a(0, s0);
+    s0 = load_a(min(c + 4, NC2 - 1));
+    __syncthreads();
+  }
+#else
   store_a(0, load_a(0));
   load_b(0, bh, bl);
   AV na = {};
@@ -711,19 +791,7 @@ __global__ __launch_bounds__(512) void k_qact2(MzQAct q) {
       na = load_a(c + 1);
       load_b(c + 1, nbh, nbl);
     }
-    const uint16_t* Ah = A[c & 1][0];
-    const uint16_t* Al = A[c & 1][1];
-#pragma unroll
-    for (int h = 0; h < MI2; h += 4) {  // four row fragments at a time (register pressure)
-      frag_ab ah[4], al[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = 16 * (h + i) + c16;
-        ah[i] = __builtin_bit_cast(frag_ab, *reinterpret_cast<const uint4*>(Ah + r * AST + 8 * g4));
-        al[i] = __builtin_bit_cast(frag_ab, *reinterpret_cast<const uint4*>(Al + r * AST + 8 * g4));
-      }
-      mfma_x3<4>(ah, al, bh, bl, *reinterpret_cast<frag_cd(*)[4][4]>(&acc[h]));
-    }
+    chunk_mfma(c & 1, bh, bl);
     if (c + 1 < NC2) {
       store_a((c + 1) & 1, na);
 #pragma unroll
@@ -734,6 +802,7 @@ __global__ __launch_bounds__(512) void k_qact2(MzQAct q) {
     }
     __syncthreads();
   }
+#endif
 
   // h2 = act(acc + b2) in f32; fc3 partial sums over this wave's 64 columns, per row and action,
   // four row fragments at a time
@@ -798,8 +867,13 @@ __global__ __launch_bounds__(512) void k_qact2(MzQAct q) {
       qv[a] = v + q.b3[a];
     }
     int best = 0;  // torch.argmax: the first maximum, a NaN counts as the maximum
+    float bv = qv[0];  // (a scalar: qv[best] is a dynamic index the compiler moves to LDS)
+#pragma unroll
     for (int a = 1; a < 4; ++a)
-      if (!isnan(qv[best]) && (isnan(qv[a]) || qv[a] > qv[best])) best = a;
+      if (!isnan(bv) && (isnan(qv[a]) || qv[a] > bv)) {
+        best = a;
+        bv = qv[a];
+      }
     const int row = r0 + tid;
     const int inst = q.rows ? q.rows[row] : row;
     if (q.greedy) q.greedy[inst] = best;
