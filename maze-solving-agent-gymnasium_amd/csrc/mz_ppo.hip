@@ -302,7 +302,10 @@ __global__ __launch_bounds__(256) void k_ppo_head1(MzPpoHead q) {
     pg += p[k] * g[k];
   }
   const int a = (int)q.action[i];
-  q.lp_new[i] = zz[a] - mx - lS;  // log_softmax(z)[a]
+  float za = zz[0];  // zz[a] by selects: a dynamic index would put zz in LDS (promote-alloca)
+#pragma unroll
+  for (int k = 1; k < 4; ++k) za = k == a ? zz[k] : za;
+  q.lp_new[i] = za - mx - lS;  // log_softmax(z)[a]
   q.ent[i] = ent;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {

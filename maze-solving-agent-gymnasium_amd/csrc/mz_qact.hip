@@ -488,6 +488,14 @@ __device__ inline int a_off(int r, int oct) { return r * ARS + 8 * (oct ^ ((4 - 
 constexpr int ARS = AST;
 __device__ inline int a_off(int r, int oct) { return r * ARS + 8 * oct; }
 #endif
+// k_qfc1's output tiles per XCD: 1 (each XCD's L2 holds one 1.6 MB hi / lo weight slice; a row
+// tile's A chunks are read by 4 XCDs), 2 or 4 (more weight slices per L2, fewer A reads from HBM)
+#ifndef MZ_QFC1_NTX
+#define MZ_QFC1_NTX 1
+#endif
+constexpr int QF_NTX = MZ_QFC1_NTX;
+constexpr int QF_S = 8 * QF_NTX / NTL1;  // XCDs sharing one set of QF_NTX output tiles
+static_assert(QF_S >= 1 && 8 % QF_S == 0, "output tiles per XCD");
 #ifndef MZ_QFC1_BDIST
 #define MZ_QFC1_BDIST 2  // chunks ahead the fc1 weight fragments are loaded (1 or 2)
 #endif
@@ -550,8 +558,10 @@ void k_qfc1(MzQAct q, int row_tiles, const uint16_t* __restrict__ feat) {
   const int tid = threadIdx.x, lane = tid & (WAVE - 1);
   const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);
   const int g4 = lane >> 4, c16 = lane & 15;
-  const int b = blockIdx.x, x = b & 7;
-  const int nt = x / XPT, rt = (b >> 3) * XPT + (x % XPT);
+  // workgroup b runs on XCD x = b % 8; XCD x cycles through QF_NTX output tiles of its set, one
+  // row tile after another (consecutive workgroups on an XCD share the row tile's A chunks in L2)
+  const int b = blockIdx.x, x = b & 7, k = b >> 3;
+  const int nt = (x / QF_S) * QF_NTX + k % QF_NTX, rt = (k / QF_NTX) * QF_S + x % QF_S;
   if (rt >= row_tiles) return;
   const int m = q.count ? min(q.n, *q.count) : q.n;
   const int r0 = rt * RT1;
@@ -979,7 +989,7 @@ hipError_t mz_launch_qact(const MzQAct& q, int relu, hipStream_t s) {
       hipLaunchKernelGGL(k_qconv<true>, dim3(rt * groups), dim3(T1), 0, s, q, rt, groups, feat);
     else
       hipLaunchKernelGGL(k_qconv<false>, dim3(rt * groups), dim3(T1), 0, s, q, rt, groups, feat);
-    hipLaunchKernelGGL(k_qfc1, dim3(blocks1), dim3(T1), 0, s, q, rt, feat);
+    hipLaunchKernelGGL(k_qfc1, dim3(8 * QF_NTX * ((rt + QF_S - 1) / QF_S)), dim3(T1), 0, s, q, rt, feat);
   }
   const int blocks2 = (q.n + RT2 - 1) / RT2;
   if (relu)
