@@ -496,9 +496,11 @@ __device__ inline int a_off(int r, int oct) { return r * ARS + 8 * oct; }
 constexpr int QF_NTX = MZ_QFC1_NTX;
 constexpr int QF_S = 8 * QF_NTX / NTL1;  // XCDs sharing one set of QF_NTX output tiles
 static_assert(QF_S >= 1 && 8 % QF_S == 0, "output tiles per XCD");
-#ifndef MZ_QFC1_BDIST
-#define MZ_QFC1_BDIST 2  // chunks ahead the fc1 weight fragments are loaded (1 or 2)
+// k_qfc1's chunks per LDS stage (one barrier per stage)
+#ifndef MZ_QFC1_CPB
+#define MZ_QFC1_CPB 2
 #endif
+constexpr int QF_CPB = MZ_QFC1_CPB;
 
 
 // grid: row tiles x `groups` chunk groups (small batches: a row tile's 50 chunks over several
@@ -550,9 +552,13 @@ __global__ __launch_bounds__(T1) void k_qconv(MzQAct q, int row_tiles, int group
   }
 }
 
-__global__ __launch_bounds__(T1) __attribute__((amdgpu_waves_per_eu(2, 2)))
+#ifndef MZ_QFC1_WPE
+#define MZ_QFC1_WPE 2  // k_qfc1 waves per SIMD the register budget is sized for
+#endif
+__global__ __launch_bounds__(T1) __attribute__((amdgpu_waves_per_eu(MZ_QFC1_WPE, MZ_QFC1_WPE)))
 void k_qfc1(MzQAct q, int row_tiles, const uint16_t* __restrict__ feat) {
-  __shared__ __align__(16) uint16_t A[2][2][RT1 * ARS];  // [buffer][hi, lo][row][k]
+  // [buffer][chunk of the stage][hi, lo][row][k]
+  __shared__ __align__(16) uint16_t A[2][QF_CPB][2][RT1 * ARS];
   constexpr int NP = 2 * RT1 * 32 / 8 / T1;  // 16-B pieces of a chunk's A tile per thread
   static_assert(NP * T1 == 2 * RT1 * 32 / 8, "whole 16-B pieces per thread");
   const int tid = threadIdx.x, lane = tid & (WAVE - 1);
@@ -580,7 +586,9 @@ void k_qfc1(MzQAct q, int row_tiles, const uint16_t* __restrict__ feat) {
   const auto rs_l = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(q.w1l) + (size_t)nt * NT1 * K1,
                                                       0, NT1 * K1 * 2, 0x00020000);
   const int boff = (cq * 4 * 64 + lane) * 16;
+  // B fragments of chunk c (clamped: past the last chunk a load re-reads chunk NCH - 1, unused)
   auto load_b = [&](int c, uint4* dh, uint4* dl) {
+    c = min(c, NCH - 1);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int off = boff + c * (QW1 * 4 * 64 * 16) + j * (64 * 16);
@@ -592,9 +600,9 @@ void k_qfc1(MzQAct q, int row_tiles, const uint16_t* __restrict__ feat) {
   // octet tid % 4)
   const u32x4* fsrc = reinterpret_cast<const u32x4*>(feat + (size_t)rt * NCH * FT_CHUNK);
   frag_ab ah[4], al[4];
-  auto fc1_read = [&](int c) {
-    const uint16_t* Ah = A[c & 1][0];
-    const uint16_t* Al = A[c & 1][1];
+  auto fc1_read = [&](int buf, int sub) {
+    const uint16_t* Ah = A[buf][sub][0];
+    const uint16_t* Al = A[buf][sub][1];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = 16 * i + c16;
@@ -602,80 +610,75 @@ void k_qfc1(MzQAct q, int row_tiles, const uint16_t* __restrict__ feat) {
       al[i] = __builtin_bit_cast(frag_ab, *reinterpret_cast<const uint4*>(Al + a_off(r, g4)));
     }
   };
-  static_assert(NCH % 2 == 0, "loop unrolled by two");
-  // A tiles staged through LDS (one 16-B piece of hi and of lo per thread), each loaded into
-  // registers two chunks ahead of its LDS store (slots s0 / s1): all waves read the same 8 KB,
-  // so LDS staging beats per-wave fragment loads (70.7-71.0 vs 73.0-73.4 M env steps/s in
-  // training), and the two-chunk distance beats one (74.5-74.9 vs 73.0-73.4 M; the forward alone
-  // 1.04 vs 1.10 ms at 65,536 rows) — profiles/r04l/ — with the Q values bit for bit the same
-  // piece p of a chunk: half p / 256 (hi, lo), row (p % 256) / 4, k octet p % 4; thread tid
-  // takes pieces tid + k T1
-  u32x4 s0[NP], s1[NP];
-  auto ld = [&](int c, u32x4 (&r)[NP]) {
+  // A tiles staged through LDS (one 16-B piece of hi and of lo per thread and chunk), each stage
+  // (QF_CPB chunks) loaded into registers two stages ahead of its LDS store (sets s0 / s1): all
+  // waves read the same 8 KB per chunk, so LDS staging beats per-wave fragment loads (70.7-71.0 vs
+  // 73.0-73.4 M env steps/s in training), and the two-chunk distance beats one (74.5-74.9 vs
+  // 73.0-73.4 M; the forward alone 1.04 vs 1.10 ms at 65,536 rows) — profiles/r04l/ — with the Q
+  // values bit for bit the same. Piece p of a chunk: half p / 256 (hi, lo), row (p % 256) / 4, k
+  // octet p % 4; thread tid takes pieces tid + k T1. Stage loads are clamped like load_b.
+  constexpr int NST = NCH / QF_CPB;  // stages
+  static_assert(NST * QF_CPB == NCH, "whole stages");
+  u32x4 s0[QF_CPB][NP], s1[QF_CPB][NP];
+  auto ld = [&](int sg, u32x4 (&r)[QF_CPB][NP]) {
+    sg = min(sg, NST - 1);
 #pragma unroll
-    for (int k = 0; k < NP; ++k) r[k] = fsrc[(size_t)c * (FT_CHUNK / 8) + tid + k * T1];
+    for (int h = 0; h < QF_CPB; ++h)
+#pragma unroll
+      for (int k = 0; k < NP; ++k)
+        r[h][k] = fsrc[(size_t)(sg * QF_CPB + h) * (FT_CHUNK / 8) + tid + k * T1];
   };
-  auto st = [&](int buf, const u32x4 (&r)[NP]) {
+  auto st = [&](int buf, const u32x4 (&r)[QF_CPB][NP]) {
 #pragma unroll
-    for (int k = 0; k < NP; ++k) {
-      const int pc = tid + k * T1, idx = pc & 255;
-      *reinterpret_cast<u32x4*>(A[buf][pc >> 8] + a_off(idx >> 2, idx & 3)) = r[k];
+    for (int h = 0; h < QF_CPB; ++h)
+#pragma unroll
+      for (int k = 0; k < NP; ++k) {
+        const int pc = tid + k * T1, idx = pc & 255;
+        *reinterpret_cast<u32x4*>(A[buf][h][pc >> 8] + a_off(idx >> 2, idx & 3)) = r[h][k];
+      }
+  };
+  // One stage: its chunks' MFMAs from LDS buffer sg & 1 (chunk 2j + 1 of the stage's pairs on the
+  // B set nbh / nbl, the others on bh / bl; each set reloaded two chunks ahead right after the
+  // MFMAs that read it), then stage sg + 1 from `nxt` into the other buffer and stage sg + 3
+  // into `nxt`. B fragments are two chunks ahead, A tiles two stages.
+  auto stage = [&](int sg, u32x4 (&nxt)[QF_CPB][NP]) {
+#pragma unroll
+    for (int h = 0; h < QF_CPB; ++h) {
+      const int c = sg * QF_CPB + h;
+      fc1_read(sg & 1, h);
+      if ((c & 1) == 0) {
+        mfma_x3(ah, al, bh, bl, acc);
+        load_b(c + 2, bh, bl);
+      } else {
+        mfma_x3(ah, al, nbh, nbl, acc);
+        load_b(c + 2, nbh, nbl);
+      }
+      if (QF_CPB > 1) __builtin_amdgcn_sched_barrier(0);  // each reload right after its MFMAs
     }
+    st((sg + 1) & 1, nxt);  // (the last stage's store fills a buffer no one reads again)
+    ld(sg + 3, nxt);
+    __syncthreads();
   };
+  // prologue in the loop's load order (A stage 1, B chunks 0 and 1, A stage 2; sched_barrier
+  // keeps the compiler from regrouping them): s_waitcnt counts are merged over the loop's entry
+  // and back edge, and a prologue with the A tiles last made every iteration wait for all but 2
+  // loads. Loads inside the loop are unconditional for the same reason (a conditional load made
+  // it wait vmcnt(0) before each iteration's first MFMA).
   ld(0, s0);
   st(0, s0);
-#if MZ_QFC1_BDIST == 2
-  // B fragments two chunks ahead with the same two register sets: chunk c + 2's load is issued
-  // right after chunk c's MFMAs (which read the set at issue). The prologue issues its loads in
-  // the loop's order (A c + 1, B c, A c + 2, B c + 1; sched_barrier keeps the compiler from
-  // regrouping them): s_waitcnt counts are merged over the loop's entry and back edge, and a
-  // prologue order with the A tiles last made every iteration wait for all but 2 loads
   ld(1, s1);
   __builtin_amdgcn_sched_barrier(0);
   load_b(0, bh, bl);
-  __builtin_amdgcn_sched_barrier(0);
-  ld(2, s0);
-  __builtin_amdgcn_sched_barrier(0);
   load_b(1, nbh, nbl);
-  __syncthreads();
-  for (int c = 0; c < NCH; c += 2) {
-    fc1_read(c);
-    mfma_x3(ah, al, bh, bl, acc);
-    // loads past the last chunk re-read chunk NCH - 1 (unused): unconditional loads keep the
-    // compiler's s_waitcnt counts exact across the loop (a conditional load made it wait for
-    // every load in flight, vmcnt(0), before the first MFMA of each iteration)
-    load_b(min(c + 2, NCH - 1), bh, bl);
-    st(1, s1);
-    ld(min(c + 3, NCH - 1), s1);
-    __syncthreads();
-    fc1_read(c + 1);
-    mfma_x3(ah, al, nbh, nbl, acc);
-    load_b(min(c + 3, NCH - 1), nbh, nbl);
-    st(0, s0);  // (the last iteration's store fills a buffer no one reads again)
-    ld(min(c + 4, NCH - 1), s0);
-    __syncthreads();
-  }
-#else
-  ld(1, s1);
+  __builtin_amdgcn_sched_barrier(0);
   ld(2, s0);
-  load_b(0, bh, bl);
   __syncthreads();
-  for (int c = 0; c < NCH; c += 2) {
-    // chunk c in LDS buffer 0; s1 = chunk c + 1, s0 = chunk c + 2
-    load_b(c + 1, nbh, nbl);
-    fc1_read(c);
-    mfma_x3(ah, al, bh, bl, acc);
-    st(1, s1);
-    if (c + 3 < NCH) ld(c + 3, s1);
-    __syncthreads();
-    if (c + 2 < NCH) load_b(c + 2, bh, bl);
-    fc1_read(c + 1);
-    mfma_x3(ah, al, nbh, nbl, acc);
-    if (c + 2 < NCH) st(0, s0);
-    if (c + 4 < NCH) ld(c + 4, s0);
-    __syncthreads();
+  int sg = 0;
+  for (; sg + 1 < NST; sg += 2) {
+    stage(sg, s1);
+    stage(sg + 1, s0);
   }
-#endif
+  if (sg < NST) stage(sg, s1);
   // epilogue: as k_qact1
 #pragma unroll
   for (int j = 0; j < 4; ++j) {

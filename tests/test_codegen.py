@@ -54,9 +54,12 @@ def test_no_scratch_and_declared_lds_only(qact_asm):
     for part in ("k_qfc1", "k_qact2", "k_qconv"):
         for k in find(meta, part):
             assert meta[k]["private_segment_fixed_size"] == 0, k
-    # k_qfc1: A[2 buffers][hi, lo][64 rows x 32 bf16]; k_qact2: the same + part[8][64][4] f32
+    # k_qfc1: A[2 buffers][MZ_QFC1_CPB chunks][hi, lo][64 rows x 32 bf16]; k_qact2: A[2][hi, lo]
+    # [64 x 32] + part[8][64][4] f32
+    src = open(os.path.join(CSRC, "mz_qact.hip")).read()
+    cpb = int(re.search(r"#define MZ_QFC1_CPB (\d+)", src).group(1))
     for k in find(meta, "k_qfc1"):
-        assert meta[k]["group_segment_fixed_size"] == 2 * 2 * 64 * 32 * 2, k
+        assert meta[k]["group_segment_fixed_size"] == 2 * cpb * 2 * 64 * 32 * 2, k
     for k in find(meta, "k_qact2"):
         assert meta[k]["group_segment_fixed_size"] == 2 * 2 * 64 * 32 * 2 + 8 * 64 * 4 * 4, k
 
