@@ -63,12 +63,6 @@ constexpr int AST = 40;            // k_qact1 LDS A-tile row stride in bf16 (32 
 #define MZ_QACT2_ROWS 64
 #endif
 constexpr int RT2 = MZ_QACT2_ROWS;
-// k_qact2's h1 chunks and fc2 fragments: 1 chunk ahead (the single-buffered loop) or 2. Two ahead
-// is faster alone (k_qact2 MFMA busy 0.43 -> 0.47) and slower inside training: 71.0 / 71.0 vs
-// 75.3 / 74.9 M env steps/s, the same box interleaved (profiles/r04p/)
-#ifndef MZ_QACT2_AHEAD
-#define MZ_QACT2_AHEAD 1
-#endif
 constexpr int MI2 = RT2 / 16;      // k_qact2 row fragments per wave
 
 typedef __attribute__((ext_vector_type(8))) __bf16 frag_ab;
@@ -697,7 +691,7 @@ void k_qfc1(MzQAct q, int row_tiles, const uint16_t* __restrict__ feat) {
 // ---- k_qact2 -------------------------------------------------------------------------------
 template <bool RELU>
 __global__ __launch_bounds__(512) void k_qact2(MzQAct q) {
-  __shared__ __align__(16) uint16_t A[2][2][RT2 * ARS];
+  __shared__ __align__(16) uint16_t A[2][1][2][RT2 * ARS];  // [buffer][chunk][hi, lo]
   __shared__ float part[8][RT2][4];
   const int tid = threadIdx.x, lane = tid & (WAVE - 1);
   const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);
@@ -720,15 +714,15 @@ __global__ __launch_bounds__(512) void k_qact2(MzQAct q) {
       a.v[u] = *reinterpret_cast<const f32x4*>(q.h1 + (size_t)(r0 + min(ar + 64 * u, nr - 1)) * N1 + 32 * c + ak);
     return a;
   };
-  auto store_a = [&](int buf, const AV& a) {
+  auto store_a = [&](int buf, int sub, const AV& a) {
 #pragma unroll
     for (int u = 0; u < AU; ++u) {
       uint32_t h0, l0, h1, l1;
       split2(a.v[u].x, a.v[u].y, h0, l0);
       split2(a.v[u].z, a.v[u].w, h1, l1);
       const int o = a_off(ar + 64 * u, ak >> 3) + (ak & 7);
-      uint32_t* ph = reinterpret_cast<uint32_t*>(A[buf][0] + o);
-      uint32_t* pl = reinterpret_cast<uint32_t*>(A[buf][1] + o);
+      uint32_t* ph = reinterpret_cast<uint32_t*>(A[buf][sub][0] + o);
+      uint32_t* pl = reinterpret_cast<uint32_t*>(A[buf][sub][1] + o);
       ph[0] = h0; ph[1] = h1;
       pl[0] = l0; pl[1] = l1;
     }
@@ -754,9 +748,9 @@ __global__ __launch_bounds__(512) void k_qact2(MzQAct q) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = frag_cd{0.0f, 0.0f, 0.0f, 0.0f};
   constexpr int NC2 = N1 / 32;
-  auto chunk_mfma = [&](int buf, const uint4 (&b_h)[4], const uint4 (&b_l)[4]) {
-    const uint16_t* Ah = A[buf][0];
-    const uint16_t* Al = A[buf][1];
+  auto chunk_mfma = [&](int buf, int sub, const uint4 (&b_h)[4], const uint4 (&b_l)[4]) {
+    const uint16_t* Ah = A[buf][sub][0];
+    const uint16_t* Al = A[buf][sub][1];
 #pragma unroll
     for (int h = 0; h < MI2; h += 4) {  // four row fragments at a time (register pressure)
       frag_ab ah[4], al[4];
@@ -769,33 +763,12 @@ __global__ __launch_bounds__(512) void k_qact2(MzQAct q) {
       mfma_x3<4>(ah, al, b_h, b_l, *reinterpret_cast<frag_cd(*)[4][4]>(&acc[h]));
     }
   };
-#if MZ_QACT2_AHEAD == 2
-  // h1 chunks loaded two chunks ahead of their LDS store (s1 / s0), the fc2 fragments two chunks
-  // ahead in two register sets, each load issued right after the MFMAs that free its registers
-  static_assert(NC2 % 2 == 0, "loop unrolled by two");
-  store_a(0, load_a(0));
-  AV s1 = load_a(1);  // the loop's load order (as k_qfc1's prologue)
-  __builtin_amdgcn_sched_barrier(0);
-  load_b(0, bh, bl);
-  __builtin_amdgcn_sched_barrier(0);
-  AV s0 = load_a(2);
-  __builtin_amdgcn_sched_barrier(0);
-  load_b(1, nbh, nbl);
-  __syncthreads();
-  for (int c = 0; c < NC2; c += 2) {
-    chunk_mfma(0, bh, bl);
-    load_b(min(c + 2, NC2 - 1), bh, bl);  // unconditional, clamped: as k_qfc1
-    store_a(1, s1);
-    s1 = load_a(min(c + 3, NC2 - 1));
-    __syncthreads();
-    chunk_mfma(1, nbh, nbl);
-    load_b(min(c + 3, NC2 - 1), nbh, nbl);
-    store_a(0, s0);
-    s0 = load_a(min(c + 4, NC2 - 1));
-    __syncthreads();
-  }
-#else
-  store_a(0, load_a(0));
+  // one chunk ahead, one barrier per chunk. Measured and not kept, all faster alone and slower
+  // inside training (the update stream's kernels share the CUs): h1 chunks and fc2 fragments two
+  // chunks ahead (MFMA busy 0.43 -> 0.47; 71.0 / 71.0 vs 75.3 / 74.9 M env steps/s,
+  // profiles/r04p/), two chunks per LDS stage (0.50 -> 0.51; 72.1 / 72.7 vs 75.8 / 76.4 M,
+  // profiles/r04t/)
+  store_a(0, 0, load_a(0));
   load_b(0, bh, bl);
   AV na = {};
   __syncthreads();
@@ -804,9 +777,9 @@ __global__ __launch_bounds__(512) void k_qact2(MzQAct q) {
       na = load_a(c + 1);
       load_b(c + 1, nbh, nbl);
     }
-    chunk_mfma(c & 1, bh, bl);
+    chunk_mfma(c & 1, 0, bh, bl);
     if (c + 1 < NC2) {
-      store_a((c + 1) & 1, na);
+      store_a((c + 1) & 1, 0, na);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         bh[j] = nbh[j];
@@ -815,7 +788,6 @@ __global__ __launch_bounds__(512) void k_qact2(MzQAct q) {
     }
     __syncthreads();
   }
-#endif
 
   // h2 = act(acc + b2) in f32; fc3 partial sums over this wave's 64 columns, per row and action,
   // four row fragments at a time
