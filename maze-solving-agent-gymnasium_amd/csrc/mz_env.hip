@@ -718,6 +718,13 @@ __global__ __launch_bounds__(WAVE) void k_bank_fill(MzDev bd, const int* head, i
 // measured best there (68.3 / 68.5 vs 67.0 / 67.4 M env steps/s with 4,
 // profiles/r03_adamw_qw8_rd1/train.jsonl); config 2's 4,096 instances (64 groups) spent 218 us
 // per vector step here with one wave per group (profiles/r04f_cfg2_train_streams.json).
+// k_reset_done's rare in-place build (no bank class, or the bank is exhausted), out of line and
+// taking the handle by value: a call that takes the kernel argument's address made every wave
+// copy the whole MzDev to scratch on entry (~20 scratch stores per lane), resets or not
+__device__ __noinline__ void reset_build_cold(MzDev d, int e, bool tor, uint64_t seed, uint8_t* lds) {
+  mz_build_one(d, e, tor, true, d.algo[e], seed, (int)(d.meta0[e] & 0xFF), nullptr, 0, 0, 0, 0, lds);
+}
+
 template <bool TOR, bool ENRICH>
 __global__ __launch_bounds__(WAVE) void k_reset_done(MzDev d, int regen, uint64_t seed,
                                                      uint32_t epoch, MzOut o, int split) {
@@ -753,8 +760,7 @@ __global__ __launch_bounds__(WAVE) void k_reset_done(MzDev d, int regen, uint64_
     if (__shfl((int)win, j)) {
       have_meta = bank_take(d, ej, cj, sj, meta);
       if (!have_meta)  // no bank class or the bank is exhausted: build in place
-        mz_build_one(d, ej, TOR, true, d.algo[ej], seed + (uint64_t)ej + ((uint64_t)epoch << 32),
-                     (int)(d.meta0[ej] & 0xFF), nullptr, 0, 0, 0, 0, lds);
+        reset_build_cold(d, ej, TOR, seed + (uint64_t)ej + ((uint64_t)epoch << 32), lds);
       __syncthreads();  // this workgroup's global stores are visible to it past the barrier
     }
     reset_one<TOR, ENRICH>(d, ej, o, wsh, have_meta ? &meta : nullptr);
