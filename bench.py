@@ -82,6 +82,11 @@ def parse(argv=None):
     ap.add_argument("--train-steps", type=int, default=2400,
                     help="DDQN vector steps for the win-rate half of the metric (0 = skip)")
     ap.add_argument("--eval-mazes", type=int, default=1000)
+    ap.add_argument("--candidates", type=int, default=6,
+                    help="mazes the trainers train on: each the easiest of C candidates by McClendon "
+                         "difficulty (the reference env's generate_maze, base_maze_env.py:78-97) — "
+                         "the initial mazes and the maze bank's replacements for winners; 1 = one "
+                         "Philox maze each")
     ap.add_argument("--curriculum-envs", type=int, default=4096)
     ap.add_argument("--curriculum-dim", type=int, default=41)
     ap.add_argument("--curriculum-updates", type=int, default=4)
@@ -147,9 +152,12 @@ def win_rate(a, dev, rank=0, world=1):
     from mazerl.agents.dqn import VectorDQNLearner
     from mazerl.distributed import GradAllReduce, broadcast_params
     from mazerl.trainers.vector_trainer import VectorOffPolicyTrainer, best_of_mazes, evaluate
+    t_gen = time.perf_counter()
     env = VectorMazeEnv(a.envs, a.dim, enrich=True, device=dev, algorithm=a.algo,
                         seed=0xA11CE + rank * a.envs, done_list=False, window=False,
-                        window_bits=True)  # acting reads the bits
+                        window_bits=True, candidates=a.candidates)  # acting reads the bits
+    torch.cuda.synchronize()
+    t_gen = time.perf_counter() - t_gen
     decay = ((a.dim - 1) * (a.dim - 1) // 2) * 5 / 40.0
     L = VectorDQNLearner(a.envs, dev, variant="ddqn", lr=1e-3, eps_start=0.95, eps_final=0.1,
                          eps_decay=decay, gamma=0.7, batch_size=a.batch, capacity=2_000_000,
@@ -159,15 +167,19 @@ def win_rate(a, dev, rank=0, world=1):
     if world > 1:
         broadcast_params(L.source)
         L.target.load_state_dict(L.source.state_dict())
-    tr = VectorOffPolicyTrainer(env, L, seed=3 + 7919 * rank, fused=bool(a.fused_bookkeeping))
+    tr = VectorOffPolicyTrainer(env, L, seed=3 + 7919 * rank, fused=bool(a.fused_bookkeeping),
+                                bank_candidates=a.candidates)
     tr.train(20)  # warm-up: MIOpen / hipBLASLt first calls
     if world > 1:
         dist.barrier()
+    w0, e0 = int(tr.wins), int(tr.episodes)
     secs = tr.train(a.train_steps, **progress(rank, "win-rate leg"))
     if world > 1:
         t = torch.tensor([secs], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         secs = float(t.item())
+    train_wins, train_eps = int(tr.wins) - w0, int(tr.episodes) - e0
+    sel = env.select_stats()
     env.close()
     if rank != 0:
         return None
@@ -192,6 +204,16 @@ def win_rate(a, dev, rank=0, world=1):
                 "after 125 single-env episodes with its change_algorithm curriculum (README.md); "
                 "see curriculum_leg for the curriculum-trained learner")),
             "eval_mazes": n, "variant": "ddqn",
+            "training_mazes": {
+                "candidates": a.candidates,
+                "selection": ("each the easiest of %d by McClendon difficulty, chosen on the GPU "
+                              "(initial mazes: mz_generate_best; winners' new mazes: the maze "
+                              "bank's best-of-C refills on the side stream)" % a.candidates)
+                             if a.candidates > 1 else "one Philox maze each (no selection)",
+                "initial_generation_seconds": round(t_gen, 3),
+                "selection_stats": sel,
+                "wins_per_vector_step": train_wins / max(1, a.train_steps),
+                "episodes_per_vector_step": train_eps / max(1, a.train_steps)},
             "ranks": world, "train_vector_steps": a.train_steps + 20,
             "train_seconds_steady": round(secs, 3),
             "train_env_steps_per_s": a.envs * a.train_steps * world / secs,

@@ -36,6 +36,7 @@ extern "C" {
 
 #define MZ_MAX_DIM 127
 #define MZ_BANK_MAX_DIMS 64  /* maze sizes one bank can hold (mz_bank_create_dims) */
+#define MZ_MAX_CANDIDATES 64 /* candidates of a best-of-C selection (mz_bank_create_ex, mz_generate_best) */
 #define MZ_WINDOW 15
 #define MZ_WINDOW_BITS 675   /* 3 x 15 x 15 */
 #define MZ_WINDOW_WORDS 22   /* uint32 words per instance in window_bits (bits 675..703 zero) */
@@ -99,9 +100,38 @@ int mz_load_mazes(mz_handle* h, const uint8_t* grids_host, int32_t dim,
  * per-instance algorithm ids (algo_dev [n] or NULL = algo_all) and Philox seeds
  * seed + env_id; then builds tables and resets them. Replaces gen_maze / gen_maze_no_border
  * (maze_generation.py:6-56) + update_new_maze (simple_maze_env.py:118-127) with candidates=1
- * (best-of-6 difficulty selection, base_maze_env.py:78-97, is not applied — documented). */
+ * (the best-of-6 difficulty selection, base_maze_env.py:78-97, is mz_generate_best). */
 int mz_generate(mz_handle* h, const int32_t* env_ids_dev, int32_t n, const uint8_t* algo_dev,
                 int32_t algo_all, int32_t dim, uint64_t seed, void* stream);
+
+/* Best-of-C generation: the reference's new-maze selection (BaseMazeEnv.generate_maze,
+ * base_maze_env.py:78-97; ToroidalMazeEnv.generate_maze, toroidal_maze_env.py:40-54: six
+ * gen_maze / gen_maze_no_border candidates, the one with the smallest McClendon difficulty —
+ * maze_complexity_evaluation.py:319-329, a toroidal maze scored as its bordered maze — kept, the
+ * first on ties) for the listed instances, on the GPU: `candidates` Philox mazes per instance
+ * (candidate c of instance e: seed + e * candidates + c, the mazes mz_generate of
+ * n * candidates instances from `seed` builds for instances e * candidates + c), scored by the
+ * difficulty kernel, the first minimum copied into the instance (which is then reset like after
+ * mz_generate). candidates == 1 is mz_generate_ex(MZ_RNG_PHILOX). Selection statistics:
+ * mz_select_stats. Replaces update_new_maze (simple_maze_env.py:118-127) / the env constructors'
+ * first maze (simple_maze_env.py:19-36). */
+int mz_generate_best(mz_handle* h, const int32_t* env_ids_dev, int32_t n, const uint8_t* algo_dev,
+                     int32_t algo_all, int32_t dim, uint64_t seed, int32_t candidates,
+                     void* stream);
+/* Counters of every best-of-C selection on this handle (bank refills and mz_generate_best) ->
+ * out3_dev [3] int32 (device, nullable): groups with a candidate the GPU difficulty kernel leaves
+ * to the host (status != 0; the group picks among the others), groups where a candidate listed
+ * before the chosen one lies within a relative 2^-40 of its difficulty product (its log could
+ * tie the chosen one's: the reference would keep the earlier), groups selected. reset != 0 zeroes
+ * them after the copy. */
+int mz_select_stats(mz_handle* h, int32_t* out3_dev, int32_t reset, void* stream);
+/* Per-instance size of a winner's next maze for mz_reset_done / mz_reset_list with regen_won:
+ * dims_dev [B] uint8 (device, owned by the caller, read by every later reset launch; NULL = each
+ * instance's current size, the default). 0 = the winner keeps its maze and is only reset — the
+ * variable-size envs' update_maze when `shape + 4 > max_shape` (simple_variable_maze_env.py:93-112,
+ * toroidal_variable_maze_env.py:113-131), which leaves the maze as it is. A value the handle cannot
+ * hold (even, < 5, > max_dim) counts as 0. */
+int mz_set_regen_dims(mz_handle* h, const uint8_t* dims_dev);
 
 /* rng of mz_generate_ex:
  *   MZ_RNG_PHILOX   Philox4x32 stream seed + env_id (as mz_generate): every random choice of the
@@ -201,8 +231,22 @@ int mz_bank_create(mz_handle* h, int32_t slots, int32_t dim, uint32_t algo_mask)
  * Philox seeds with di << 48 (di = 0: mz_bank_create's). */
 int mz_bank_create_dims(mz_handle* h, int32_t slots, const int32_t* dims, int32_t ndims,
                         uint32_t algo_mask);
+/* mz_bank_create_dims whose slots are best-of-`candidates` mazes (1..MZ_MAX_CANDIDATES): every
+ * refilled slot is the easiest of `candidates` mazes by McClendon difficulty, the first on ties —
+ * the reference's generate_maze selection for the new maze of a win (base_maze_env.py:78-97,
+ * toroidal_maze_env.py:40-54, via update_maze at off_policy_trainer.py:202 / ppo_trainer.py:96).
+ * Candidate c of slot j of a fill: Philox key + j * candidates + c + (epoch << 32) with the
+ * block's key as mz_bank_fill's (candidates = 1: mz_bank_create_dims exactly). Needs the
+ * difficulty kernel's LDS plan (max_dim <= 91 euclidean, <= 89 toroidal) when candidates > 1;
+ * the K * candidates candidate mazes live in scratch owned by the handle. */
+int mz_bank_create_ex(mz_handle* h, int32_t slots, const int32_t* dims, int32_t ndims,
+                      uint32_t algo_mask, int32_t candidates);
 /* Rebuild the slots of `bank` consumed since its last fill (every slot on the first fill). */
 int mz_bank_fill(mz_handle* h, int32_t bank, uint64_t seed, void* stream);
+/* Inspect one bank slot (synchronous; tests): the grid (0 wall, 1 floor, 2 goal) into
+ * grid_host [N][N] (N = the slot's size, <= max_dim) and (start r, start c, goal r, goal c). */
+int mz_bank_slot_grid(mz_handle* h, int32_t bank, int32_t algo, int32_t size_index, int32_t slot,
+                      uint8_t* grid_host, int32_t* info4_host);
 /* Bank consumed by later mz_reset_done(regen_won) launches; -1 = none (build in place). */
 int mz_bank_use(mz_handle* h, int32_t bank);
 /* Consumed-slot counters of `bank` per algorithm id and size index -> out3_dev [3][ndims] int32
@@ -375,7 +419,8 @@ int mz_maze_complexity(const uint8_t* grid_host, int32_t h, int32_t w, int32_t s
  * the LDS plan holds, a hallway of more than 63 view nodes), 3 invalid (start == goal, bad id,
  * log domain) — the caller computes every nonzero-status maze with mz_difficulty (toroidal: on
  * the bordered grid). Asynchronous on `stream`. Returns MZ_EINVAL_SHAPE when the evaluated grid's
- * pitch exceeds the kernel's LDS plan (P > 92; toroidal P > 87). */
+ * pitch exceeds the kernel's LDS plan (odd pitches: P > 91; toroidal P > 89 — the bordered grid
+ * is P + 2; tests/test_abi.py derives both limits from the plan). */
 int mz_difficulty_batch(mz_handle* h, const int32_t* env_ids_dev, int32_t n, double* out_dev,
                         int32_t* status_dev, void* stream);
 

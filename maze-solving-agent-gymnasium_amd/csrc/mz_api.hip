@@ -5,6 +5,7 @@
 // MZ_EINVAL_SHAPE), builds the exact penalty tables once (glibc exp, like CPython's math.exp),
 // and launches the kernels of mz_env.hip. No compute path runs on the host: every env quantity is
 // produced by a gfx950 kernel.
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -18,8 +19,20 @@
 #include "mz_learner.h"
 #include "mz_mcclendon.h"
 
+// Candidate mazes of a best-of-C selection (maze bank refills with C > 1, mz_generate_best): an
+// MzDev view over `cap` scratch instances (cells, plane strips, per-instance words) plus the
+// McClendon output per candidate.
+struct MzCandStore {
+  int cap = 0;
+  MzDev v{};
+  double* score = nullptr;    // [cap][2]: prod_b (C_b + 1) * C_0, sum (k_mcclendon)
+  int32_t* status = nullptr;  // [cap]
+};
+
 struct MzBankStore {  // two banks x the enabled algorithms x sizes x K slots (mz_bank_*)
   int K = 0, nA = 0, nD = 0;
+  int C = 1;                   // candidates per slot (best-of-C by McClendon difficulty)
+  MzCandStore cand;            // K * C candidates (C > 1), reused by every block's refill
   int dims[MZ_BANK_MAX_DIMS] = {};
   uint32_t amask = 0;
   uint32_t* cells = nullptr;   // [2][nA][nD][K][P*P]
@@ -41,6 +54,8 @@ struct mz_handle {
   uint8_t* staging = nullptr;
   size_t staging_bytes = 0;
   MzBankStore bank;
+  MzCandStore gen;             // mz_generate_best's candidates (chunks of the instance list)
+  int* sel_stats = nullptr;    // [4] best-of-C selections: unresolved groups, near ties, groups
 };
 
 namespace {
@@ -132,6 +147,26 @@ int alloc(mz_handle* h, T** p, size_t count) {
   return MZ_OK;
 }
 
+// scratch for `cap` candidate mazes: a view of the handle's layout over its own arrays
+int cand_alloc(mz_handle* h, MzCandStore& cs, int cap) {
+  const MzDev& d = h->d;
+  MzDev v = d;
+  const size_t n = (size_t)cap, P = (size_t)d.P;
+  int rc;
+  if ((rc = alloc(h, &v.cells, n * P * P)) || (rc = alloc(h, &v.planes, n * (size_t)d.PW + 16)) ||
+      (rc = alloc(h, &v.meta0, n)) || (rc = alloc(h, &v.meta1, n)) || (rc = alloc(h, &v.posw, n)) ||
+      (rc = alloc(h, &v.stw, n)) || (rc = alloc(h, &v.curw, n)) || (rc = alloc(h, &v.algo, n)) ||
+      (rc = alloc(h, &v.last_term, n)) || (rc = alloc(h, &cs.score, 2 * n)) ||
+      (rc = alloc(h, &cs.status, n)))
+    return rc;
+  v.B = cap;
+  v.bk_K = 0;
+  v.regen_dim = nullptr;
+  cs.v = v;
+  cs.cap = cap;
+  return MZ_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -169,7 +204,7 @@ int mz_create(const mz_config* cfg, mz_handle** out) {
       (rc = alloc(h, &d.meta0, B)) ||
       (rc = alloc(h, &d.meta1, B)) || (rc = alloc(h, &d.posw, B)) || (rc = alloc(h, &d.stw, B)) ||
       (rc = alloc(h, &d.curw, B)) || (rc = alloc(h, &d.algo, B)) || (rc = alloc(h, &d.last_term, B)) ||
-      (rc = alloc(h, &d.ticket, 16))) {
+      (rc = alloc(h, &d.ticket, 16)) || (rc = alloc(h, &h->sel_stats, 4))) {
     mz_destroy(h);
     return rc;
   }
@@ -518,11 +553,20 @@ int mz_pair_surrogate(const float* lp_new_dev, const float* lp_old_dev, const fl
 
 int mz_stem_workspace_floats(int32_t n) { return n > 0 ? mz_stem_chunks(n) * 32 * 28 : 0; }
 
-int mz_bank_create_dims(mz_handle* h, int32_t slots, const int32_t* dims, int32_t ndims,
-                        uint32_t algo_mask) {
+int mz_bank_create_ex(mz_handle* h, int32_t slots, const int32_t* dims, int32_t ndims,
+                      uint32_t algo_mask, int32_t candidates) {
   if (!h) return fail(MZ_EINVAL, "null handle");
   if (h->bank.K) return fail(MZ_EINVAL, "the handle already has a maze bank");
   if (slots < 1) return fail(MZ_EINVAL, "bank slots %d", slots);
+  if (candidates < 1 || candidates > MZ_MAX_CANDIDATES)
+    return fail(MZ_EINVAL, "candidates %d outside [1, %d]", candidates, MZ_MAX_CANDIDATES);
+  if (candidates > 1) {
+    int mm = 0;
+    if (mz_mcclendon_lds(h->d.P, h->d.toroidal != 0, &mm) > 160 * 1024)
+      return fail(MZ_EINVAL_SHAPE, "best-of-%d banks score with the difficulty kernel: maze pitch "
+                  "%d beyond its LDS plan", candidates, h->d.P);
+    if ((int64_t)slots * candidates > (1 << 24)) return fail(MZ_EINVAL, "slots x candidates too large");
+  }
   if (algo_mask == 0 || algo_mask > 7u) return fail(MZ_EINVAL, "algorithm mask %u", algo_mask);
   if (!dims || ndims < 1 || ndims > MZ_BANK_MAX_DIMS) return fail(MZ_EINVAL, "bank sizes %d", ndims);
   for (int i = 0; i < ndims; ++i) {
@@ -553,11 +597,21 @@ int mz_bank_create_dims(mz_handle* h, int32_t slots, const int32_t* dims, int32_
   for (int i = 0; i < ndims; ++i) b.dims[i] = dims[i];
   b.nA = nA;
   b.amask = algo_mask;
+  b.C = candidates;
+  if (candidates > 1 && (rc = cand_alloc(h, b.cand, slots * candidates))) {
+    b.K = 0;  // no bank: a later create may retry
+    return rc;
+  }
   return MZ_OK;
 }
 
+int mz_bank_create_dims(mz_handle* h, int32_t slots, const int32_t* dims, int32_t ndims,
+                        uint32_t algo_mask) {
+  return mz_bank_create_ex(h, slots, dims, ndims, algo_mask, 1);
+}
+
 int mz_bank_create(mz_handle* h, int32_t slots, int32_t dim, uint32_t algo_mask) {
-  return mz_bank_create_dims(h, slots, &dim, 1, algo_mask);
+  return mz_bank_create_ex(h, slots, &dim, 1, algo_mask, 1);
 }
 
 int mz_bank_fill(mz_handle* h, int32_t bank, uint64_t seed, void* stream) {
@@ -586,7 +640,17 @@ int mz_bank_fill(mz_handle* h, int32_t bank, uint64_t seed, void* stream) {
     int* head = b.heads + (3 * bank + a) * b.nD + di;
     // (size index di = 0 keeps the single-size bank's keys)
     const uint64_t key = seed ^ ((uint64_t)(3 * bank + a + 1) << 56) ^ ((uint64_t)di << 48);
-    MZ_HIP(mz_launch_bank_fill(bd, head, b.K, a, b.dims[di], key, b.epoch[bank], s));
+    if (b.C > 1) {  // best-of-C: candidates, their difficulty, the first minimum into the slot
+      const MzDev& cv = b.cand.v;
+      MZ_HIP(mz_launch_cand_build(cv, nullptr, 0, head, b.K, b.C, nullptr, a, b.dims[di], key,
+                                  b.epoch[bank], s));
+      MZ_HIP(mz_launch_mcclendon(cv, nullptr, b.K * b.C, b.cand.score, b.cand.status, s, head, b.C));
+      MZ_HIP(mz_launch_cand_select(cv, bd, nullptr, 0, head, b.K, b.C, b.cand.score, b.cand.status,
+                                   h->sel_stats, s));
+    } else {
+      MZ_HIP(mz_launch_cand_build(bd, nullptr, 0, head, b.K, 1, nullptr, a, b.dims[di], key,
+                                  b.epoch[bank], s));
+    }
     MZ_HIP(hipMemsetAsync(head, 0, sizeof(int), s));
     }
   }
@@ -617,6 +681,90 @@ int mz_bank_use(mz_handle* h, int32_t bank) {
   d.bk_head = b.heads + 3 * bank * b.nD;
   d.bk_slot = b.slot;
   d.bk_G = (d.B + 63) / 64;
+  return MZ_OK;
+}
+
+int mz_bank_slot_grid(mz_handle* h, int32_t bank, int32_t algo, int32_t size_index, int32_t slot,
+                      uint8_t* grid_host, int32_t* info4_host) {
+  if (!h || !h->bank.K || !grid_host || !info4_host) return fail(MZ_EINVAL, "bad arguments");
+  const MzBankStore& b = h->bank;
+  if (bank < 0 || bank > 1 || algo < 0 || algo > 2 || !((b.amask >> algo) & 1u) ||
+      size_index < 0 || size_index >= b.nD || slot < 0 || slot >= b.K)
+    return fail(MZ_EINVAL, "no such bank slot");
+  DeviceGuard g(h->cfg.device);
+  MZ_HIP(hipDeviceSynchronize());
+  const size_t P = (size_t)h->d.P;
+  const size_t i = (((size_t)bank * b.nA + mz_bank_aidx(b.amask, algo)) * b.nD + size_index) * b.K + slot;
+  uint32_t m0, m1;
+  MZ_HIP(hipMemcpy(&m0, b.meta0 + i, 4, hipMemcpyDeviceToHost));
+  MZ_HIP(hipMemcpy(&m1, b.meta1 + i, 4, hipMemcpyDeviceToHost));
+  std::vector<uint32_t> cw(P * P);
+  MZ_HIP(hipMemcpy(cw.data(), b.cells + i * P * P, 4 * cw.size(), hipMemcpyDeviceToHost));
+  const int N = m0 & 0xFF, gr = m1 & 0xFF, gc = (m1 >> 8) & 0xFF;
+  if (N < 5 || N > (int)P) return fail(MZ_EINVAL, "bank slot not built");
+  for (int r = 0; r < N; ++r)
+    for (int c = 0; c < N; ++c) {
+      const bool open = (cw[(size_t)r * P + c] & MZ_CELL_OPEN) != 0;
+      grid_host[r * N + c] = !open ? 0 : ((r == gr && c == gc) ? 2 : 1);
+    }
+  info4_host[0] = (m0 >> 16) & 0xFF;
+  info4_host[1] = m0 >> 24;
+  info4_host[2] = gr;
+  info4_host[3] = gc;
+  return MZ_OK;
+}
+
+int mz_set_regen_dims(mz_handle* h, const uint8_t* dims_dev) {
+  if (!h) return fail(MZ_EINVAL, "null handle");
+  h->d.regen_dim = dims_dev;
+  return MZ_OK;
+}
+
+int mz_generate_best(mz_handle* h, const int32_t* env_ids_dev, int32_t n, const uint8_t* algo_dev,
+                     int32_t algo_all, int32_t dim, uint64_t seed, int32_t candidates,
+                     void* stream) {
+  if (!h) return fail(MZ_EINVAL, "null handle");
+  if (candidates < 1 || candidates > MZ_MAX_CANDIDATES)
+    return fail(MZ_EINVAL, "candidates %d outside [1, %d]", candidates, MZ_MAX_CANDIDATES);
+  if (candidates == 1)
+    return mz_generate_ex(h, env_ids_dev, n, algo_dev, algo_all, dim, seed, MZ_RNG_PHILOX, stream);
+  if (!env_ids_dev) n = h->d.B;
+  if (n < 0 || n > h->d.B) return fail(MZ_EINVAL, "n out of range");
+  if (!algo_dev && (algo_all < 0 || algo_all > 2)) return fail(MZ_EINVAL, "algorithm id %d", algo_all);
+  int rc = check_dim(h, dim);
+  if (rc) return rc;
+  int mm = 0;
+  if (mz_mcclendon_lds(h->d.P, h->d.toroidal != 0, &mm) > 160 * 1024)
+    return fail(MZ_EINVAL_SHAPE, "best-of-%d generation scores with the difficulty kernel: maze "
+                "pitch %d beyond its LDS plan", candidates, h->d.P);
+  if (n == 0) return MZ_OK;
+  DeviceGuard g(h->cfg.device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // chunks of <= 49,152 candidates (1.45 GB of scratch at 81 x 81)
+  const int chunk = std::max(1, std::min(n, 49152 / candidates));
+  if (h->gen.cap < chunk * candidates) {
+    if (h->gen.cap) MZ_HIP(hipStreamSynchronize(s));  // (the old scratch stays owned by the handle)
+    if ((rc = cand_alloc(h, h->gen, chunk * candidates))) return rc;
+  }
+  const MzDev& cv = h->gen.v;
+  for (int j0 = 0; j0 < n; j0 += chunk) {
+    const int m = std::min(chunk, n - j0);
+    const int32_t* ids = env_ids_dev ? env_ids_dev + j0 : nullptr;
+    const uint8_t* al = algo_dev ? algo_dev + j0 : nullptr;
+    MZ_HIP(mz_launch_cand_build(cv, ids, j0, nullptr, m, candidates, al, algo_all, dim, seed, 0u, s));
+    MZ_HIP(mz_launch_mcclendon(cv, nullptr, m * candidates, h->gen.score, h->gen.status, s));
+    MZ_HIP(mz_launch_cand_select(cv, h->d, ids, j0, nullptr, m, candidates, h->gen.score,
+                                 h->gen.status, h->sel_stats, s));
+  }
+  return MZ_OK;
+}
+
+int mz_select_stats(mz_handle* h, int32_t* out3_dev, int32_t reset, void* stream) {
+  if (!h) return fail(MZ_EINVAL, "null handle");
+  DeviceGuard g(h->cfg.device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (out3_dev) MZ_HIP(hipMemcpyAsync(out3_dev, h->sel_stats, 3 * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+  if (reset) MZ_HIP(hipMemsetAsync(h->sel_stats, 0, 4 * sizeof(int32_t), s));
   return MZ_OK;
 }
 

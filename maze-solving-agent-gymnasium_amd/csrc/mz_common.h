@@ -81,7 +81,19 @@ struct MzDev {
   // of the group's winners, bk_slot[class * bk_G + g]
   int* bk_slot;             // [3 * bk_nd][bk_G]
   int bk_G;                 // 64-instance groups, ceil(B / 64)
+  // per-instance size of a winner's next maze (the variable-size envs' update_maze growth,
+  // simple_variable_maze_env.py:93-112 / toroidal_variable_maze_env.py:113-131): 0 = the winner
+  // keeps its maze (the reference's `shape > max_shape` branch), null = its current size
+  const uint8_t* regen_dim;
 };
+
+// size of instance e's next maze when it wins (0: no new maze; a size the handle cannot hold —
+// even, < 5 or above the pitch — counts as 0, so no build can write past the instance's arrays)
+__device__ inline int mz_regen_dim(const MzDev& d, int e) {
+  if (!d.regen_dim) return (int)(d.meta0[e] & 0xFF);
+  const int n = (int)d.regen_dim[e];
+  return (n >= 5 && n <= d.P && (n & 1)) ? n : 0;
+}
 
 __host__ __device__ inline int mz_bank_aidx(uint32_t amask, int a) {
   return __builtin_popcount(amask & ((1u << a) - 1u));

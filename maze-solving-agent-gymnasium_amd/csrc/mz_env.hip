@@ -598,7 +598,7 @@ __global__ __launch_bounds__(WAVE) void k_reset_list(MzDev d, const int32_t* idx
 // size index di, -1 when no bank is in use or the bank does not hold that algorithm / size.
 __device__ inline int bank_class(const MzDev& d, int e) {
   if (d.bk_K == 0) return -1;
-  const int a = d.algo[e], N = (int)(d.meta0[e] & 0xFF);
+  const int a = d.algo[e], N = mz_regen_dim(d, e);
   if (N >= 128 || !((d.bk_amask >> a) & 1u)) return -1;
   const int di = d.bk_didx[N];
   return di < 0 ? -1 : a * d.bk_nd + di;
@@ -606,7 +606,7 @@ __device__ inline int bank_class(const MzDev& d, int e) {
 
 // whether instance e is a winner k_reset_done(regen) gives a new maze
 __device__ inline bool regen_winner(const MzDev& d, int e) {
-  return e < d.B && ((d.posw[e] >> 20) & 1u) && d.last_term[e];
+  return e < d.B && ((d.posw[e] >> 20) & 1u) && d.last_term[e] && mz_regen_dim(d, e) != 0;
 }
 
 // Copy n words, each lane keeping 32 loads in flight (a one-word-per-pass loop waits a full
@@ -693,16 +693,83 @@ __global__ __launch_bounds__(BS_T) void k_bank_scan(MzDev d) {
   if (t == 0) d.bk_head[c] = carry;
 }
 
-// Fill one bank block (algorithm `algo`, `bd` = MzDev view whose instance arrays are the block's
-// slots): rebuild the slots consumed since the last fill (all of them when *head >= K).
-__global__ __launch_bounds__(WAVE) void k_bank_fill(MzDev bd, const int* head, int K, int algo,
-                                                    int dim, uint64_t seed, uint32_t epoch) {
+// Candidate builds (one wave per maze, persistent): target j of a list of n targets (n = the
+// static count, or min(*count, n) — a bank block's slots consumed since its last fill) gets C
+// candidate mazes at indices j * C + c of the view `cd`, Philox seed
+//   seed + (id(j) * C + c) + (epoch << 32),   id(j) = ids ? ids[j] : base + j,
+// so C = 1 with cd = the bank block is the bank's own fill (seed + slot + epoch << 32), and
+// C > 1 over the instances of a handle draws the candidates best_of_mazes draws for those
+// instances (VectorMazeEnv.generate of n * C instances from `seed`: candidate c of maze k is
+// instance k * C + c, seed + k * C + c). The algorithm: algo_list[j] or algo_all.
+__global__ __launch_bounds__(WAVE) void k_cand_build(MzDev cd, const int32_t* ids, int base,
+                                                     const int* count, int n, int C,
+                                                     const uint8_t* algo_list, int algo_all,
+                                                     int dim, uint64_t seed, uint32_t epoch) {
   extern __shared__ __align__(16) uint8_t lds[];
-  const int used = min(*head, K);
-  for (int j = blockIdx.x; j < used; j += gridDim.x) {
-    mz_build_one(bd, j, bd.toroidal, true, algo, seed + (uint64_t)j + ((uint64_t)epoch << 32), dim,
-                 nullptr, 0, 0, 0, 0, lds);
+  const int used = count ? min(*count, n) : n;
+  for (int t = blockIdx.x; t < used * C; t += gridDim.x) {
+    const int j = t / C, c = t - j * C;
+    const int algo = algo_list ? algo_list[j] : algo_all;
+    const uint64_t id = (uint64_t)(ids ? ids[j] : base + j);
+    if (threadIdx.x == 0) cd.algo[t] = (uint8_t)algo;
+    mz_build_one(cd, t, cd.toroidal, true, algo, seed + id * (uint64_t)C + (uint64_t)c +
+                 ((uint64_t)epoch << 32), dim, nullptr, 0, 0, 0, 0, lds);
     __syncthreads();
+  }
+}
+
+// Best-of-C selection (BaseMazeEnv.generate_maze, base_maze_env.py:78-97; toroidal
+// toroidal_maze_env.py:40-54): target j keeps the candidate with the smallest McClendon
+// difficulty, the FIRST one on ties (the reference replaces only on a strict `<`). The kernel
+// compares prod_b (C_b + 1) * C_0 (k_mcclendon's output, whose math.log the reference compares):
+// log is monotone, so the first minimum of the products is the first minimum of the logs except
+// when two different products round to the same log — counted in stats[1] (a candidate within a
+// relative 2^-40 of the minimum, listed before it), never seen on the fixtures. A group with a
+// candidate the kernel left to the host (status != 0: not a tree, a hallway beyond the wave's set
+// table, ...) picks among the others and is counted in stats[0]; stats[2] counts the groups.
+// One wave per target: the chosen candidate's cells, plane strips and per-instance words are
+// copied into dst instance dst_ids[j] (or base + j).
+__global__ __launch_bounds__(WAVE) void k_cand_select(MzDev cd, MzDev dst, const int32_t* dst_ids,
+                                                      int base, const int* count, int n, int C,
+                                                      const double* score, const int32_t* status,
+                                                      int* stats) {
+  const int used = count ? min(*count, n) : n;
+  const int lane = threadIdx.x;
+  for (int j = blockIdx.x; j < used; j += gridDim.x) {
+    const int t0 = j * C;
+    const bool ok = lane < C && status[t0 + lane] == 0;
+    const double p = lane < C ? score[2 * (t0 + lane)] : 0.0;
+    const unsigned long long okm = __ballot(ok);
+    // first minimum over the resolvable candidates (wave-uniform loop over C <= 64)
+    int pick = 0;
+    double best = 0.0;
+    bool have = false;
+    for (int c = 0; c < C; ++c) {
+      if (!((okm >> c) & 1ull)) continue;
+      const double pc = __shfl(p, c);
+      if (!have || pc < best) { best = pc; pick = c; have = true; }
+    }
+    const bool near = ok && lane < pick && p != best && p <= best * (1.0 + 0x1p-40);
+    const unsigned long long nearm = __ballot(near);
+    if (lane == 0) {
+      if (okm != ((C >= 64) ? ~0ull : ((1ull << C) - 1ull))) atomicAdd(stats + 0, 1);
+      if (nearm) atomicAdd(stats + 1, 1);
+      atomicAdd(stats + 2, 1);
+    }
+    const size_t src = (size_t)(t0 + pick);
+    const size_t de = (size_t)(dst_ids ? dst_ids[j] : base + j);
+    const size_t pp = (size_t)cd.P * cd.P, pw = (size_t)cd.PW;
+    wave_copy(dst.cells + de * pp, cd.cells + src * pp, pp);
+    wave_copy(dst.planes + de * pw, cd.planes + src * pw, pw);
+    if (lane == 0) {
+      dst.meta0[de] = cd.meta0[src];
+      dst.meta1[de] = cd.meta1[src];
+      dst.posw[de] = cd.posw[src];
+      dst.stw[de] = cd.stw[src];
+      dst.curw[de] = cd.curw[src];
+      dst.last_term[de] = cd.last_term[src];
+      dst.algo[de] = cd.algo[src];
+    }
   }
 }
 
@@ -722,7 +789,7 @@ __global__ __launch_bounds__(WAVE) void k_bank_fill(MzDev bd, const int* head, i
 // taking the handle by value: a call that takes the kernel argument's address made every wave
 // copy the whole MzDev to scratch on entry (~20 scratch stores per lane), resets or not
 __device__ __noinline__ void reset_build_cold(MzDev d, int e, bool tor, uint64_t seed, uint8_t* lds) {
-  mz_build_one(d, e, tor, true, d.algo[e], seed, (int)(d.meta0[e] & 0xFF), nullptr, 0, 0, 0, 0, lds);
+  mz_build_one(d, e, tor, true, d.algo[e], seed, mz_regen_dim(d, e), nullptr, 0, 0, 0, 0, lds);
 }
 
 template <bool TOR, bool ENRICH>
@@ -733,7 +800,8 @@ __global__ __launch_bounds__(WAVE) void k_reset_done(MzDev d, int regen, uint64_
   const int grp = blockIdx.x / split, part = blockIdx.x - grp * split;
   const int lane = threadIdx.x, e = grp * WAVE + lane;
   const bool done = e < d.B && ((d.posw[e] >> 20) & 1u);
-  const bool win = regen && done && d.last_term[e];  // gets a new maze (loaded once, coalesced)
+  // gets a new maze (loaded once, coalesced); a winner whose next size is 0 keeps its maze
+  const bool win = regen && done && d.last_term[e] && mz_regen_dim(d, e) != 0;
   // this lane's bank slot if it is a winner with a bank class: the group's first slot of the
   // class (k_bank_scan) + its rank among the group's winners of the class
   int cls = -1, slot = 0;
@@ -799,9 +867,10 @@ __global__ __launch_bounds__(WAVE) void k_regen_list(MzDev d, const int32_t* idx
   const int n = count ? min(*count, n_static) : n_static;
   for (int j = blockIdx.x; j < n; j += gridDim.x) {
     const int e = idx ? idx[j] : j;
-    if (!d.last_term[e]) continue;  // uniform per block
+    const int dim = mz_regen_dim(d, e);
+    if (!d.last_term[e] || dim == 0) continue;  // uniform per block
     mz_build_one(d, e, d.toroidal, true, d.algo[e], seed + (uint64_t)e + ((uint64_t)epoch << 32),
-                 (int)(d.meta0[e] & 0xFF), nullptr, 0, 0, 0, 0, lds);
+                 dim, nullptr, 0, 0, 0, 0, lds);
     __syncthreads();
   }
 }
@@ -1045,16 +1114,29 @@ hipError_t mz_launch_reset_done(const MzDev& d, int regen, uint64_t seed, uint32
   return hipGetLastError();
 }
 
-hipError_t mz_launch_bank_fill(const MzDev& bd, const int* head, int K, int algo, int dim,
-                               uint64_t seed, uint32_t epoch, hipStream_t s) {
-  const size_t lds = mz_build_lds_launch(bd.P, bd.toroidal, true, MZ_PY_PHILOX);
-  hipError_t ae = mz_lds_attr(reinterpret_cast<const void*>(k_bank_fill), lds);
+hipError_t mz_launch_cand_build(const MzDev& cd, const int32_t* ids, int base, const int* count, int n,
+                                int C, const uint8_t* algo_list, int algo_all, int dim,
+                                uint64_t seed, uint32_t epoch, hipStream_t s) {
+  if (n <= 0 || C <= 0) return hipSuccess;
+  const size_t lds = mz_build_lds_launch(cd.P, cd.toroidal, true, MZ_PY_PHILOX);
+  hipError_t ae = mz_lds_attr(reinterpret_cast<const void*>(k_cand_build), lds);
   if (ae != hipSuccess) return ae;
-  // a refill runs beside the trainer's acting and update kernels: MZ_BANK_WGS caps its resident
-  // builds (0 = as many as fit) so that it leaves CUs / LDS to them
-  const int grid = MZ_BANK_WGS > 0 ? std::min(K, MZ_BANK_WGS) : mz_build_grid(K, lds);
-  hipLaunchKernelGGL(k_bank_fill, dim3(std::max(grid, 1)), dim3(WAVE), lds, s, bd, head, K, algo, dim,
-                     seed, epoch);
+  // a bank refill runs beside the trainer's acting and update kernels: MZ_BANK_WGS caps its
+  // resident builds (0 = as many as fit) so that it leaves CUs / LDS to them
+  const int total = n * C;
+  const int grid = MZ_BANK_WGS > 0 ? std::min(total, MZ_BANK_WGS) : mz_build_grid(total, lds);
+  hipLaunchKernelGGL(k_cand_build, dim3(std::max(grid, 1)), dim3(WAVE), lds, s, cd, ids, base, count, n,
+                     C, algo_list, algo_all, dim, seed, epoch);
+  return hipGetLastError();
+}
+
+hipError_t mz_launch_cand_select(const MzDev& cd, const MzDev& dst, const int32_t* dst_ids,
+                                 int base, const int* count, int n, int C, const double* score,
+                                 const int32_t* status, int* stats, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (C < 1 || C > WAVE) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_cand_select, dim3(std::min(n, 4096)), dim3(WAVE), 0, s, cd, dst, dst_ids,
+                     base, count, n, C, score, status, stats);
   return hipGetLastError();
 }
 

@@ -30,8 +30,13 @@ hipError_t mz_launch_qfront(const uint32_t* bits, const float* obs6, const int32
                             const int32_t* count, int n, const float* w, const float* b,
                             float drop_p, uint64_t seed, uint64_t counter, uint16_t* out, int ld,
                             hipStream_t s);
-hipError_t mz_launch_bank_fill(const MzDev& bd, const int* head, int K, int algo, int dim,
-                               uint64_t seed, uint32_t epoch, hipStream_t s);
+// candidate builds / best-of-C selection (maze bank refills with C > 1, mz_generate_best)
+hipError_t mz_launch_cand_build(const MzDev& cd, const int32_t* ids, int base, const int* count, int n,
+                                int C, const uint8_t* algo_list, int algo_all, int dim,
+                                uint64_t seed, uint32_t epoch, hipStream_t s);
+hipError_t mz_launch_cand_select(const MzDev& cd, const MzDev& dst, const int32_t* dst_ids,
+                                 int base, const int* count, int n, int C, const double* score,
+                                 const int32_t* status, int* stats, hipStream_t s);
 size_t mz_metrics_lds_bytes(int P);
 hipError_t mz_launch_metrics(const MzDev& d, const int32_t* env_ids, int32_t n, double* out,
                              hipStream_t s);

@@ -10,6 +10,8 @@
 
 // out[i] = {prod, sum} of instance ids[i] (ids null: i); status[i] 0 ok, 1 not a tree, 2 outside
 // the kernel's cases (host restatement), 3 invalid. Toroidal handles: the bordered maze.
+// limit (device, nullable): only i < min(*limit, n / mult) * mult are scored (the rest untouched).
 size_t mz_mcclendon_lds(int P, bool toroidal, int* mm);
 hipError_t mz_launch_mcclendon(const MzDev& d, const int32_t* ids, int n, double* out,
-                               int32_t* status, hipStream_t s);
+                               int32_t* status, hipStream_t s, const int* limit = nullptr,
+                               int mult = 1);

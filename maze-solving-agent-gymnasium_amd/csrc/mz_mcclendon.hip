@@ -53,6 +53,17 @@ namespace {
 #define MZ_MC_T 1024  // 16 waves: hallways in flight per CU (256: 28 -> 12 ms per 6,000 81x81 mazes)
 #endif
 constexpr int T = MZ_MC_T;  // threads per maze workgroup
+// MZ_MC_PROBE = k (timing experiments only, wrong results): the kernel returns after phase k
+// (1 A squares, 2 B solution path, 3 C dead ends / first(), 4 D node order, 5 E edges,
+// 6 F components, 7 G hallway sums)
+#ifndef MZ_MC_PROBE
+#define MZ_MC_PROBE 0
+#endif
+#define MC_PROBE_AT(k)                                                            \
+  if (MZ_MC_PROBE == (k)) {                                                       \
+    if (threadIdx.x == 0) { out[2 * i] = out[2 * i + 1] = 0.0; status[i] = 0; }   \
+    return;                                                                       \
+  }
 constexpr int WAVE = 64;
 constexpr uint16_t NONE = 0xFFFF;
 constexpr uint8_t F_OPEN = 1, F_POINT = 2, F_SOL = 4, F_JUNC = 8, F_DEAD = 16;
@@ -236,12 +247,15 @@ __device__ inline bool ws_merge(WSet& dst, const WSet& src) {
 typedef unsigned __int128 u128;
 
 __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, int n, int MM,
-                                                 double* out, int32_t* status) {
+                                                 double* out, int32_t* status, const int* limit,
+                                                 int mult) {
   extern __shared__ __align__(16) unsigned char lds[];
   __shared__ int wsum[T / WAVE];
   __shared__ int s_bad, s_nsol, s_noff, s_open, s_edges, s_Hn, s_Bn;
   const int i = blockIdx.x;
   if (i >= n) return;
+  // a bank refill scores the candidates of its consumed slots only: min(*limit, n / mult) groups
+  if (limit && i >= min(*limit, n / mult) * mult) return;
   const int e = ids ? ids[i] : i;
   auto fail = [&](int code) {
     if (threadIdx.x == 0) { out[2 * i] = out[2 * i + 1] = 0.0; status[i] = code; }
@@ -414,6 +428,7 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
     return;
   }
   if (s_bad) { fail(2); return; }
+  MC_PROBE_AT(1)
   // ---- B. the solution path (start -> goal along the goal-rooted parents), its points first --
   if (threadIdx.x == 0) {
     int x = start, k = 0, plain = 0;
@@ -435,6 +450,7 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
   }
   __syncthreads();
   if (s_bad) { fail(2); return; }
+  MC_PROBE_AT(2)
   // ---- C. dead ends (value 1, one open neighbour, off the solution), row-major ranks --------
   {
     int carry = 0;
@@ -473,6 +489,7 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
     }
   }
   __syncthreads();
+  MC_PROBE_AT(3)
   // ---- D. node order: solution points, then (first(x), -D(x)) ---------------------------------
   for (int q = threadIdx.x; q < NN; q += T) {
     if ((fl[q] & F_POINT) && !(fl[q] & F_SOL)) {
@@ -496,6 +513,7 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
     nsq[nsol + k] = (uint16_t)q;
   }
   __syncthreads();
+  MC_PROBE_AT(4)
   // ---- E. contracted edges and each node's adjacency in insertion order ----------------------
   for (int v = threadIdx.x; v < M; v += T) {
     const int q = nsq[v], r = q / N, c = q - r * N;
@@ -553,6 +571,7 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
     nfl[v] = (uint8_t)(deg | (sol ? N_SOL : 0) | (deg == 3 ? N_JUNC : 0));
   }
   __syncthreads();  // the square region is free from here on
+  MC_PROBE_AT(5)
   // ---- F. hallways: components of the non-solution, non-junction nodes -----------------------
   auto in_h = [&](int v) { return !(nfl[v] & N_SOL) && (nfl[v] & 7) != 3; };
   auto in_b = [&](int v) { return !(nfl[v] & N_SOL) || (nfl[v] & N_JUNC); };
@@ -627,6 +646,7 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
   for (int v = threadIdx.x; v < M; v += T) bid[v] = br[v] != NONE ? pref[bmin[br[v]]] : NONE;
   __syncthreads();
   const int Hn = s_Hn, Bn = s_Bn;
+  MC_PROBE_AT(6)
   // ---- G. hallway complexities, one wave per hallway (extract_hallways :186-221,
   // complexity_of_hallway :286-296) ---------------------------------------------------------
   // member lists grouped by hallway id (the phase-F roots / minima are dead now)
@@ -811,6 +831,7 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
   }
   __syncthreads();
   if (s_bad) { fail(2); return; }
+  MC_PROBE_AT(7)
   // hallway 0: the solution branch, edges in path order
   if (threadIdx.x == 0) {
     double s = 0.0;
@@ -879,7 +900,7 @@ size_t mz_mcclendon_lds(int P, bool toroidal, int* mm) {
 }
 
 hipError_t mz_launch_mcclendon(const MzDev& d, const int32_t* ids, int n, double* out,
-                               int32_t* status, hipStream_t s) {
+                               int32_t* status, hipStream_t s, const int* limit, int mult) {
   if (n <= 0) return hipSuccess;
   int MM = 0;
   const size_t bytes = mz_mcclendon_lds(d.P, d.toroidal != 0, &MM);
@@ -889,6 +910,7 @@ hipError_t mz_launch_mcclendon(const MzDev& d, const int32_t* ids, int n, double
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(k_mcclendon, dim3(n), dim3(T), bytes, s, d, ids, n, MM, out, status);
+  hipLaunchKernelGGL(k_mcclendon, dim3(n), dim3(T), bytes, s, d, ids, n, MM, out, status, limit,
+                     mult < 1 ? 1 : mult);
   return hipGetLastError();
 }

@@ -20,7 +20,8 @@ SOURCES = ["mz_env.hip", "mz_api.hip", "mz_difficulty.hip", "mz_qnet.hip", "mz_m
            "mz_qact.hip", "mz_mcclendon.hip"]
 EXTRA_FLAGS = {"mz_qnet.hip": ["-ffinite-math-only"]}
 BASE_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall"]
-DEPS = SOURCES + ["mz_common.h", "mz_kernels.h", "mz_build.inc.h", "mz_pygen.inc.h"]
+DEPS = SOURCES + ["mz_common.h", "mz_kernels.h", "mz_build.inc.h", "mz_pygen.inc.h",
+                  "mz_mcclendon.h", "mz_learner.h"]
 HEADER = os.path.join(os.path.dirname(ROOT), "include", "mazerl.h")
 
 

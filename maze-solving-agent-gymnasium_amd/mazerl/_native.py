@@ -38,7 +38,8 @@ EXPORTS = ["mz_last_error", "mz_device_count", "mz_create", "mz_destroy", "mz_lo
            "mz_generate", "mz_generate_ex", "mz_generate_state", "mz_reset_all", "mz_reset_list", "mz_reset_done", "mz_step", "mz_step_ex", "mz_direction_mask",
            "mz_act", "mz_step_act", "mz_expand_window", "mz_set_algorithm", "mz_query", "mz_get_grid",
            "mz_difficulty", "mz_maze_complexity", "mz_maze_metrics", "mz_difficulty_batch", "mz_get_meta", "mz_discounted_returns", "mz_q_front",
-           "mz_bank_create", "mz_bank_create_dims", "mz_bank_fill", "mz_bank_use",
+           "mz_bank_create", "mz_bank_create_dims", "mz_bank_create_ex", "mz_bank_fill", "mz_bank_use",
+           "mz_bank_slot_grid", "mz_generate_best", "mz_select_stats", "mz_set_regen_dims",
            "mz_bank_consumed", "mz_state_bytes", "mz_state_save", "mz_state_load",
            "mz_stem_forward", "mz_stem_backward", "mz_stem_workspace_floats", "mz_adamw_flat",
            "mz_pair_surrogate", "mz_leaky_relu_bf16", "mz_colsum_f32",
@@ -99,7 +100,13 @@ def load(build_if_missing=True):
     L.mz_difficulty_batch.argtypes = [vp, vp, C.c_int32, vp, vp, vp]
     L.mz_bank_create.argtypes = [vp, C.c_int32, C.c_int32, C.c_uint32]
     L.mz_bank_create_dims.argtypes = [vp, C.c_int32, vp, C.c_int32, C.c_uint32]
+    L.mz_bank_create_ex.argtypes = [vp, C.c_int32, vp, C.c_int32, C.c_uint32, C.c_int32]
     L.mz_bank_fill.argtypes = [vp, C.c_int32, C.c_uint64, vp]
+    L.mz_bank_slot_grid.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32, vp, vp]
+    L.mz_generate_best.argtypes = [vp, vp, C.c_int32, vp, C.c_int32, C.c_int32, C.c_uint64,
+                                   C.c_int32, vp]
+    L.mz_select_stats.argtypes = [vp, vp, C.c_int32, vp]
+    L.mz_set_regen_dims.argtypes = [vp, vp]
     L.mz_bank_use.argtypes = [vp, C.c_int32]
     L.mz_bank_consumed.argtypes = [vp, C.c_int32, vp, vp]
     L.mz_state_bytes.argtypes = [vp, C.POINTER(C.c_uint64)]
@@ -127,7 +134,6 @@ def load(build_if_missing=True):
     L.mz_stem_backward.argtypes = [vp, vp, vp, C.c_int32, C.c_int32, C.c_float, vp, vp, vp, vp]
     L.mz_stem_workspace_floats.argtypes = [C.c_int32]
     L.mz_qact_workspace_floats.argtypes = [C.c_int32]
-    L.mz_qact_workspace_floats.restype = C.c_int64
     L.mz_leaky_relu_bf16.argtypes = [vp, C.c_int64, C.c_float, vp]
     L.mz_colsum_f32.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, vp, vp]
     L.mz_replay_gather.argtypes = [vp, C.c_int32, C.c_int64] + [vp] * 11
@@ -151,6 +157,7 @@ def load(build_if_missing=True):
     for f in EXPORTS:
         if f != "mz_last_error":
             getattr(L, f).restype = C.c_int
+    L.mz_qact_workspace_floats.restype = C.c_int64
     _lib = L
     return L
 

@@ -13,7 +13,10 @@ Per vector step, with no host round trip (csrc/mz_ppo.hip):
   finish   mz_ppo_finish: per finished episode calculate_returns / calculate_advantages
            (:171-186; returns in float64, normalised with the unbiased std) and its rows appended
            to the update pool (fixed-capacity SoA columns in HBM);
-  reset    winners get new mazes (update_maze), truncated instances restart theirs.
+  reset    winners get new mazes (update_maze), truncated instances restart theirs; with a
+           curriculum / growth schedule (schedule.py) the winners' next algorithm
+           (change_algorithm, ppo_trainer.py:137-141) and size (+4 growth, the max-shape stop,
+           :96-105) first.
 The pool's appended-rows total is copied to the host one step late (it only grows), so the
 "pool holds `pool_size` rows" test costs no synchronisation; when it passes, the update runs:
 optimize_model over the first pool_size rows (ppo_steps passes of unshuffled minibatches: clipped
@@ -29,6 +32,7 @@ import torch.nn.functional as F
 
 from .. import _native as N
 from ..agents.ppo import ActorCriticNet, PPOMinibatchGraph, make_optimizer, optimize_model
+from .schedule import WinSchedule, curriculum_rule
 
 
 def episode_bound(max_dim, toroidal):
@@ -73,17 +77,30 @@ def pool_update(net, opt, cols, coef, batch_size, ppo_steps, allreduce=None, gra
 class VectorPPOTrainer:
     def __init__(self, env, device, actor_lr=3e-4, critic_lr=1e-4, gamma=0.9, batch_size=2048,
                  ppo_steps=4, pool_size=65536, hidden_dim=1024, h_channels=32, seed=0,
-                 allreduce=None, use_graph=True, bank=True, pool_capacity=None):
+                 allreduce=None, use_graph=True, bank=True, pool_capacity=None, curriculum=False,
+                 growth=None, algorithm="r-prim", bank_candidates=1):
+        """curriculum (False | True / "global" | "per-instance"), growth ((start, max_dim): the
+        variable-size envs' +4 per win and the max-shape stop), algorithm (the initial mazes'),
+        bank_candidates (best-of-C replacement mazes): schedule.py, VectorOffPolicyTrainer."""
         self.env = env
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise RuntimeError("VectorPPOTrainer runs on the GPU (libmazerl HIP kernels)")
         if env.window_bits is None or env.reward64 is None:
             raise ValueError("VectorPPOTrainer needs an env with window_bits=True, reward64=True")
+        rule = curriculum_rule(curriculum)
+        self.curriculum = rule
+        self.schedule = (WinSchedule(env, rule, growth, None, algorithm)
+                         if (rule is not None or growth is not None) else None)
+        self.stopped_at = None
         if bank:
             # winners' new mazes (update_maze) copied from a bank built ahead of time on a side
             # stream, one per grid size of the variable-size env, instead of built inline
-            env.enable_bank(dims=getattr(env, "dims_in_use", None))
+            dims = getattr(env, "dims_in_use", None)
+            if self.schedule is not None and self.schedule.growth is not None:
+                dims = self.schedule.sizes()
+            env.enable_bank(algorithms=[0, 1, 2] if rule else None, dims=dims,
+                            candidates=bank_candidates)
         torch.manual_seed(seed)
         self.net = ActorCriticNet(3, 6, 4, h_channels, hidden_dim).to(self.device)
         # the update reads the pool's packed windows through the HIP stem and replays a captured
@@ -218,17 +235,23 @@ class VectorPPOTrainer:
     def _update(self, frac):
         P = self.pool_size
         k = torch.div(self.pool_fill, P, rounding_mode="floor")
+        # [update count, -record overflows, -pool over capacity]: one MIN all-reduce gives the
+        # ranks' common update count and the MAX of both error flags, so every rank raises
+        # together (a rank raising alone would leave the others blocked in pool_update's
+        # collectives)
+        chk = torch.cat([k, -self.stats[3:4], -(self.pool_fill > self.cap).to(torch.int64)])
         if self.allreduce is not None:
             import torch.distributed as dist
-            dist.all_reduce(k, op=dist.ReduceOp.MIN)
+            dist.all_reduce(chk, op=dist.ReduceOp.MIN)
         # one synchronisation per update: the fill, the update count over the ranks, overflows
-        fill, k, over = (int(x) for x in torch.cat([self.pool_fill, k, self.stats[3:4]]).cpu())
+        fill, k, over, overcap = (int(x) for x in torch.cat([self.pool_fill, chk]).cpu())
+        over, overcap = -over, -overcap
         if over:
             raise RuntimeError(f"PPO episode records overflowed: {over} episodes reached "
-                               f"L = {self.L} steps (mz_ppo_scan stats[3])")
-        if fill > self.cap:
-            raise RuntimeError(f"PPO pool overflow: {fill} rows > capacity {self.cap} "
-                               "(raise pool_capacity)")
+                               f"L = {self.L} steps (mz_ppo_scan stats[3], max over the ranks)")
+        if overcap:
+            raise RuntimeError(f"PPO pool overflow: more rows than the capacity {self.cap} on a "
+                               f"rank (this rank: {fill}; raise pool_capacity)")
         coef = 1e-2 - (1e-2 - 5e-4) * frac  # ppo_trainer.py:73
         for j in range(k):
             self.rows_trained += pool_update(self.net, self.opt, self._cols(j * P, (j + 1) * P),
@@ -247,14 +270,29 @@ class VectorPPOTrainer:
         self._act()
         env.step(self.act_out)
         self._scan_finish()
+        sch = self.schedule
+        if sch is not None:  # change_algorithm for the winners (ppo_trainer.py:95)
+            won = env.terminated.bool()
+            sch.before_reset(won)
         env.reset_done(regen_won=True)
+        if sch is not None:  # update_maze's sizes, the max-shape stop (:96-105)
+            sch.after_reset(won)
         if self._due():
             self._update(frac)
 
+    @property
+    def algo(self):
+        return None if self.schedule is None else self.schedule.maze_algo
+
     def train(self, vector_steps, log_every=0, log=print):
         t0 = time.perf_counter()
+        sch = self.schedule
         for k in range(vector_steps):
             self.vector_step(frac=k / max(1, vector_steps))
+            # the max-shape stop (ppo_trainer.py:104-105) once every instance reached it
+            if sch is not None and sch.growth is not None and (k + 1) % 32 == 0 and sch.all_retired():
+                self.stopped_at = k + 1
+                break
             if log_every and (k + 1) % log_every == 0 and log:
                 log(dict(step=k + 1, episodes=self.episodes, wins=self.wins, updates=self.updates,
                          seconds=round(time.perf_counter() - t0, 2)))
@@ -278,7 +316,8 @@ class VectorPPOTrainer:
             ost = {k: getattr(o, k).clone() for k in ("exp_avg", "exp_avg_sq", "step_t", "lr_dev")}
         else:
             ost = {"torch": o.state_dict()}
-        return {"format": "mazerl.VectorPPOTrainer/1", "L": self.L, "cap": self.cap,
+        return {"format": "mazerl.VectorPPOTrainer/2", "L": self.L, "cap": self.cap,
+                "schedule": None if self.schedule is None else self.schedule.state_dict(),
                 "net": {k: v.clone() for k, v in self.net.state_dict().items()}, "opt": ost,
                 "t": t, "records": {k: getattr(self, k)[live] for k in self._REC},
                 "pool_fill": fill, "pool": {k: getattr(self, k)[:fill].clone() for k in self._POOL},
@@ -290,9 +329,16 @@ class VectorPPOTrainer:
                 "env": self.env.state_dict()}
 
     def load_state_dict(self, sd):
-        if sd.get("format") != "mazerl.VectorPPOTrainer/1" or sd["L"] != self.L or sd["cap"] != self.cap:
+        if sd.get("format") == "mazerl.VectorPPOTrainer/1":
+            raise ValueError("a format-1 VectorPPOTrainer checkpoint (3 stats counters, a different "
+                             "record length rule): not loadable by this version")
+        if sd.get("format") != "mazerl.VectorPPOTrainer/2" or sd["L"] != self.L or sd["cap"] != self.cap:
             raise ValueError("not a VectorPPOTrainer state_dict of this shape")
+        if (sd["schedule"] is None) != (self.schedule is None):
+            raise ValueError("curriculum / growth differ from the saved trainer's")
         self.env.load_state_dict(sd["env"])
+        if self.schedule is not None:
+            self.schedule.load_state_dict(sd["schedule"])
         with torch.no_grad():
             self.net.load_state_dict(sd["net"])
         o, so = self.opt, sd["opt"]

@@ -11,7 +11,9 @@ VectorOffPolicyTrainer.train() is NeuralOffPolicyTrainer.train (lib/trainers/off
   bookkeeping: steps_done += 1, = 0 on a win (off_policy_trainer.py:192); wins/episodes counters
   auto-reset: winners get a new maze (update_maze, :202), truncated instances restart the same
              maze (reset, :153) — one flag-scan kernel; new mazes are copied from a bank of
-             pre-generated mazes (refilled in bulk on a side stream)
+             pre-generated mazes (refilled in bulk on a side stream; bank_candidates=6: each the
+             easiest of 6 by McClendon difficulty, the reference env's generate_maze selection,
+             base_maze_env.py:78-97); change_algorithm / growth / the max-shape stop: schedule.py
   K learner updates (replay ratio), target sync / cosine step per update count.
 evaluate() is NeuralOffPolicyTrainer.test(new=True)/infer (:228-299): fresh mazes, one episode
 each, win = terminated; greedy (eps = 0) or the reference's epsilon protocol (Q14).
@@ -22,48 +24,50 @@ import time
 import torch
 
 from ..vector_env import ALGOS, VectorMazeEnv
+from .schedule import WinSchedule, curriculum_rule
 
 
 class VectorOffPolicyTrainer:
+    """curriculum: False | True / "global" | "per-instance" (change_algorithm, schedule.py);
+    growth: None | (start, max_dim) — the variable-size envs' +4 growth per win and the max-shape
+    stop (schedule.py; make the env with make_env(B, start, max_dim=max_dim)); algorithm: the
+    initial mazes' algorithm (str or per-instance ids), the curriculum's base;
+    bank_candidates: best-of-C maze bank (1 = one Philox maze per slot)."""
+
     def __init__(self, env, learner, seed=0, regen_won=True, curriculum=False, allreduce_stats=None,
-                 bank=True, fused=True):
+                 bank=True, fused=True, growth=None, algorithm="r-prim", bank_candidates=1):
         self.env, self.learner = env, learner
+        rule = curriculum_rule(curriculum)
+        self.schedule = (WinSchedule(env, rule, growth, learner, algorithm)
+                         if (rule is not None or growth is not None) else None)
         if regen_won and bank:
             # winners' new mazes come from a bank refilled on a side stream (VectorMazeEnv.
             # enable_bank): a maze build is a ~1 ms serial chain that would stall the step
-            env.enable_bank(algorithms=[0, 1, 2] if curriculum else None,
-                            dims=getattr(env, "dims_in_use", None))
+            dims = getattr(env, "dims_in_use", None)
+            if self.schedule is not None and self.schedule.growth is not None:
+                dims = self.schedule.sizes()
+            env.enable_bank(algorithms=[0, 1, 2] if rule else None, dims=dims,
+                            candidates=bank_candidates)
         self.seed = seed
         # fused: the per-step bookkeeping and the replay push as HIP launches (mz_trainer_tick,
         # mz_replay_push) instead of ~25 torch ops; False keeps the torch path (A/B, tests)
         self.fused = bool(fused)
         self.regen_won = regen_won
-        self.curriculum = curriculum
+        self.curriculum = rule
         self.allreduce_stats = allreduce_stats
         dev = env.device
         self.wins = torch.zeros((), dtype=torch.int64, device=dev)
         self.episodes = torch.zeros((), dtype=torch.int64, device=dev)
         self.inst_wins = torch.zeros(env.num_envs, dtype=torch.int32, device=dev)
         self.counter = 0
+        self.stopped_at = None  # vector step of the max-shape stop (growth), if it came
         self._eps = None  # the next step's epsilon, computed at the end of the previous step
         self.history = []
 
-    def _change_algorithm(self, term):
-        """NeuralOffPolicyTrainer.change_algorithm (off_policy_trainer.py:302-310, called on every
-        win, :201) per instance: at the 5th win epsilon_decay *= 3 and the maze algorithm becomes
-        prim&kill, at the 10th epsilon_decay *= 4 and dfs (steps_done = 0 on every win is the
-        common bookkeeping); the winner's new maze (update_maze, :202) is then drawn with the new
-        algorithm by the reset that follows. The learner's eps_decay becomes a per-instance
-        tensor."""
-        L, dev = self.learner, self.env.device
-        self.inst_wins += term.to(torch.int32)
-        if not torch.is_tensor(L.eps_decay):
-            L.eps_decay = torch.full((self.env.num_envs,), float(L.eps_decay), device=dev)
-        w = self.inst_wins
-        L.eps_decay.mul_(torch.where(term & (w == 5), 3.0, torch.where(term & (w == 10), 4.0, 1.0)))
-        self.algo = torch.where(w >= 10, ALGOS["dfs"],
-                                torch.where(w >= 5, ALGOS["prim&kill"], ALGOS["r-prim"])).to(torch.uint8)
-        self.env.set_algorithm(self.algo)
+    @property
+    def algo(self):
+        """Algorithm id of each instance's current maze (None without a schedule)."""
+        return None if self.schedule is None else self.schedule.maze_algo
 
     def _expand(self, bits):
         return self.env.expand_window(bits)
@@ -85,6 +89,7 @@ class VectorOffPolicyTrainer:
             s6, sw = env.obs6.clone(), env.window_bits.clone()
         env.step_act(eps=eps, greedy=greedy, seed=self.seed, counter=self.counter)
         self.counter += 1
+        # (a curriculum changes epsilon_decay on the device: the torch bookkeeping path)
         tick = getattr(L, "tick", None) if self.fused and not self.curriculum else None
         # steps_done (+1, 0 on a win), wins / episodes, the next step's epsilon and its greedy-row
         # list — issued now, so that its count reaches the host while the stream runs the push
@@ -100,13 +105,18 @@ class VectorOffPolicyTrainer:
                 L.prepare_greedy(self._eps, self.seed, self.counter)
             self.wins += term.sum()
             self.episodes += (term | env.truncated.bool()).sum()
-            if self.curriculum:  # change_algorithm (off_policy_trainer.py:302-310), per instance
-                self._change_algorithm(term)
+        sch = self.schedule
+        if sch is not None:  # change_algorithm for this step's winners (off_policy_trainer.py:201)
+            won = env.terminated.bool()
+            self.inst_wins += won.to(torch.int32)
+            sch.before_reset(won)
         if ring:
             rp.push_rest(env.actions, env.reward, env.obs6, env.window_bits)
         else:
             rp.push(s6, sw, env.actions, env.reward, env.obs6, env.window_bits)
         env.reset_done(regen_won=self.regen_won)
+        if sch is not None:  # update_maze's sizes, the max-shape stop (:202-212)
+            sch.after_reset(won)
         # with an overlapped learner the updates run on its side stream; the next push (one row
         # per instance) is kept out of their sample range
         return L.update(self._expand, reserve=env.num_envs)
@@ -134,19 +144,27 @@ class VectorOffPolicyTrainer:
         after a load_state_dict continue exactly as further train() calls on the saved trainer
         would have."""
         L = self.learner
-        return {"format": "mazerl.VectorOffPolicyTrainer/1", "seed": self.seed,
+        return {"format": "mazerl.VectorOffPolicyTrainer/2", "seed": self.seed,
                 "counter": self.counter, "wins": self.wins.clone(), "episodes": self.episodes.clone(),
                 "inst_wins": self.inst_wins.clone(), "curriculum": self.curriculum,
                 "regen_won": self.regen_won, "history": list(self.history),
+                "schedule": None if self.schedule is None else self.schedule.state_dict(),
                 "learner": L.state_dict(), "env": self.env.state_dict()}
 
     def load_state_dict(self, sd):
-        if sd.get("format") != "mazerl.VectorOffPolicyTrainer/1":
+        fmt = sd.get("format")
+        if fmt == "mazerl.VectorOffPolicyTrainer/1":
+            raise ValueError("a format-1 VectorOffPolicyTrainer checkpoint (before the win "
+                             "schedule, round 5): not loadable by this version")
+        if fmt != "mazerl.VectorOffPolicyTrainer/2":
             raise ValueError("not a VectorOffPolicyTrainer state_dict")
-        if bool(sd["curriculum"]) != bool(self.curriculum) or bool(sd["regen_won"]) != bool(self.regen_won):
-            raise ValueError("curriculum / regen_won differ from the saved trainer's")
+        if sd["curriculum"] != self.curriculum or bool(sd["regen_won"]) != bool(self.regen_won) \
+                or (sd["schedule"] is None) != (self.schedule is None):
+            raise ValueError("curriculum / growth / regen_won differ from the saved trainer's")
         self.env.load_state_dict(sd["env"])
         self.learner.load_state_dict(sd["learner"])
+        if self.schedule is not None:
+            self.schedule.load_state_dict(sd["schedule"])
         self.seed, self.counter = int(sd["seed"]), int(sd["counter"])
         self.wins.copy_(sd["wins"])
         self.episodes.copy_(sd["episodes"])
@@ -161,8 +179,13 @@ class VectorOffPolicyTrainer:
         rows = getattr(self.learner, "_rows", None)
         if rows is not None:
             rows._issued = None
+        sch = self.schedule
         for k in range(vector_steps):
             loss = self.vector_step()
+            # the max-shape stop (off_policy_trainer.py:210-212) once every instance reached it
+            if sch is not None and sch.growth is not None and (k + 1) % 32 == 0 and sch.all_retired():
+                self.stopped_at = k + 1
+                break
             if log_every and (k + 1) % log_every == 0:
                 torch.cuda.synchronize()
                 rec = dict(step=k + 1, wins=int(self.wins), episodes=int(self.episodes),
@@ -179,12 +202,15 @@ class VectorOffPolicyTrainer:
 
 
 def make_env(num_envs, dims, toroidal=False, algorithm="r-prim", seed=0x5EED0000, device=None,
-             **kw):
-    """VectorMazeEnv whose instance i gets maze size dims[i % len(dims)] (variable-size configs)."""
+             max_dim=None, candidates=1, **kw):
+    """VectorMazeEnv whose instance i gets maze size dims[i % len(dims)] (variable-size configs);
+    max_dim: the handle's pitch (default max(dims); a growth schedule needs its max size);
+    candidates > 1: every initial maze the easiest of `candidates` (the reference env's
+    generate_maze selection, base_maze_env.py:78-97 — its constructors draw the first maze so)."""
     dims = [dims] if isinstance(dims, int) else list(dims)
     env = VectorMazeEnv(num_envs, dims[0], toroidal=toroidal, enrich=True, device=device,
-                        max_dim=max(dims), algorithm=algorithm, seed=seed, generate=len(dims) == 1,
-                        **kw)
+                        max_dim=max(max(dims), int(max_dim or 0)), algorithm=algorithm, seed=seed,
+                        generate=len(dims) == 1, candidates=candidates, **kw)
     env.dims_in_use = sorted(set(dims))  # (a maze bank for the winners then holds every size)
     if len(dims) > 1:
         ids = torch.arange(num_envs, device=env.device)
@@ -192,7 +218,8 @@ def make_env(num_envs, dims, toroidal=False, algorithm="r-prim", seed=0x5EED0000
             sel = ids[ids % len(dims) == j]
             if sel.numel():
                 algo = algorithm if isinstance(algorithm, str) else torch.as_tensor(algorithm)[sel.cpu()]
-                env.generate(env_ids=sel.to(torch.int32), algorithm=algo, dim=n, seed=seed)
+                env.generate(env_ids=sel.to(torch.int32), algorithm=algo, dim=n, seed=seed,
+                             candidates=candidates)
         env.set_algorithm(algorithm if isinstance(algorithm, str) else torch.as_tensor(algorithm).to(torch.uint8))
         env.reset()
     return env
@@ -276,7 +303,7 @@ def steps_done_epsilon(learner, num_mazes):
     idx = torch.arange(num_mazes, device=sd0.device) % B
     sd0 = sd0[idx]
     dec = learner.eps_decay
-    dec = dec[idx] if torch.is_tensor(dec) else torch.full_like(sd0, float(dec))
+    dec = dec[idx] if torch.is_tensor(dec) and dec.dim() > 0 else torch.full_like(sd0, float(dec))
     e0, e1 = float(learner.eps_start), float(learner.eps_final)
 
     def eps(k):
@@ -295,6 +322,9 @@ def evaluate(learner, num_mazes, dim, algorithm="r-prim", seed=0x7E57, eps=0.0, 
     Returns (rate, vector steps) or, with return_won, (rate, vector steps, won bool [n] on the
     host)."""
     bits = getattr(learner, "supports_bits", False)
+    if not isinstance(algorithm, str) and mazes is None:
+        raise ValueError("a per-maze algorithm list needs the mazes: pass best_of_mazes(...)'s "
+                         "output as mazes= (evaluate generates one algorithm's mazes itself)")
     algo0 = algorithm if isinstance(algorithm, str) else "r-prim"
     env = make_env(num_mazes, dim, toroidal=toroidal, algorithm=algo0, seed=seed,
                    device=device, done_list=False, pos=False, window=not bits, window_bits=True)

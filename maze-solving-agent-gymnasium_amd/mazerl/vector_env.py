@@ -33,7 +33,7 @@ class VectorMazeEnv:
     def __init__(self, num_envs, maze_dim, toroidal=False, enrich=True, device=None,
                  max_dim=None, algorithm="r-prim", seed=0x5EED0000, generate=True,
                  window=True, window_bits=True, reward64=False, pos=True, done_list=True,
-                 host_scalars=False):
+                 host_scalars=False, candidates=1):
         if not torch.cuda.is_available():
             raise RuntimeError("VectorMazeEnv needs a HIP GPU (libmazerl.so has no CPU path)")
         self.lib = N.load()
@@ -83,8 +83,9 @@ class VectorMazeEnv:
         self._bank = None
         self.algos_in_use = set()  # algorithm ids regeneration may ask for (sizes the bank)
         self._count_zero = True  # done_count is 0 (fresh, or consumed by reset_done)
+        self._regen_dims = None
         if generate:
-            self.generate(algorithm=algorithm)
+            self.generate(algorithm=algorithm, candidates=candidates)
             self.reset()
 
     # ---------------------------------------------------------------------------------------
@@ -140,12 +141,17 @@ class VectorMazeEnv:
             pass
 
     # ---------------------------------------------------------------------------------------
-    def generate(self, env_ids=None, algorithm="r-prim", dim=None, seed=None, rng="philox"):
+    def generate(self, env_ids=None, algorithm="r-prim", dim=None, seed=None, rng="philox",
+                 candidates=1):
         """New mazes for env_ids (None = all): gen_maze(shape, algorithm) per instance.
         rng="philox": Philox stream seed + env_id (every random choice uniform over the same
         candidates as the reference); rng="cpython": bit-exact — instance i gets the maze of
         `random.seed(seed + i); gen_maze((dim, dim), algorithm)` (MT19937 + CPython set order
-        emulated on the GPU)."""
+        emulated on the GPU).
+        candidates > 1 (Philox): the reference env's selection (BaseMazeEnv.generate_maze,
+        base_maze_env.py:78-97; toroidal_maze_env.py:40-54) — the easiest of `candidates` mazes
+        by McClendon difficulty, all on the GPU (mz_generate_best: candidate c of instance e is
+        the maze of Philox seed + e * candidates + c, as best_of_mazes draws them)."""
         dim = int(dim or self.maze_dim)
         seed = self.seed if seed is None else int(seed)
         ids = None if env_ids is None else torch.as_tensor(env_ids, dtype=torch.int32, device=self.device)
@@ -163,9 +169,40 @@ class VectorMazeEnv:
                 raise ValueError("per-instance algorithm ids must match the env list")
             self.algos_in_use.update(ALGOS.values())
         mode = {"philox": N.MZ_RNG_PHILOX, "cpython": N.MZ_RNG_CPYTHON}[rng]
+        if int(candidates) > 1:
+            if mode != N.MZ_RNG_PHILOX:
+                raise ValueError("best-of-C generation draws Philox candidates (rng='philox')")
+            N.check(self.lib.mz_generate_best(self._h, _ptr(ids), n, _ptr(algo_t), algo_all, dim,
+                                              seed & 0xFFFFFFFFFFFFFFFF, int(candidates),
+                                              self._stream()))
+            return self
         N.check(self.lib.mz_generate_ex(self._h, _ptr(ids), n, _ptr(algo_t), algo_all, dim,
                                         seed & 0xFFFFFFFFFFFFFFFF, mode, self._stream()))
         return self
+
+    def select_stats(self, reset=False):
+        """Best-of-C selection counters of this handle (bank refills + generate(candidates > 1)):
+        {"unresolved": groups with a candidate the GPU difficulty kernel could not score (picked
+        among the others), "near_ties": groups whose choice a 1-ulp log tie could change,
+        "groups": selections made}."""
+        out = torch.zeros(3, dtype=torch.int32, device=self.device)
+        N.check(self.lib.mz_select_stats(self._h, out.data_ptr(), int(bool(reset)), self._stream()))
+        u, t, g = (int(x) for x in out.cpu())
+        return {"unresolved": u, "near_ties": t, "groups": g}
+
+    def set_regen_dims(self, dims):
+        """Per-instance size of a winner's next maze (uint8 device tensor [B], kept referenced
+        here; 0 = the winner keeps its maze — update_maze past max_shape), or None: each
+        instance's current size. Read by every later reset_done / reset_list(regen_won)."""
+        if dims is None:
+            self._regen_dims = None
+            N.check(self.lib.mz_set_regen_dims(self._h, None))
+            return
+        t = torch.as_tensor(dims, device=self.device).to(torch.uint8).contiguous()
+        if t.numel() != self.num_envs:
+            raise ValueError("one size per instance")
+        self._regen_dims = t
+        N.check(self.lib.mz_set_regen_dims(self._h, t.data_ptr()))
 
     def generate_from_random(self, env_id=0, algorithm="r-prim", dim=None, rnd=None):
         """One maze for instance env_id drawn from a Python random.Random (default: the global
@@ -248,14 +285,19 @@ class VectorMazeEnv:
 
     # ---------------------------------------------------------------------------------------
     # Maze bank: winners' new mazes are generated ahead of time, in bulk, on a side stream.
-    def enable_bank(self, slots=None, swap_every=8, algorithms=None, seed=None, dims=None):
+    def enable_bank(self, slots=None, swap_every=8, algorithms=None, seed=None, dims=None,
+                    candidates=1):
         """Two banks of `slots` mazes per algorithm (size maze_dim, or per size of `dims` — the
         variable-size envs): reset_done(regen_won=True) consumes the active one; every
         `swap_every` such calls the banks swap and the retired one is refilled on a side stream
         (ordered after the launches that consumed it; the main stream waits for a refill only
         when that bank comes back). Default slots: B / 8 (split over the sizes, >= 16 each).
         Default seed: derived from the env's seed, which carries the shard's first global
-        instance id, so the ranks of a data-parallel run draw different replacement mazes."""
+        instance id, so the ranks of a data-parallel run draw different replacement mazes.
+        candidates > 1: every refilled slot is the easiest of `candidates` mazes by McClendon
+        difficulty (the reference's generate_maze selection for a win's new maze,
+        base_maze_env.py:78-97 via update_maze, off_policy_trainer.py:202), chosen on the GPU
+        inside the refill (mz_bank_create_ex)."""
         if self._bank is not None:
             return
         if seed is None:
@@ -268,13 +310,11 @@ class VectorMazeEnv:
         else:
             ids = [ALGOS[a] if isinstance(a, str) else int(a) for a in algorithms]
             mask = sum(1 << i for i in set(ids))
-        if len(dims) == 1:
-            N.check(self.lib.mz_bank_create(self._h, K, dims[0], mask))
-        else:
-            arr = (N.C.c_int32 * len(dims))(*dims)
-            N.check(self.lib.mz_bank_create_dims(self._h, K, arr, len(dims), mask))
+        arr = (N.C.c_int32 * len(dims))(*dims)
+        N.check(self.lib.mz_bank_create_ex(self._h, K, arr, len(dims), mask, int(candidates)))
         self._bank = dict(K=K, dims=dims, swap=int(swap_every), calls=0, cur=0, seed=int(seed),
-                          side=torch.cuda.Stream(self.device), ready=[None, None])
+                          side=torch.cuda.Stream(self.device), ready=[None, None],
+                          candidates=int(candidates))
         st = self._stream()
         for b in (0, 1):
             N.check(self.lib.mz_bank_fill(self._h, b, self._bank["seed"], st))
@@ -299,6 +339,18 @@ class VectorMazeEnv:
         ev = torch.cuda.Event()
         ev.record(side)
         bk["ready"][old] = ev
+
+    def bank_slot(self, bank, algorithm, dim, slot):
+        """One bank slot's maze (synchronous; tests): (grid uint8 [N, N], (sr, sc, gr, gc))."""
+        import numpy as np
+        a = ALGOS[algorithm] if isinstance(algorithm, str) else int(algorithm)
+        di = self._bank["dims"].index(int(dim))
+        g = np.zeros((self.max_dim, self.max_dim), np.uint8)
+        info = np.zeros(4, np.int32)
+        N.check(self.lib.mz_bank_slot_grid(self._h, int(bank), a, di, int(slot), g.ctypes.data,
+                                           info.ctypes.data))
+        n = int(dim)
+        return g.reshape(-1)[:n * n].reshape(n, n).copy(), tuple(int(x) for x in info)
 
     def bank_consumed(self, bank=None):
         """int32 [3] (a single-size bank) or [3, n_sizes]: slots of `bank` (default: the active
@@ -331,12 +383,14 @@ class VectorMazeEnv:
         out = {k: getattr(self, k).clone() for k in self._OUTPUTS if getattr(self, k) is not None}
         bank = None
         if self._bank is not None:
-            bank = {k: self._bank[k] for k in ("K", "dims", "swap", "calls", "cur", "seed")}
+            bank = {k: self._bank[k] for k in ("K", "dims", "swap", "calls", "cur", "seed",
+                                               "candidates")}
         return {"format": "mazerl.VectorMazeEnv/1", "num_envs": self.num_envs,
                 "maze_dim": self.maze_dim, "max_dim": self.max_dim, "toroidal": self.toroidal,
                 "enrich": self.enrich, "seed": self.seed, "epoch": self.epoch,
                 "count_zero": self._count_zero, "algos_in_use": sorted(self.algos_in_use),
-                "device_state": blob, "outputs": out, "bank": bank}
+                "device_state": blob, "outputs": out, "bank": bank,
+                "regen_dims": None if self._regen_dims is None else self._regen_dims.clone()}
 
     def load_state_dict(self, sd):
         """Restore a state_dict() into this env (same num_envs / max_dim / toroidal / enrich and,
@@ -345,7 +399,8 @@ class VectorMazeEnv:
             raise ValueError("not a VectorMazeEnv state_dict")
         bank = sd.get("bank")
         if (bank is None) != (self._bank is None) or (bank is not None and (
-                bank["K"] != self._bank["K"] or list(bank["dims"]) != list(self._bank["dims"]))):
+                bank["K"] != self._bank["K"] or list(bank["dims"]) != list(self._bank["dims"])
+                or int(bank.get("candidates", 1)) != self._bank["candidates"])):
             raise ValueError("maze bank mismatch: call enable_bank() with the saved geometry "
                              "(or not at all) before load_state_dict()")
         blob = sd["device_state"].to(device=self.device, dtype=torch.uint8).contiguous()
@@ -363,6 +418,7 @@ class VectorMazeEnv:
         self.seed, self.epoch = int(sd["seed"]), int(sd["epoch"])
         self._count_zero = bool(sd["count_zero"])
         self.algos_in_use = set(sd.get("algos_in_use", ()))
+        self.set_regen_dims(sd.get("regen_dims"))
         if bank is not None:
             self._bank.update(swap=int(bank["swap"]), calls=int(bank["calls"]),
                               cur=int(bank["cur"]), seed=int(bank["seed"]), ready=[None, None])

@@ -192,7 +192,7 @@ def test_best_of_mazes_mixed_algorithms_toroidal_variable_sizes():
 
 
 def test_curriculum_change_algorithm_per_instance():
-    """VectorOffPolicyTrainer(curriculum=True): NeuralOffPolicyTrainer.change_algorithm
+    """VectorOffPolicyTrainer(curriculum="per-instance"): NeuralOffPolicyTrainer.change_algorithm
     (off_policy_trainer.py:302-310, on every win) per instance — epsilon_decay * 3 at the 5th win
     and * 4 at the 10th, the algorithm prim&kill from the 5th win and dfs from the 10th; steps_done
     = 0 on every win. Wins are recounted here from each step's terminated flags."""
@@ -203,7 +203,7 @@ def test_curriculum_change_algorithm_per_instance():
     env = _env(B, dim=15)
     L = VectorDQNLearner(B, "cuda:0", variant="dqn", batch_size=128, capacity=1 << 15,
                          eps_decay=base, eps_start=1.0, eps_final=1.0)  # random walks: many wins
-    tr = VectorOffPolicyTrainer(env, L, seed=5, curriculum=True)
+    tr = VectorOffPolicyTrainer(env, L, seed=5, curriculum="per-instance")
     wins = torch.zeros(B, dtype=torch.int32, device="cuda:0")
     last = {}
     step_act = env.step_act
@@ -220,6 +220,7 @@ def test_curriculum_change_algorithm_per_instance():
         assert torch.equal(L.steps_done[term], torch.zeros_like(L.steps_done[term]))
     torch.cuda.synchronize()
     assert torch.equal(tr.inst_wins, wins) and int(wins.sum()) > 0
+    assert torch.equal(tr.schedule.inst_wins, wins)
 
     def expect(w):
         mult = torch.where(w >= 10, 12.0, torch.where(w >= 5, 3.0, 1.0))
@@ -229,13 +230,18 @@ def test_curriculum_change_algorithm_per_instance():
     d, a = expect(wins)
     assert torch.equal(L.eps_decay, d) and torch.equal(tr.algo.long(), a)
     # the thresholds themselves, on scripted wins: instance i wins in round k iff k < i % 13
-    tr.inst_wins.zero_()
+    sch = tr.schedule
+    sch.inst_wins.zero_()
+    sch.algo.fill_(ALGOS["r-prim"])
+    sch.maze_algo.fill_(ALGOS["r-prim"])
     L.eps_decay = base
     idx = torch.arange(B, device="cuda:0")
     for k in range(12):
-        tr._change_algorithm(k < idx % 13)
+        won = k < idx % 13
+        sch.before_reset(won)
+        sch.after_reset(won)
     w = (idx % 13).clamp(max=12).to(torch.int32)
     d, a = expect(w)
-    assert torch.equal(tr.inst_wins, w) and torch.equal(L.eps_decay, d)
+    assert torch.equal(sch.inst_wins, w) and torch.equal(L.eps_decay, d)
     assert torch.equal(tr.algo.long(), a)
     env.close()
