@@ -94,6 +94,10 @@ def parse(argv=None):
     ap.add_argument("--curriculum-steps", type=int, default=2400,
                     help="DDQN vector steps of the curriculum leg (the reference's change_algorithm "
                          "training, evaluated under its test(new=True) protocol; 0 = skip)")
+    ap.add_argument("--curriculum-rules", default="global,per-instance",
+                    help="change_algorithm over the learner's wins (global: the reference's one "
+                         "agent and class-wide ALGORITHM) and / or per instance (mazerl/trainers/"
+                         "schedule.py); one curriculum leg each, the first is curriculum_leg")
     # learner: one update of 1,024 per vector step. Sweep at 2,400 vector steps (training env
     # steps/s, greedy win-rate): 256: 58.0 M, 96.0 % / 512: 54.4 M, 95.0-96.0 % / 1,024: 50.6-
     # 50.8 M, 96.2-96.4 % / 2,048: 40.4 M, 96.5 % / 4,096: 30.4 M, 96.2 % — the win-rate is on its
@@ -117,9 +121,15 @@ def parse(argv=None):
                     help="1: the timed env steps replay captured HIP graphs of k_step launches "
                          "(the Python launch loop is timed beside them); 0: eager launches")
     ap.add_argument("--graph-chunk", type=int, default=100, help="k_step launches per graph")
-    ap.add_argument("--config-legs", default="cfg4,cfg5",
-                    help="BASELINE configs 4 (DDQN, mixed 81x81) and 5 (PPO, toroidal 17..79) at "
-                         "this N, whole-node env steps/s + win-rates ('' = skip)")
+    ap.add_argument("--config-legs", default="cfg2,cfg4,cfg5",
+                    help="BASELINE configs 2 (DQN, 15x15), 4 (DDQN, mixed 81x81) and 5 (PPO, "
+                         "toroidal 9->40 cells) at this N, whole-node env steps/s + win-rates "
+                         "('' = skip)")
+    ap.add_argument("--cfg2-envs", type=int, default=4096, help="config 2 instances per GPU")
+    ap.add_argument("--cfg2-steps", type=int, default=800)
+    ap.add_argument("--cfg5-modes", default="growth,fixed",
+                    help="config 5 legs: growth = ToroidalVariableMazeEnv's +4 growth per win from "
+                         "17 (9 cells) to 79 (40 cells); fixed = instance i of size 17 + 2 (i mod 32)")
     ap.add_argument("--cfg4-envs", type=int, default=8192, help="config 4 instances per GPU")
     ap.add_argument("--cfg5-envs", type=int, default=4096, help="config 5 instances per GPU")
     ap.add_argument("--cfg4-steps", type=int, default=600)
@@ -235,7 +245,7 @@ def win_rate(a, dev, rank=0, world=1):
                     "steps_done)"}
 
 
-def curriculum_leg(a, dev, rank=0, world=1):
+def curriculum_leg(a, dev, rank=0, world=1, rule="global"):
     """The reference's own protocol for its "new mazes" number (README: 99.6 % for DDQN at 41x41):
     DDQN trained with NeuralOffPolicyTrainer.change_algorithm (off_policy_trainer.py:302-310, per
     instance here: prim&kill mazes from an instance's 5th win, dfs from its 10th, epsilon_decay
@@ -254,7 +264,7 @@ def curriculum_leg(a, dev, rank=0, world=1):
     B, dim = a.curriculum_envs, a.curriculum_dim
     env = VectorMazeEnv(B, dim, enrich=True, device=dev, algorithm="r-prim",
                         seed=0xC0CC0000 + rank * B, done_list=False, window=False,
-                        window_bits=True)
+                        window_bits=True, candidates=a.candidates)
     decay = ((dim - 1) * (dim - 1) // 2) * 5
     L = VectorDQNLearner(B, dev, variant="ddqn", lr=1e-3, eps_start=0.95, eps_final=0.1,
                          eps_decay=decay, gamma=0.7, batch_size=a.curriculum_batch,
@@ -265,46 +275,60 @@ def curriculum_leg(a, dev, rank=0, world=1):
     if world > 1:
         broadcast_params(L.source)
         L.target.load_state_dict(L.source.state_dict())
-    tr = VectorOffPolicyTrainer(env, L, seed=11 + 7919 * rank, curriculum=True)
+    tr = VectorOffPolicyTrainer(env, L, seed=11 + 7919 * rank, curriculum=rule,
+                                bank_candidates=a.candidates)
     tr.train(20)
     if world > 1:
         dist.barrier()
-    secs = tr.train(a.curriculum_steps, **progress(rank, "curriculum leg"))
+    secs = tr.train(a.curriculum_steps, **progress(rank, f"curriculum leg ({rule})"))
     if world > 1:
         t = torch.tensor([secs], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         secs = float(t.item())
-    algo_mix = (torch.bincount(tr.algo.long(), minlength=3).tolist()
-                if getattr(tr, "algo", None) is not None else None)  # ids: ALGOS (vector_env.py)
+    summary = tr.schedule.summary()  # (rank 0's shard)
     env.close()
     if rank != 0:
         return None
     log("curriculum-leg evaluation")
     out = reference_protocol(L, a.eval_mazes, dim, dev, 0x7E5D0000)
-    out.update({"training": "change_algorithm curriculum (r-prim -> prim&kill at 5 wins -> dfs at "
-                            "10 wins, per instance)",
+    out.update({"training": ("change_algorithm curriculum (r-prim -> prim&kill at the 5th win -> dfs "
+                             "at the 10th; %s rule: %s)" % (rule, (
+                                 "the learner's wins over all instances in instance order, the "
+                                 "algorithm class-wide as the reference's ALGORITHM, epsilon_decay "
+                                 "x3 / x4 for every instance"
+                                 if rule == "global" else "each instance's own wins and "
+                                 "epsilon_decay"))),
                 "grid": dim, "envs_per_gpu": B, "epsilon_decay": decay,
+                "epsilon_decay_at_end": float(L.eps_decay) if not torch.is_tensor(L.eps_decay)
+                or L.eps_decay.dim() == 0 else float(L.eps_decay.float().mean()),
                 "updates_per_vector_step": a.curriculum_updates, "batch": a.curriculum_batch,
+                "training_mazes_candidates": a.candidates,
                 "train_vector_steps": a.curriculum_steps + 20,
                 "train_env_steps_per_s": B * a.curriculum_steps * world / secs,
-                "instances_per_algorithm_at_end": (dict(zip(["r-prim", "dfs", "prim&kill"], algo_mix))
-                                                   if algo_mix else None),
+                "total_wins": summary["total_wins"],
+                "instances_per_algorithm_at_end": summary["instances_per_algorithm"],
+                "new_mazes_per_algorithm": summary["new_mazes_per_algorithm"],
                 "eval_mazes": a.eval_mazes})
     return out
 
 
 def config_legs(a, dev, rank=0, world=1):
-    """BASELINE configs 4 and 5 at the bench's N (north_star's 8-GPU configs; per rank the share of
-    the 8-GPU job: 8,192 and 4,096 instances), each trained for a fixed number of vector steps
-    between a barrier + synchronize on each side, whole-node env steps/s = all ranks' env steps /
-    the max-over-ranks time; rank 0 then evaluates:
+    """BASELINE configs 2, 4 and 5 at the bench's N (per rank the share of each config: 4,096,
+    8,192 and 4,096 instances), each trained for a fixed number of vector steps between a barrier
+    + synchronize on each side, whole-node env steps/s = all ranks' env steps / the max-over-ranks
+    time, training mazes best-of---candidates (the reference env's selection); rank 0 evaluates:
+      cfg2  DQN on 4,096 r-prim 15x15 mazes per rank (the window is the whole maze), one update of
+            2,048 per vector step; greedy win-rate on fresh r-prim mazes as generated and best-of-6;
       cfg4  DDQN on 8,192 mixed dfs / r-prim / prim&kill 81x81 mazes per rank (algo = global
             instance id mod 3), 4 updates of 512 per vector step, source-net gradients
             all-reduced over RCCL per update; win-rates under the reference's test(new=True)
             protocol (mixed algorithms, best-of-6, greedy and epsilon from steps_done);
-      cfg5  PPO on 4,096 toroidal mazes of sizes 17..79 per rank (instance i: 17 + 2 (i mod 32)),
-            gradients all-reduced per minibatch; greedy win-rate on fresh mazes as generated and on
-            best-of-6 mazes (toroidal_maze_env.py:40-54: difficulty of the bordered maze)."""
+      cfg5  PPO on 4,096 toroidal mazes per rank, gradients all-reduced per minibatch; mode
+            "growth": every instance starts at 17 x 17 (9 cells) and grows +4 per win up to 79
+            (40 cells) as ToroidalVariableMazeEnv.update_maze (toroidal_variable_maze_env.py:113-131,
+            with the max-shape stop); mode "fixed": instance i of size 17 + 2 (i mod 32); greedy
+            win-rate on fresh mazes of sizes 17..79 as generated and best-of-6
+            (toroidal_maze_env.py:40-54: difficulty of the bordered maze)."""
     import torch
     import torch.distributed as dist
     from mazerl import VectorMazeEnv
@@ -328,13 +352,49 @@ def config_legs(a, dev, rank=0, world=1):
 
     out = {}
     legs = [x for x in a.config_legs.split(",") if x]
+    C = a.candidates
+    if "cfg2" in legs:
+        if rank == 0:
+            log("config 2 leg (DQN, 15x15)")
+        B, dim = a.cfg2_envs, 15
+        env = VectorMazeEnv(B, dim, enrich=True, device=dev, algorithm="r-prim",
+                            seed=0x5EED0000 + rank * B, done_list=False, window=False,
+                            window_bits=True, candidates=C)
+        decay = ((dim - 1) * (dim - 1) // 2) * 5 / 40.0
+        L = VectorDQNLearner(B, dev, variant="dqn", lr=1e-3, eps_start=0.95, eps_final=0.1,
+                             eps_decay=decay, gamma=0.7, batch_size=2048, updates_per_step=1,
+                             capacity=2_000_000, target_every=13,
+                             allreduce=GradAllReduce() if world > 1 else None, overlap=True, seed=0)
+        if world > 1:
+            broadcast_params(L.source)
+            L.target.load_state_dict(L.source.state_dict())
+        tr = VectorOffPolicyTrainer(env, L, seed=7919 * rank + 2, bank_candidates=C)
+        tr.train(20)
+        secs = timed_train(tr, a.cfg2_steps, "config 2 leg")
+        rec = {"envs_per_gpu": B, "grid": dim, "algo": "r-prim", "variant": "dqn",
+               "vector_steps": a.cfg2_steps, "seconds": round(secs, 3),
+               "env_steps_per_s": B * a.cfg2_steps * world / secs, "updates": L.n_updates,
+               "batch": 2048, "updates_per_vector_step": 1, "training_mazes_candidates": C,
+               "grad_allreduce": (dist.get_backend() if world > 1 else None)}
+        env.close()
+        if rank == 0:
+            n = a.cfg_eval_mazes
+            rec["win_rate_greedy"], _ = evaluate(L, n, dim, "r-prim", seed=0x7E520000, eps=0.0,
+                                                 device=dev)
+            mz = best_of_mazes(n, dim, "r-prim", seed=0x7E530000, device=dev)
+            rec["win_rate_greedy_best_of_6"], _ = evaluate(L, n, dim, "r-prim", seed=0x7E530000,
+                                                           eps=0.0, device=dev, mazes=mz)
+            rec["eval_mazes"] = n
+        out["cfg2"] = rec
+        del tr, L
     if "cfg4" in legs:
         if rank == 0:
             log("config 4 leg (DDQN, mixed 81x81)")
         B, dim = a.cfg4_envs, 81
         algo = ((torch.arange(B) + rank * B) % 3).to(torch.uint8)
         env = VectorMazeEnv(B, dim, enrich=True, device=dev, algorithm=algo,
-                            seed=0x5EED0000 + rank * B, done_list=False, window=False, window_bits=True)
+                            seed=0x5EED0000 + rank * B, done_list=False, window=False, window_bits=True,
+                            candidates=C)
         env.set_algorithm(algo)
         decay = ((dim - 1) * (dim - 1) // 2) * 5 / 40.0
         # 4 updates of 512 per vector step: at 8,192 instances one update of 2,048 (the same
@@ -347,14 +407,15 @@ def config_legs(a, dev, rank=0, world=1):
         if world > 1:
             broadcast_params(L.source)
             L.target.load_state_dict(L.source.state_dict())
-        tr = VectorOffPolicyTrainer(env, L, seed=7919 * rank)
+        tr = VectorOffPolicyTrainer(env, L, seed=7919 * rank, bank_candidates=C)
         tr.train(20)
         secs = timed_train(tr, a.cfg4_steps, "config 4 leg")
         env.close()
         rec = {"envs_per_gpu": B, "grid": dim, "algo": "mixed (global id mod 3)",
                "vector_steps": a.cfg4_steps, "seconds": round(secs, 3),
                "env_steps_per_s": B * a.cfg4_steps * world / secs, "updates": L.n_updates,
-               "batch": 512, "updates_per_vector_step": 4, "grad_allreduce": (dist.get_backend() if world > 1 else None)}
+               "batch": 512, "updates_per_vector_step": 4, "training_mazes_candidates": C,
+               "grad_allreduce": (dist.get_backend() if world > 1 else None)}
         if rank == 0:
             rec["win_rate_reference_protocol"] = reference_protocol(L, a.cfg_eval_mazes, dim, dev,
                                                                     0x7E5A0000)
@@ -362,35 +423,46 @@ def config_legs(a, dev, rank=0, world=1):
         out["cfg4"] = rec
         del tr, L
     if "cfg5" in legs:
-        if rank == 0:
-            log("config 5 leg (PPO, toroidal 17..79)")
-        B = a.cfg5_envs
         dims = list(range(17, 80, 2))
-        env = make_env(B, dims, toroidal=True, algorithm="r-prim", seed=0x5EED0000 + rank * B,
-                       device=dev, done_list=False, reward64=True, window=False, window_bits=True)
-        tr = VectorPPOTrainer(env, dev, gamma=0.9, batch_size=2048, ppo_steps=2, pool_size=32768,
-                              seed=7919 * rank, allreduce=GradAllReduce() if world > 1 else None)
-        if world > 1:
-            broadcast_params(tr.net)
-        tr.train(20)
-        secs = timed_train(tr, a.cfg5_steps, "config 5 leg")
-        rec = {"envs_per_gpu": B, "dims": [dims[0], dims[-1]], "toroidal": True,
-               "vector_steps": a.cfg5_steps, "seconds": round(secs, 3),
-               "env_steps_per_s": B * a.cfg5_steps * world / secs, "updates": tr.updates,
-               "grad_allreduce": (dist.get_backend() if world > 1 else None)}
-        env.close()
-        if rank == 0:
-            n = a.cfg_eval_mazes
-            rec["win_rate_greedy"], _ = evaluate(tr, n, dims, "r-prim", seed=0x7E5B0000, eps=0.0,
-                                                 toroidal=True, device=dev)
-            t6 = time.perf_counter()
-            mz = best_of_mazes(n, dims, "r-prim", seed=0x7E5C0000, device=dev, toroidal=True)
-            rec["best_of_6_selection_seconds"] = round(time.perf_counter() - t6, 3)
-            rec["win_rate_greedy_best_of_6"], _ = evaluate(tr, n, dims, seed=0x7E5C0000, eps=0.0,
-                                                           toroidal=True, device=dev, mazes=mz)
-            rec["eval_mazes"] = n
-        out["cfg5"] = rec
-        del tr
+        for mode in [m for m in a.cfg5_modes.split(",") if m]:
+            if rank == 0:
+                log(f"config 5 leg (PPO, toroidal 17..79, {mode})")
+            B = a.cfg5_envs
+            growth = (17, 79) if mode == "growth" else None
+            env = make_env(B, [17] if growth else dims, toroidal=True, algorithm="r-prim",
+                           seed=0x5EED0000 + rank * B, device=dev, done_list=False, reward64=True,
+                           window=False, window_bits=True, candidates=C, max_dim=79)
+            tr = VectorPPOTrainer(env, dev, gamma=0.9, batch_size=2048, ppo_steps=2,
+                                  pool_size=32768, seed=7919 * rank, growth=growth,
+                                  bank_candidates=C,
+                                  allreduce=GradAllReduce() if world > 1 else None)
+            if world > 1:
+                broadcast_params(tr.net)
+            tr.train(20)
+            secs = timed_train(tr, a.cfg5_steps, f"config 5 leg ({mode})")
+            rec = {"mode": mode, "envs_per_gpu": B, "dims": [dims[0], dims[-1]], "toroidal": True,
+                   "vector_steps": a.cfg5_steps, "seconds": round(secs, 3),
+                   "env_steps_per_s": B * a.cfg5_steps * world / secs, "updates": tr.updates,
+                   "training_mazes_candidates": C,
+                   "grad_allreduce": (dist.get_backend() if world > 1 else None)}
+            if growth:
+                sm = tr.schedule.summary()
+                rec.update(growth=list(growth), train_wins=sm["total_wins"],
+                           instances_per_size_at_end={k: v for k, v in sm["instances_per_size"].items() if v},
+                           retired=sm["retired"], stopped_at=tr.stopped_at)
+            env.close()
+            if rank == 0:
+                n = a.cfg_eval_mazes
+                rec["win_rate_greedy"], _ = evaluate(tr, n, dims, "r-prim", seed=0x7E5B0000, eps=0.0,
+                                                     toroidal=True, device=dev)
+                t6 = time.perf_counter()
+                mz = best_of_mazes(n, dims, "r-prim", seed=0x7E5C0000, device=dev, toroidal=True)
+                rec["best_of_6_selection_seconds"] = round(time.perf_counter() - t6, 3)
+                rec["win_rate_greedy_best_of_6"], _ = evaluate(tr, n, dims, seed=0x7E5C0000, eps=0.0,
+                                                               toroidal=True, device=dev, mazes=mz)
+                rec["eval_mazes"] = n
+            out["cfg5" if mode == "fixed" else f"cfg5_{mode}"] = rec
+            del tr
     return out
 
 
@@ -489,8 +561,10 @@ def launch(n, argv, timeout, environ=None, script=None):
     """Start N child processes of this script (subprocess, never exec: the parent has not touched
     the GPU and stays a plain supervisor). Rank 0's stdout is relayed: JSON object lines to stdout
     (the bench line), anything else (e.g. the communication library's own banners) to stderr; the
-    other ranks' stdout goes to stderr. If any rank fails or the deadline passes, every rank's
-    process group is killed and the exit status is non-zero. Returns the exit status."""
+    other ranks' stdout goes to stderr. If any rank fails, the deadline passes, or the supervisor
+    itself gets SIGTERM / SIGINT (an outer `timeout`, Ctrl-C — the ranks run in sessions of their
+    own and would not see it), every rank's process group is killed and the exit status is
+    non-zero. Returns the exit status."""
     import signal
     import subprocess
     import threading
@@ -498,48 +572,70 @@ def launch(n, argv, timeout, environ=None, script=None):
     port = int(environ.get("MASTER_PORT") or _free_port())
     script = script or os.path.abspath(__file__)
     procs = []
-    for r, env in enumerate(launch_plan(n, environ, port)):
-        procs.append(subprocess.Popen([sys.executable, "-u", script] + list(argv), env=env,
-                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(),
-                                      start_new_session=True, text=True))
+    got = []  # signals received by the supervisor
 
-    def relay(stream):
-        for line in stream:
-            dst = sys.stdout if line.lstrip().startswith("{") else sys.stderr
-            dst.write(line)
-            dst.flush()
+    def on_signal(signum, frame):
+        got.append(signum)
 
-    reader = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
-    reader.start()
-    deadline = time.monotonic() + timeout
+    old = {sig: signal.signal(sig, on_signal) for sig in (signal.SIGTERM, signal.SIGINT)}
     rc = 0
-    while True:
-        codes = [p.poll() for p in procs]
-        bad = [c for c in codes if c not in (None, 0)]
-        if bad:
-            rc = bad[0] if bad[0] > 0 else 128 - bad[0]
-            print(f"bench launcher: a rank exited with {bad[0]}; stopping the others", file=sys.stderr)
-            break
-        if all(c == 0 for c in codes):
-            break
-        if time.monotonic() > deadline:
-            rc = 124
-            print(f"bench launcher: deadline of {timeout:.0f} s passed; stopping the ranks",
-                  file=sys.stderr)
-            break
-        time.sleep(0.2)
-    if rc:
-        for sig, wait in ((signal.SIGTERM, 10.0), (signal.SIGKILL, 5.0)):
-            for p in procs:
-                if p.poll() is None:
-                    try:
-                        os.killpg(p.pid, sig)
-                    except ProcessLookupError:
-                        pass
-            t0 = time.monotonic()
-            while any(p.poll() is None for p in procs) and time.monotonic() - t0 < wait:
-                time.sleep(0.1)
-    reader.join(timeout=5.0)
+    reader = None
+    try:
+        for r, env in enumerate(launch_plan(n, environ, port)):
+            procs.append(subprocess.Popen([sys.executable, "-u", script] + list(argv), env=env,
+                                          stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(),
+                                          start_new_session=True, text=True))
+
+        def relay(stream):
+            for line in stream:
+                dst = sys.stdout if line.lstrip().startswith("{") else sys.stderr
+                dst.write(line)
+                dst.flush()
+
+        reader = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
+        reader.start()
+        deadline = time.monotonic() + timeout
+        while True:
+            if got:
+                rc = 128 + got[0]
+                print(f"bench launcher: got signal {got[0]}; stopping the ranks", file=sys.stderr)
+                break
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0] if bad[0] > 0 else 128 - bad[0]
+                print(f"bench launcher: a rank exited with {bad[0]}; stopping the others",
+                      file=sys.stderr)
+                break
+            if all(c == 0 for c in codes):
+                break
+            if time.monotonic() > deadline:
+                rc = 124
+                print(f"bench launcher: deadline of {timeout:.0f} s passed; stopping the ranks",
+                      file=sys.stderr)
+                break
+            time.sleep(0.2)
+    except BaseException:
+        rc = rc or 1
+        raise
+    finally:
+        # every exit path that leaves ranks running (a failure, the deadline, a signal, an
+        # exception in this loop) tears their process groups down: SIGTERM, then SIGKILL
+        if any(p.poll() is None for p in procs):
+            for sig, wait in ((signal.SIGTERM, 10.0), (signal.SIGKILL, 5.0)):
+                for p in procs:
+                    if p.poll() is None:
+                        try:
+                            os.killpg(p.pid, sig)
+                        except ProcessLookupError:
+                            pass
+                t0 = time.monotonic()
+                while any(p.poll() is None for p in procs) and time.monotonic() - t0 < wait:
+                    time.sleep(0.1)
+        for sig, h in old.items():
+            signal.signal(sig, h)
+        if reader is not None:
+            reader.join(timeout=5.0)
     return rc
 
 
@@ -852,11 +948,12 @@ def main():
             out["win_rate"] = wr
             out["q_head"] = q_head(dev, B)
     if a.curriculum_steps > 0:
-        if rank == 0:
-            log("DDQN curriculum leg (the reference's new-maze protocol)")
-        cl = curriculum_leg(a, dev, rank, world)
-        if rank == 0:
-            out["curriculum_leg"] = cl
+        for j, rule in enumerate(x for x in a.curriculum_rules.split(",") if x):
+            if rank == 0:
+                log(f"DDQN curriculum leg, {rule} rule (the reference's new-maze protocol)")
+            cl = curriculum_leg(a, dev, rank, world, rule)
+            if rank == 0:
+                out["curriculum_leg" if j == 0 else "curriculum_leg_" + rule.replace("-", "_")] = cl
     if a.config_legs:
         cl = config_legs(a, dev, rank, world)
         if rank == 0:

@@ -132,6 +132,14 @@ struct WSet {
   int mask, fill, used;
   bool small;  // still the 8-slot smalltable
 };
+// The occupancy words and counters are wave-uniform: readfirstlane keeps them in SGPRs (scalar
+// branches over the probe sequence), and every update below is a value select — a field chosen
+// by a branch (`j < 64 ? o0 : o1` as an lvalue) made the compiler address the struct in scratch.
+__device__ inline uint64_t ws_uni64(uint64_t x) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
 __device__ inline void ws_init(WSet& s) {
   s.v0 = s.v1 = WS_EMPTY;
   s.o0 = s.o1 = 0;
@@ -139,33 +147,33 @@ __device__ inline void ws_init(WSet& s) {
   s.fill = s.used = 0;
   s.small = true;
 }
-__device__ inline bool ws_occ(const WSet& s, int j) {
-  return j < 64 ? ((s.o0 >> j) & 1) : ((s.o1 >> (j - 64)) & 1);
-}
 // the first empty slot of key's probe sequence (the key is known to be absent)
 __device__ inline int ws_free_slot(const WSet& s, uint32_t key) {
+  const uint64_t o0 = ws_uni64(s.o0), o1 = ws_uni64(s.o1);
+  const uint32_t mask = (uint32_t)__builtin_amdgcn_readfirstlane(s.mask);
   uint32_t perturb = key;
-  int i = (int)(key & (uint32_t)s.mask);
+  int i = (int)(key & mask);
   for (;;) {
-    const int last = i + 9 <= s.mask ? i + 9 : i;
+    const int last = i + 9 <= (int)mask ? i + 9 : i;
     for (int j = i; j <= last; ++j)
-      if (!ws_occ(s, j)) return j;
+      if (!(((j < 64 ? o0 : o1) >> (j & 63)) & 1ull)) return j;
     perturb >>= 5;
-    i = (int)(((uint32_t)i * 5u + 1u + perturb) & (uint32_t)s.mask);
+    i = (int)(((uint32_t)i * 5u + 1u + perturb) & mask);
   }
 }
 __device__ inline void ws_put(WSet& s, int j, uint32_t val) {
   const int lane = threadIdx.x & (WAVE - 1);
-  if (j < 64) {
-    if (lane == j) s.v0 = val;
-    s.o0 |= 1ull << j;
-  } else {
-    if (lane == j - 64) s.v1 = val;
-    s.o1 |= 1ull << (j - 64);
-  }
+  const bool hi = j >= 64;
+  const uint64_t b = 1ull << (j & 63);
+  const bool mine = lane == (j & 63);
+  s.v0 = (mine && !hi) ? val : s.v0;
+  s.v1 = (mine && hi) ? val : s.v1;
+  s.o0 = ws_uni64(s.o0 | (hi ? 0ull : b));
+  s.o1 = ws_uni64(s.o1 | (hi ? b : 0ull));
 }
 __device__ inline uint32_t ws_get(const WSet& s, int j) {
-  return j < 64 ? (uint32_t)__shfl((int)s.v0, j) : (uint32_t)__shfl((int)s.v1, j - 64);
+  const int v = __shfl((int)(j < 64 ? s.v0 : s.v1), j & 63);
+  return (uint32_t)v;
 }
 // next occupied slot after j (table order), -1 at the end
 __device__ inline int ws_next(const WSet& s, int j) {
@@ -430,23 +438,78 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
   if (s_bad) { fail(2); return; }
   MC_PROBE_AT(1)
   // ---- B. the solution path (start -> goal along the goal-rooted parents), its points first --
-  if (threadIdx.x == 0) {
-    int x = start, k = 0, plain = 0;
-    for (int guard = 0; guard < NN; ++guard) {
-      fl[x] |= F_SOL;
-      if (fl[x] & F_POINT) {
-        plain += (fl[x] & F_JUNC) ? 0 : 1;
-        if (k < MM) nsq[k] = (uint16_t)x;
-        pos[x] = (uint16_t)k++;
+  // The path is start's chain of goal-ward parents — thousands of squares in a dfs maze, a serial
+  // pointer chase. Instead: 32-step jump pointers by 5 doubling rounds over every square (in fst,
+  // free until phase C, as two u16 arrays), lane 0 walks the milestones start, gp^32(start), ...
+  // (<= NN / 32 of them), then one thread per 32-square segment marks its squares and counts its
+  // points, a scan gives each segment its first position, and a second walk writes the positions
+  // (the same order as the serial walk: segment by segment along the path).
+  {
+    uint16_t* jc = reinterpret_cast<uint16_t*>(fst);
+    uint16_t* jn = jc + NNP;
+    for (int q = threadIdx.x; q < NN; q += T) jc[q] = gp[q];
+    __syncthreads();
+    for (int r = 0; r < 5; ++r) {
+      for (int q = threadIdx.x; q < NN; q += T) {
+        const int a = jc[q];
+        jn[q] = a == NONE ? NONE : jc[a];
       }
-      if (x == goal) break;
-      x = gp[x];
-      if (x == NONE) { s_bad = 1; break; }
+      __syncthreads();
+      uint16_t* t = jc; jc = jn; jn = t;
     }
-    s_nsol = k;
-    // every solution point a junction: the solution hallway would lie inside a branch (the
-    // reference then counts it twice) — left to the host restatement
-    if (k > MM || plain == 0) s_bad = 2;
+    uint16_t* mil = reinterpret_cast<uint16_t*>(keys);  // the node region is free until phase D
+    if (threadIdx.x == 0) {
+      int x = start, k = 0;
+      mil[k++] = (uint16_t)x;
+      while (jc[x] != NONE && k < NN) {
+        x = jc[x];
+        mil[k++] = (uint16_t)x;
+      }
+      s_noff = k;  // (s_noff is the phase-D counter: reset below)
+      s_open = 0;  // (read by phase A's checks only: the plain-point count from here)
+    }
+    __syncthreads();
+    const int K = s_noff;
+    int cnt = 0, plain = 0;
+    const bool seg = threadIdx.x < K;
+    if (seg) {
+      int x = mil[threadIdx.x];
+      for (int j = 0; j < 32; ++j) {
+        fl[x] |= F_SOL;
+        if (fl[x] & F_POINT) {
+          ++cnt;
+          plain += (fl[x] & F_JUNC) ? 0 : 1;
+        }
+        if (x == goal) break;
+        x = gp[x];
+        if (x == NONE) { s_bad = 1; break; }
+      }
+    }
+    if (plain) atomicAdd(&s_open, plain);  // (s_open is free after phase A: the plain-point count)
+    int tot;
+    const int base = block_excl(seg ? cnt : 0, wsum, &tot);
+    if (seg) {
+      int x = mil[threadIdx.x], k = base;
+      for (int j = 0; j < 32; ++j) {
+        if (fl[x] & F_POINT) {
+          if (k < MM) nsq[k] = (uint16_t)x;
+          pos[x] = (uint16_t)k++;
+        }
+        if (x == goal) break;
+        x = gp[x];
+        if (x == NONE) break;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      s_nsol = tot;
+      // every solution point a junction: the solution hallway would lie inside a branch (the
+      // reference then counts it twice) — left to the host restatement
+      if (tot > MM || s_open == 0) s_bad = s_bad ? s_bad : 2;
+      s_noff = 0;
+    }
+    // fst back to its phase-C initial value
+    for (int q = threadIdx.x; q < NN; q += T) fst[q] = 0xFFFFFFFFu;
   }
   __syncthreads();
   if (s_bad) { fail(2); return; }

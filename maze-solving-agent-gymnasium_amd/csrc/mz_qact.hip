@@ -83,8 +83,8 @@ __device__ inline float bf16_round(float x) {  // x rounded to bf16, as f32 (RNE
 }
 // x = hi + lo + O(2^-17 x): the two bf16 halves, packed for a pair of adjacent elements
 __device__ inline void split2(float x0, float x1, uint32_t& hi, uint32_t& lo) {
-  const float h0 = bf16_round(x0), h1 = bf16_round(x1);
-  hi = bf16x2(h0, h1);
+  hi = bf16x2(x0, x1);  // one packed conversion; its halves back as f32 by shift / mask
+  const float h0 = __uint_as_float(hi << 16), h1 = __uint_as_float(hi & 0xFFFF0000u);
   lo = bf16x2(x0 - h0, x1 - h1);
 }
 
@@ -129,15 +129,12 @@ __device__ inline void mfma_x3(const frag_ab (&ah)[I], const frag_ab (&al)[I], c
 }
 
 // ---- the conv stem (shared by k_qact1 and k_qconv) --------------------------------------------
-// LDS tables and the tile's window rows: lut (8 patch bits -> 8 bf16), spread (8 bits -> bits at
-// 3i), wb (the rows' window bits), crow (column-interleaved padded window rows). Two barriers.
-__device__ inline void conv_tables(const MzQAct& q, int r0, int nr, int tid, int nthr, uint4* lut,
+// LDS tables and the tile's window rows: spread (8 bits -> bits at 3i), wb (the rows' window
+// bits), crow (column-interleaved padded window rows). Two barriers.
+__device__ inline void conv_tables(const MzQAct& q, int r0, int nr, int tid, int nthr,
                                    uint32_t* spread, uint64_t* crow, uint32_t* wb) {
   for (int i = tid; i < 256; i += nthr) {
-    uint32_t v[4], sp = 0;
-    for (int p = 0; p < 4; ++p)
-      v[p] = (((i >> (2 * p)) & 1) ? 0x3F80u : 0u) | (((i >> (2 * p + 1)) & 1) ? 0x3F800000u : 0u);
-    lut[i] = make_uint4(v[0], v[1], v[2], v[3]);
+    uint32_t sp = 0;
     for (int k = 0; k < 8; ++k) sp |= ((uint32_t)(i >> k) & 1u) << (3 * k);
     spread[i] = sp;
   }
@@ -215,9 +212,20 @@ __device__ inline void drop_seeds(const MzQAct& q, int r0, int w, int g4, int c1
 // the MFMA's A row of this lane = c16: instance 4t + c16 / 4, position c16 % 4 of its 2x2 pooling
 // window): LeakyReLU, DDQN's dropout, 2x2 max-pool, split into bf16 hi / lo. Out: for each tile
 // tt, row il[tt] of the 64-row block, channels 2 c16 and 2 c16 + 1 packed as hi[tt] / lo[tt].
+// 8 patch bits -> the MFMA operand's 8 bf16 (0 / 1.0), bit 2i in the low and bit 2i + 1 in the
+// high half of word i: y = B | B << 15 puts bit 2i + 1 at 2i + 16, so word i = ((y >> 2i) & 0x10001)
+// * 0x3F80. Arithmetic instead of a 256-entry LDS table: that table's data-dependent 16-B reads
+// were most of k_qconv's LDS bank conflicts (16.0 M of 29.4 M LDS-active cycles,
+// profiles/r04final_qact_pmc.json)
+__device__ inline uint4 patch_bf16(uint32_t B) {
+  const uint32_t y = B | (B << 15);
+  return make_uint4((y & 0x10001u) * 0x3F80u, ((y >> 2) & 0x10001u) * 0x3F80u,
+                    ((y >> 4) & 0x10001u) * 0x3F80u, ((y >> 6) & 0x10001u) * 0x3F80u);
+}
+
 template <bool DROP, int TPWv>
 __device__ inline void conv_chunk_vals(const MzQAct& q, int c, int w, int g4, int c16,
-                                       const uint4* lut, const uint64_t* crow, const ConvW& cw,
+                                       const uint64_t* crow, const ConvW& cw,
                                        uint32_t (&rs)[4], int (&il)[TPWv], uint32_t (&hi)[TPWv],
                                        uint32_t (&lo)[TPWv]) {
   const int py = c / 7, px = c - py * 7;
@@ -230,7 +238,7 @@ __device__ inline void conv_chunk_vals(const MzQAct& q, int c, int w, int g4, in
     const uint32_t p = ((uint32_t)(cr[0] >> (3 * xx)) & 0x1FFu) |
                        (((uint32_t)(cr[1] >> (3 * xx)) & 0x1FFu) << 9) |
                        (((uint32_t)(cr[2] >> (3 * xx)) & 0x1FFu) << 18);
-    a[tt] = __builtin_bit_cast(frag_ab, lut[(p >> (8 * g4)) & 0xFFu]);
+    a[tt] = __builtin_bit_cast(frag_ab, patch_bf16((p >> (8 * g4)) & 0xFFu));
   }
   frag_cd e[TPWv], o[TPWv];
 #pragma unroll
@@ -296,7 +304,6 @@ __device__ inline void obs_vals(const MzQAct& q, int r0, int nr, int r, int k2, 
 template <bool DROP>
 __global__ __launch_bounds__(T1) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void k_qact1(MzQAct q, int row_tiles) {
-  __shared__ uint4 lut[256];                   // 8 patch bits -> 8 bf16 (0 / 1.0)
   __shared__ uint32_t spread[256];             // 8 bits -> bits at 3i
   __shared__ uint64_t crow[RT1 * PR];          // column-interleaved padded window rows
   __shared__ uint32_t wb[RT1 * 22];            // the rows' window bits
@@ -315,7 +322,7 @@ void k_qact1(MzQAct q, int row_tiles) {
   if (r0 >= m) return;
   const int nr = min(RT1, m - r0);
 
-  conv_tables(q, r0, nr, tid, T1, lut, spread, crow, wb);
+  conv_tables(q, r0, nr, tid, T1, spread, crow, wb);
   const ConvW cw = conv_weights(q, g4, c16);
   uint32_t rs[4];
   if (DROP) drop_seeds<TPW>(q, r0, w, g4, c16, rs);
@@ -350,7 +357,7 @@ void k_qact1(MzQAct q, int row_tiles) {
   auto conv_chunk = [&](int c) {
     int il[TPW];
     uint32_t hi[TPW], lo[TPW];
-    conv_chunk_vals<DROP, TPW>(q, c, w, g4, c16, lut, crow, cw, rs, il, hi, lo);
+    conv_chunk_vals<DROP, TPW>(q, c, w, g4, c16, crow, cw, rs, il, hi, lo);
     uint16_t* Ah = A[c & 1][0];
     uint16_t* Al = A[c & 1][1];
 #pragma unroll
@@ -502,7 +509,6 @@ constexpr int QF_CPB = MZ_QFC1_CPB;
 template <bool DROP>
 __global__ __launch_bounds__(T1) void k_qconv(MzQAct q, int row_tiles, int groups,
                                               uint16_t* __restrict__ feat) {
-  __shared__ uint4 lut[256];
   __shared__ uint32_t spread[256];
   __shared__ uint64_t crow[RT1 * PR];
   __shared__ uint32_t wb[RT1 * 22];
@@ -517,7 +523,7 @@ __global__ __launch_bounds__(T1) void k_qconv(MzQAct q, int row_tiles, int group
   const int nr = min(RT1, m - r0);
   const int per = (NCH + groups - 1) / groups;
   const int c0 = grp * per, c1 = min(NCH, c0 + per);
-  conv_tables(q, r0, nr, tid, T1, lut, spread, crow, wb);
+  conv_tables(q, r0, nr, tid, T1, spread, crow, wb);
   const ConvW cw = conv_weights(q, g4, c16);
   uint32_t rs[4];
   if (DROP) drop_seeds<TPW>(q, r0, w, g4, c16, rs);
@@ -525,7 +531,7 @@ __global__ __launch_bounds__(T1) void k_qconv(MzQAct q, int row_tiles, int group
   for (int c = c0; c < min(c1, NCH - 1); ++c) {
     int il[TPW];
     uint32_t hi[TPW], lo[TPW];
-    conv_chunk_vals<DROP, TPW>(q, c, w, g4, c16, lut, crow, cw, rs, il, hi, lo);
+    conv_chunk_vals<DROP, TPW>(q, c, w, g4, c16, crow, cw, rs, il, hi, lo);
     uint32_t* fh = reinterpret_cast<uint32_t*>(ft + (size_t)c * FT_CHUNK);
     uint32_t* fl = fh + RT1 * 16;
 #pragma unroll

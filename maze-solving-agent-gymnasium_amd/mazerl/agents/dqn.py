@@ -33,6 +33,8 @@ from .nets import QNet
 
 
 STACK_ROWS = True  # DDQN on packed windows (GPU): source(s) and source(s') as one pass
+# the overlapped learner's K updates of a vector step as one graph replay (MZ_K_BLOCK=1; 0: K replays)
+K_BLOCK = os.environ.get("MZ_K_BLOCK", "0") != "0"
 # GPU: the loss and its gradient w.r.t. the Q rows as two HIP launches (MZ_FUSED_LOSS=0: torch ops)
 FUSED_LOSS = os.environ.get("MZ_FUSED_LOSS", "1") != "0"
 
@@ -293,6 +295,8 @@ class VectorDQNLearner:
             self.opt = optim.AdamW(self.source.parameters(), lr)
         self._graph = None
         self._graph_loss = None
+        self._graphK = [None, None]  # K-update graphs of the overlapped learner, per index slot
+        self._graphK_loss = [None, None]
         self._eager_updates = 0
         self.sched = lr_scheduler.CosineAnnealingLR(self.opt, T_max=t_max, eta_min=1e-5)
         from ..replay import DeviceReplay
@@ -486,9 +490,20 @@ class VectorDQNLearner:
         self._sample_counter += 1
         if self._acting == slot:  # greedy() must switch to a newer snapshot before reading again
             self._acting = None
+        block = self._k_block_ok()
+        if block and self._graphK[slot] is None:
+            self._capture_k_block(slot)
         S.wait_stream(M)  # push(t), the indices, and every greedy() that read this slot
         with torch.cuda.stream(S):
-            for k in range(K):
+            if block:
+                # the K updates as ONE replay: no target sync or schedule step falls between them
+                self._graphK[slot].replay()
+                self.n_updates += K
+                if self.n_updates % self.target_every == 0:
+                    self._sync_target()
+                if self.n_updates % self.updates_per_epoch == 0:
+                    self.sched.step()
+            for k in range(0 if block else K):
                 rp.idx_static.copy_(idx[k])
                 self._graph[0].replay()
                 if self.allreduce is not None:
@@ -507,8 +522,31 @@ class VectorDQNLearner:
         self._idx_ev[slot] = ev
         self._published.append((slot, ev))
         self._par ^= 1
-        self.last_loss = self._graph_loss
+        self.last_loss = self._graphK_loss[slot] if block else self._graph_loss
         return self.last_loss
+
+    # K > 1 updates per vector step: one captured graph per index slot replays all K (the index
+    # copies included), when neither the target sync nor the cosine schedule's step falls strictly
+    # between two of them (those run on the host between replays); else the per-update replays.
+    # The same kernels in the same order as K single-update replays: the same results bit for bit.
+    # Not with a gradient all-reduce (the collective runs between graph replays).
+    def _k_block_ok(self):
+        K = self.updates_per_step
+        if K < 2 or self.allreduce is not None or not K_BLOCK or not self.bit_stem:
+            return False
+        n0 = self.n_updates
+        return all((n0 + j) % self.target_every and (n0 + j) % self.updates_per_epoch
+                   for j in range(1, K))
+
+    def _capture_k_block(self, slot):
+        rp, K = self.replay, self.updates_per_step
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for k in range(K):
+                rp.idx_static.copy_(self._idx[slot][k])
+                loss = self._one_update(None, static=True)
+        self._graphK[slot] = g
+        self._graphK_loss[slot] = loss
 
     def finish(self):
         """Join the side stream: the main stream waits for every issued update; greedy() acts with

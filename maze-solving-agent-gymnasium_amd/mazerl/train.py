@@ -14,8 +14,7 @@ import torch
 
 from .agents.dqn import VectorDQNLearner
 from .distributed import GradAllReduce, allreduce_sum, broadcast_params, init_from_env
-from .trainers.vector_trainer import VectorOffPolicyTrainer, best_of_mazes, evaluate
-from .vector_env import VectorMazeEnv
+from .trainers.vector_trainer import VectorOffPolicyTrainer, best_of_mazes, evaluate, make_env
 
 
 def parse(argv=None):
@@ -36,9 +35,18 @@ def parse(argv=None):
     ap.add_argument("--target-every", type=int, default=13)
     ap.add_argument("--eval-mazes", type=int, default=1000)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--curriculum", action="store_true",
-                    help="change_algorithm per instance (off_policy_trainer.py:302-310): prim&kill "
-                         "from the 5th win, dfs from the 10th, epsilon_decay *3 / *4")
+    ap.add_argument("--curriculum", default="none", choices=["none", "global", "per-instance"],
+                    help="change_algorithm (off_policy_trainer.py:302-310): prim&kill from the 5th "
+                         "win, dfs from the 10th, epsilon_decay *3 / *4 — counted over the learner's "
+                         "wins (global, the reference's one agent) or per instance "
+                         "(mazerl/trainers/schedule.py)")
+    ap.add_argument("--growth", default=None,
+                    help="START,MAX: the variable-size env's +4 growth per win from START up to MAX "
+                         "and the max-shape stop (simple_variable_maze_env.py:93-112, "
+                         "off_policy_trainer.py:210-212); --dim is then MAX")
+    ap.add_argument("--candidates", type=int, default=6,
+                    help="training mazes: each the easiest of C by McClendon difficulty "
+                         "(base_maze_env.py:78-97); 1 = one Philox maze each")
     ap.add_argument("--log-every", type=int, default=50)
     ap.add_argument("--acting", default="x3", choices=["x3", "bf16"],
                     help="acting forward: x3 = f32-accurate bf16x3 MFMA (QAct); bf16 = bf16 head")
@@ -65,9 +73,12 @@ def main(argv=None):
         algo = (torch.arange(B) + rank * B) % 3
     else:
         algo = a.algo
-    env = VectorMazeEnv(B, a.dim, enrich=True, device=dev, algorithm=algo,
-                        seed=0x5EED0000 + rank * B, done_list=False, pos=True,
-                        window=False, window_bits=True)  # acting reads the bits (agents/fused.py)
+    growth = tuple(int(x) for x in a.growth.split(",")) if a.growth else None
+    if growth:
+        a.dim = growth[1]
+    env = make_env(B, growth[0] if growth else a.dim, algorithm=algo, seed=0x5EED0000 + rank * B,
+                   device=dev, max_dim=a.dim, candidates=a.candidates, done_list=False, pos=True,
+                   window=False, window_bits=True)  # acting reads the bits (agents/fused.py)
     env.set_algorithm(algo if isinstance(algo, str) else algo.to(torch.uint8))
     decay = a.eps_decay or ((a.dim - 1) * (a.dim - 1) // 2) * 5 / 40.0
     learner = VectorDQNLearner(B, dev, variant=a.variant, lr=a.lr, eps_start=a.eps_start,
@@ -79,7 +90,9 @@ def main(argv=None):
     if world > 1:
         broadcast_params(learner.source)
         learner.target.load_state_dict(learner.source.state_dict())
-    trainer = VectorOffPolicyTrainer(env, learner, seed=a.seed + 7919 * rank, curriculum=a.curriculum)
+    trainer = VectorOffPolicyTrainer(env, learner, seed=a.seed + 7919 * rank,
+                                     curriculum=None if a.curriculum == "none" else a.curriculum,
+                                     growth=growth, algorithm=algo, bank_candidates=a.candidates)
     if a.resume:  # every rank its own shard's env / replay; the nets are identical on all ranks
         from .checkpoint import load_checkpoint
         load_checkpoint(_ck_path(a.resume, rank, world), trainer)
@@ -115,6 +128,8 @@ def main(argv=None):
             "win_rate_greedy": greedy, "win_rate_eps": epsr, "eval_eps": a.eps_final,
             "win_rate_greedy_best_of_6": g6, "win_rate_eps_best_of_6": e6,
             "eval_mazes": a.eval_mazes, "eval_steps": [kg, ke],
+            "candidates": a.candidates, "stopped_at": trainer.stopped_at,
+            "schedule": trainer.schedule.summary() if trainer.schedule is not None else None,
         }
         print(json.dumps(res), flush=True)
     env.close()

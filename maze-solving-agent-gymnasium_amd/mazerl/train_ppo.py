@@ -29,6 +29,16 @@ def main(argv=None):
     ap.add_argument("--eval-mazes", type=int, default=1000)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--eager-update", action="store_true", help="no captured minibatch step")
+    ap.add_argument("--growth", default=None,
+                    help="START,MAX: ToroidalVariableMazeEnv's +4 growth per win from START up to MAX "
+                         "and the max-shape stop (toroidal_variable_maze_env.py:113-131, "
+                         "ppo_trainer.py:96-105) instead of fixed per-instance sizes (--dims then "
+                         "only sets the evaluation sizes)")
+    ap.add_argument("--curriculum", default="none", choices=["none", "global", "per-instance"],
+                    help="change_algorithm (ppo_trainer.py:137-141)")
+    ap.add_argument("--candidates", type=int, default=6,
+                    help="training mazes: each the easiest of C by McClendon difficulty of the "
+                         "bordered maze (toroidal_maze_env.py:40-54); 1 = one Philox maze each")
     ap.add_argument("--no-bank", action="store_true",
                     help="build winners' new mazes inline instead of copying them from a maze bank")
     ap.add_argument("--resume", default=None, help="checkpoint to continue from (<path>.rank<r> "
@@ -43,11 +53,15 @@ def main(argv=None):
     rank, world, local = init_from_env()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    env = make_env(a.envs, dims, toroidal=True, algorithm=a.algo, seed=0x5EED0000 + rank * a.envs,
-                   device=dev, done_list=False, reward64=True, window=False, window_bits=True)
+    growth = tuple(int(x) for x in a.growth.split(",")) if a.growth else None
+    env = make_env(a.envs, [growth[0]] if growth else dims, toroidal=True, algorithm=a.algo,
+                   seed=0x5EED0000 + rank * a.envs, device=dev, done_list=False, reward64=True,
+                   window=False, window_bits=True, candidates=a.candidates,
+                   max_dim=max(growth[1] if growth else 0, max(dims)))
     tr = VectorPPOTrainer(env, dev, gamma=a.gamma, batch_size=a.batch, ppo_steps=a.ppo_steps,
                           pool_size=a.pool, seed=a.seed + 7919 * rank, use_graph=not a.eager_update,
-                          bank=not a.no_bank,
+                          bank=not a.no_bank, curriculum=None if a.curriculum == "none" else a.curriculum,
+                          growth=growth, algorithm=a.algo, bank_candidates=a.candidates,
                           allreduce=GradAllReduce() if world > 1 else None)
     if world > 1:
         broadcast_params(tr.net)
@@ -75,6 +89,8 @@ def main(argv=None):
                           "episodes": int(st[0]), "wins": int(st[1]), "updates": tr.updates,
                           "seed": a.seed, "acting": "f32 (ActorCriticNet.act as the reference)",
                           "win_rate_greedy": rate, "win_rate_greedy_best_of_6": rate6,
+                          "candidates": a.candidates, "stopped_at": tr.stopped_at,
+                          "schedule": tr.schedule.summary() if tr.schedule is not None else None,
                           "eval_mazes": a.eval_mazes, "eval_steps": k}), flush=True)
     env.close()
 

@@ -70,6 +70,8 @@ class WinSchedule:
         self.maze_algo = a.clone()           # algorithm of each instance's current maze
         self.total_wins = torch.zeros((), dtype=torch.int64, device=dev)
         self.inst_wins = torch.zeros(B, dtype=torch.int32, device=dev)
+        # new mazes handed to winners per algorithm id (index_add: no host synchronisation)
+        self.new_mazes = torch.zeros(3, dtype=torch.int64, device=dev)
         self.growth = None
         if growth is not None:
             start, mx = (int(x) for x in growth)
@@ -135,8 +137,10 @@ class WinSchedule:
         if self.growth is None:
             if self.rule is not None:
                 self.maze_algo = torch.where(t, self.algo, self.maze_algo)
+                self.new_mazes.index_add_(0, self.algo.long(), t.to(torch.int64))
             return
         moved = t & (self.next_dim > 0)  # winners that got a maze of the next size
+        self.new_mazes.index_add_(0, self.algo.long(), moved.to(torch.int64))
         self.dim = torch.where(moved, self.next_dim.to(torch.int32), self.dim)
         self.maze_algo = torch.where(moved, self.algo, self.maze_algo)
         self.retired |= t & (self.dim >= self.growth[1])
@@ -147,10 +151,11 @@ class WinSchedule:
 
     def summary(self):
         """Host-side counts (one synchronisation)."""
+        names = ["r-prim", "dfs", "prim&kill"]  # ids: vector_env.ALGOS
         out = {"rule": self.rule, "total_wins": int(self.total_wins),
                "instances_per_algorithm": dict(zip(
-                   ["r-prim", "dfs", "prim&kill"],
-                   torch.bincount(self.maze_algo.long(), minlength=3).tolist()))}
+                   names, torch.bincount(self.maze_algo.long(), minlength=3).tolist())),
+               "new_mazes_per_algorithm": dict(zip(names, self.new_mazes.tolist()))}
         if self.growth is not None:
             sizes = growth_sizes(*self.growth)
             cnt = torch.bincount((self.dim - self.growth[0]) // 4, minlength=len(sizes)).tolist()
@@ -158,7 +163,7 @@ class WinSchedule:
                        retired=int(self.retired.sum()))
         return out
 
-    _STATE = ("algo", "maze_algo", "total_wins", "inst_wins")
+    _STATE = ("algo", "maze_algo", "total_wins", "inst_wins", "new_mazes")
 
     def state_dict(self):
         sd = {k: getattr(self, k).clone() for k in self._STATE}

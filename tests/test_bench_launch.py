@@ -94,3 +94,45 @@ def test_launch_deadline(tmp_path):
     """, 2, timeout=2.0)
     assert p.returncode == 124
     assert "deadline" in p.stderr
+
+
+def test_supervisor_sigterm_stops_the_ranks(tmp_path):
+    """An outer `timeout` signals only the supervisor's process group; the ranks run in sessions of
+    their own, so the supervisor must kill them on SIGTERM."""
+    import signal
+    import time
+    pidfile = tmp_path / "pids"
+    script = tmp_path / "rank.py"
+    script.write_text(textwrap.dedent(f"""
+        import os, time
+        with open({str(pidfile)!r}, "a") as f:
+            f.write(str(os.getpid()) + "\\n")
+        time.sleep(120)
+    """))
+    code = (f"import sys; sys.path.insert(0, {ROOT!r}); import bench; "
+            f"sys.exit(bench.launch(3, [], 600.0, script={str(script)!r}))")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "MASTER_PORT")}
+    sup = subprocess.Popen([sys.executable, "-c", code], env=env, stdout=subprocess.PIPE,
+                           stderr=subprocess.PIPE, text=True)
+    t0 = time.monotonic()
+    while time.monotonic() - t0 < 60:
+        if pidfile.exists() and len(pidfile.read_text().split()) == 3:
+            break
+        time.sleep(0.1)
+    pids = [int(x) for x in pidfile.read_text().split()]
+    assert len(pids) == 3
+    sup.send_signal(signal.SIGTERM)
+    out, err = sup.communicate(timeout=60)
+    assert sup.returncode == 128 + signal.SIGTERM, err
+    assert "got signal" in err
+
+    def alive(pid):
+        try:
+            os.kill(pid, 0)
+        except ProcessLookupError:
+            return False
+        return True
+    t0 = time.monotonic()
+    while any(alive(p) for p in pids) and time.monotonic() - t0 < 10:
+        time.sleep(0.1)
+    assert not any(alive(p) for p in pids)

@@ -244,3 +244,52 @@ def test_stacked_ddqn_pass_train_mode_matches_torch_with_same_masks():
     g_ref = torch.autograd.grad((q_ref[:b] * R.double()).sum(), list(ref.parameters()))
     for (name, _), a, c in zip(net.named_parameters(), g, g_ref):
         assert _close(a, c.float(), 1e-4, 1e-5), name
+
+
+def test_k_update_block_graph_matches_per_update_replays():
+    """K = 4 updates per vector step as one captured graph per index slot (agents/dqn.py
+    _capture_k_block) against the K single-update replays (MZ_K_BLOCK off): the same kernels in
+    the same order, so parameters, optimizer state and losses agree bit for bit over vector steps
+    where the target sync falls at a block's end, strictly inside one (the per-update fallback) and
+    between blocks."""
+    from mazerl import VectorMazeEnv
+    from mazerl.agents import dqn as D
+    env = VectorMazeEnv(4, 21, enrich=True, device="cuda", seed=1)
+    kw = dict(batch_size=256, capacity=4096, updates_per_step=4, target_every=13,
+              updates_per_epoch=100)
+    A, B = _mk(True, **kw), _mk(True, **kw)
+    B.source.load_state_dict(A.source.state_dict())
+    B.target.load_state_dict(A.target.state_dict())
+    g = torch.Generator(device="cuda").manual_seed(11)
+    n = 4096
+    s6, s6n = (torch.randn(n, 6, device="cuda", generator=g) for _ in range(2))
+    sw, swn = (torch.randint(0, 2**31 - 1, (n, 22), device="cuda", generator=g, dtype=torch.int32)
+               for _ in range(2))
+    a = torch.randint(0, 4, (n,), device="cuda", generator=g)
+    r = torch.randn(n, device="cuda", generator=g)
+    for L in (A, B):
+        L.replay.push(s6, sw, a, r, s6n, swn)
+    blocks = 0
+    for k in range(14):
+        old = D.K_BLOCK
+        try:
+            D.K_BLOCK = True
+            blocks += int(A._async and A._k_block_ok())
+            la = A.update(env.expand_window, reserve=0)
+            D.K_BLOCK = False
+            lb = B.update(env.expand_window, reserve=0)
+        finally:
+            D.K_BLOCK = old
+        torch.cuda.synchronize()
+        assert A.n_updates == B.n_updates
+        assert float(la) == float(lb), k
+        for (name, pa), pb in zip(A.source.named_parameters(), B.source.parameters()):
+            assert torch.equal(pa, pb), (k, name)
+        for pa, pb in zip(A.target.parameters(), B.target.parameters()):
+            assert torch.equal(pa, pb), k
+    assert torch.equal(A.opt.exp_avg, B.opt.exp_avg) and torch.equal(A.opt.exp_avg_sq, B.opt.exp_avg_sq)
+    assert blocks >= 5 and all(gk is not None for gk in A._graphK)
+    assert all(gk is None for gk in B._graphK)
+    A.finish()
+    B.finish()
+    env.close()
