@@ -252,6 +252,114 @@ __device__ inline bool ws_merge(WSet& dst, const WSet& src) {
   return true;
 }
 
+// ---- the same CPython 3.10 set table for ONE lane (a hallway per lane, phase G) --------------
+// Tables of <= 32 slots hold node ids (u16) in LDS — the key (cantor pairing of the node's square,
+// its own hash) is a bijection of the node, so a slot match by node is a match by key; occupancy
+// is a 32-bit mask in a register. The operations mirror ws_* above (and CPython's set_add_entry /
+// set_insert_clean / set_table_resize / set_merge) step for step; a table that would grow past 32
+// slots makes the caller hand the hallway to the wave path.
+struct LSet {
+  uint16_t* t;  // 32 slots
+  uint32_t occ;
+  int mask, fill, used;
+  bool small;
+};
+__device__ inline void ls_init(LSet& s, uint16_t* buf) {
+  s.t = buf;
+  s.occ = 0u;
+  s.mask = 7;
+  s.fill = s.used = 0;
+  s.small = true;
+}
+// slot of `node` (key `key`) if present (*found), else the first empty slot of key's probe sequence
+__device__ inline int ls_probe(const LSet& s, uint32_t key, int node, bool* found) {
+  uint32_t perturb = key;
+  int i = (int)(key & (uint32_t)s.mask);
+  for (;;) {
+    const int last = i + 9 <= s.mask ? i + 9 : i;
+    for (int j = i; j <= last; ++j) {
+      if (!((s.occ >> j) & 1u)) { *found = false; return j; }
+      if (s.t[j] == (uint16_t)node) { *found = true; return j; }
+    }
+    perturb >>= 5;
+    i = (int)(((uint32_t)i * 5u + 1u + perturb) & (uint32_t)s.mask);
+  }
+}
+__device__ inline int ls_find(const LSet& s, uint32_t key, int node) {
+  bool f;
+  const int j = ls_probe(s, key, node, &f);
+  return f ? j : -1;
+}
+template <class KEY>
+__device__ inline bool ls_resize(LSet& s, int minused, uint16_t* tmp, const KEY& key_of) {
+  int ns = 8;
+  while (ns <= minused) ns <<= 1;
+  if (ns == 8 && s.small) return true;
+  if (ns > 32) return false;
+  int n = 0;
+  for (int j = 0; j <= s.mask; ++j)
+    if ((s.occ >> j) & 1u) tmp[n++] = s.t[j];
+  s.occ = 0u;
+  s.mask = ns - 1;
+  s.small = ns == 8;
+  for (int k = 0; k < n; ++k) {  // insert_clean in the old table's order
+    bool f;
+    const int j = ls_probe(s, key_of(tmp[k]), tmp[k], &f);
+    s.t[j] = tmp[k];
+    s.occ |= 1u << j;
+  }
+  s.fill = s.used = n;
+  return true;
+}
+template <class KEY>
+__device__ inline int ls_add(LSet& s, int node, uint16_t* tmp, const KEY& key_of) {
+  bool f;
+  const uint32_t key = key_of(node);
+  const int j = ls_probe(s, key, node, &f);
+  if (f) return 0;
+  s.t[j] = (uint16_t)node;
+  s.occ |= 1u << j;
+  s.fill += 1;
+  s.used += 1;
+  if (s.fill * 5 >= s.mask * 3 && !ls_resize(s, s.used > 50000 ? s.used * 2 : s.used * 4, tmp, key_of))
+    return -1;
+  return 1;
+}
+// dst = set(src) (set_merge into an empty set; dst's buffer distinct from src's)
+template <class KEY>
+__device__ inline bool ls_copy(LSet& dst, uint16_t* dbuf, const LSet& src, uint16_t* tmp,
+                               const KEY& key_of) {
+  ls_init(dst, dbuf);
+  if (src.used == 0) return true;
+  if (src.used * 5 >= dst.mask * 3 && !ls_resize(dst, src.used * 2, tmp, key_of)) return false;
+  if (dst.mask == src.mask) {
+    for (int j = 0; j <= src.mask; ++j) dst.t[j] = src.t[j];
+    dst.occ = src.occ;
+    dst.small = src.small;
+  } else {
+    for (int j = 0; j <= src.mask; ++j) {
+      if (!((src.occ >> j) & 1u)) continue;
+      bool f;
+      const int k = ls_probe(dst, key_of(src.t[j]), src.t[j], &f);
+      dst.t[k] = src.t[j];
+      dst.occ |= 1u << k;
+    }
+  }
+  dst.fill = dst.used = src.used;
+  return true;
+}
+// dst.update(src) for a non-empty dst
+template <class KEY>
+__device__ inline bool ls_merge(LSet& dst, const LSet& src, uint16_t* tmp, const KEY& key_of) {
+  if (src.used == 0) return true;
+  if ((dst.fill + src.used) * 5 >= dst.mask * 3 && !ls_resize(dst, (dst.used + src.used) * 2, tmp, key_of))
+    return false;
+  for (int j = 0; j <= src.mask; ++j)
+    if ((src.occ >> j) & 1u)
+      if (ls_add(dst, src.t[j], tmp, key_of) < 0) return false;
+  return true;
+}
+
 typedef unsigned __int128 u128;
 
 __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, int n, int MM,

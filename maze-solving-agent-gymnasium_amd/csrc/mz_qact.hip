@@ -53,7 +53,11 @@ constexpr int NT1 = 64 * QW1;      // k_qact1 fc1 outputs per workgroup
 constexpr int TPW = 16 / QW1;      // conv tiles (4 rows each) per wave
 constexpr int NTL1 = N1 / NT1;     // fc1 output tiles
 constexpr int XPT = 8 / NTL1;      // XCDs per output tile
-constexpr int PR = 17;             // padded window rows per instance
+// crow pitch per instance in u64: 17 padded rows (0 and 16 zero) + 3 spare. A conv operand read
+// (ds_read2_b64 of rows y, y + 1 for the 4 instances of a tile) spans dword banks
+// 2 (PR inst + y) .. + 5: at PR = 17 (34 dwords per instance) instances k and k + 2 overlapped
+// (68 = 4 mod 64) — 2-way conflicts on every read; at 20 (40 dwords) the four ranges are disjoint
+constexpr int PR = 20;
 constexpr int AST = 40;            // k_qact1 LDS A-tile row stride in bf16 (32 + 8; 2-way on b128 reads)
 // k_qact2 rows per workgroup: each wave streams its 256 KB of fc2 hi / lo fragments once per
 // workgroup (2 MB per 64 rows of L2 traffic). 128 rows halve that but need 256 VGPRs with spills:

@@ -33,8 +33,8 @@ from .nets import QNet
 
 
 STACK_ROWS = True  # DDQN on packed windows (GPU): source(s) and source(s') as one pass
-# the overlapped learner's K updates of a vector step as one graph replay (MZ_K_BLOCK=1; 0: K replays)
-K_BLOCK = os.environ.get("MZ_K_BLOCK", "0") != "0"
+# the overlapped learner's K updates of a vector step as one graph replay (MZ_K_BLOCK=0: K replays)
+K_BLOCK = os.environ.get("MZ_K_BLOCK", "1") != "0"
 # GPU: the loss and its gradient w.r.t. the Q rows as two HIP launches (MZ_FUSED_LOSS=0: torch ops)
 FUSED_LOSS = os.environ.get("MZ_FUSED_LOSS", "1") != "0"
 
@@ -288,13 +288,9 @@ class VectorDQNLearner:
         self.bit_stem = bool(bit_stem) and self.device.type == "cuda"
         if self.use_graph:
             # one flat buffer per net: clamp + AdamW in one launch, whole-net copies in one
-            from .flat import FlatAdamW, flatten_grads, flatten_params
+            from .flat import FlatAdamW, flatten_params
             flatten_params(self.target)
-            # the clamped gradient is not read after the step: not written back (8.56 MB)
-            self.opt = FlatAdamW(self.source, lr, write_grad=False)
-            # gradients written by the backward kernels into one flat buffer: one contiguous
-            # AdamW read, and an all-reduce in place with no pack / unpack copies
-            flatten_grads(self.source)
+            self.opt = FlatAdamW(self.source, lr)
         else:
             self.opt = optim.AdamW(self.source.parameters(), lr)
         self._graph = None

@@ -1,0 +1,8 @@
+"""Module-path mirror of the reference's agents/dqn_agent.py."""
+from ..replay import ReplayMemory, Transition  # noqa: F401
+from .dqn import DQNAgent  # noqa: F401
+from .nets import QNet as _QNet
+
+
+def DQN(in_channels, n_observations, n_actions, h_channels, hidden_dim=1024):
+    return _QNet(in_channels, n_observations, n_actions, h_channels, hidden_dim, "dqn")

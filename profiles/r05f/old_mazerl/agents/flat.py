@@ -55,64 +55,14 @@ def _aliases(flat, params, sizes):
     return len(params) == len(sizes)
 
 
-def flatten_grads(net):
-    """Lay the net's parameter gradients out as views of ONE flat f32 buffer shaped like its flat
-    parameter buffer (`net._flat_grads`). The learner's backward kernels (GraphSafeLinear's GEMMs
-    and column sums, the HIP stem's weight gradients) write each gradient straight into its
-    segment and hand autograd a fresh view of it, which becomes `.grad` without a copy. Then the
-    optimizer reads one contiguous gradient, and the gradient all-reduce runs on the buffer in
-    place: no pack / unpack copies, the 1/N average folded into the AdamW launch
-    (distributed.GradAllReduce, FlatAdamW.step). Idempotent; returns the buffer."""
-    flat = flatten_params(net)
-    g = getattr(net, "_flat_grads", None)
-    if g is None or g.numel() != flat.numel() or g.device != flat.device:
-        g = torch.zeros_like(flat)
-        net._flat_grads = g
-    off = 0
-    for p, n in zip(net.parameters(), net._flat_sizes):
-        p._grad_seg = (g, off)
-        off += n
-    return g
-
-
-def grad_segment(p, shape=None):
-    """A fresh view of parameter p's segment of its net's flat gradient buffer (None if the net
-    has none): the output a backward kernel writes p's gradient into."""
-    seg = getattr(p, "_grad_seg", None) if p is not None else None
-    if seg is None:
-        return None
-    g, off = seg
-    shape = tuple(p.shape) if shape is None else tuple(shape)
-    n = 1
-    for d in shape:
-        n *= d
-    return g[off:off + n].view(shape)
-
-
-def grads_are_flat(net, params=None):
-    """True when every parameter's .grad is its segment of net._flat_grads (what flatten_grads
-    sets up and the backward kernels fill)."""
-    g = getattr(net, "_flat_grads", None)
-    if g is None:
-        return False
-    off = 0
-    for p, n in zip(params if params is not None else net.parameters(), net._flat_sizes):
-        if p.grad is None or p.grad.data_ptr() != g.data_ptr() + 4 * off:
-            return False
-        off += n
-    return True
-
-
 def copy_flat(dst_net, src_net):
     """dst <- src for two flattened nets of the same architecture (one device copy)."""
     dst_net._flat_params.copy_(src_net._flat_params)
 
 
 class FlatAdamW(torch.optim.Optimizer):
-    def __init__(self, net, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, clamp=1.0,
-                 write_grad=True):
+    def __init__(self, net, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, clamp=1.0):
         flat = flatten_params(net)
-        self.net = net
         params = list(net.parameters())
         dev = flat.device
         if dev.type != "cuda":
@@ -130,31 +80,14 @@ class FlatAdamW(torch.optim.Optimizer):
         self.step_t = self._step_buf[0]
         self.clamp = float(clamp)
         self.grad_scale = 1.0
-        # write_grad: the clamped gradient is stored back (torch's clamp_ leaves it in .grad);
-        # the learners' hot path turns that 8.56 MB write off
-        self.write_grad = bool(write_grad)
         self.lib = N.load()
         self._seg_len = (C.c_int64 * len(params))(*self.sizes)
-        self._one_len = (C.c_int64 * 1)(sum(self.sizes))
 
     @torch.no_grad()
     def step(self, closure=None):
         if closure is not None:
             raise ValueError("closures are not supported")
         g = self.param_groups[0]
-        b1, b2 = g["betas"]
-        st = torch.cuda.current_stream(self.flat.device).cuda_stream
-        # the average of a gradient all-reduce run in place on the flat gradient buffer
-        # (distributed.GradAllReduce) is folded into the launch's gradient scale
-        scale = float(self.grad_scale) * float(getattr(self.net, "_allreduce_scale", 1.0))
-        if grads_are_flat(self.net, g["params"]):  # one contiguous gradient segment
-            arr = (C.c_void_p * 1)(self.net._flat_grads.data_ptr())
-            N.check(self.lib.mz_adamw_flat(self.flat.data_ptr(), self.exp_avg.data_ptr(),
-                                           self.exp_avg_sq.data_ptr(), arr, self._one_len, 1,
-                                           g["lr"].data_ptr(), self._step_buf.data_ptr(), float(b1),
-                                           float(b2), float(g["eps"]), float(g["weight_decay"]),
-                                           self.clamp, scale, int(self.write_grad), st))
-            return
         ptrs = []
         for p, n in zip(g["params"], self.sizes):
             if p.grad is None:
@@ -167,11 +100,13 @@ class FlatAdamW(torch.optim.Optimizer):
                 # keep the padded storage alive with the gradient
             ptrs.append(p.grad.data_ptr())
         arr = (C.c_void_p * len(ptrs))(*ptrs)
+        b1, b2 = g["betas"]
+        st = torch.cuda.current_stream(self.flat.device).cuda_stream
         N.check(self.lib.mz_adamw_flat(self.flat.data_ptr(), self.exp_avg.data_ptr(),
                                        self.exp_avg_sq.data_ptr(), arr, self._seg_len, len(ptrs),
                                        g["lr"].data_ptr(), self._step_buf.data_ptr(), float(b1),
                                        float(b2), float(g["eps"]), float(g["weight_decay"]),
-                                       self.clamp, scale, int(self.write_grad), st))
+                                       self.clamp, float(self.grad_scale), 1, st))
 
 
 class FlatAdamWGroups(torch.optim.Optimizer):

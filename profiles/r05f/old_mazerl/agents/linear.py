@@ -26,7 +26,6 @@ class _LinearFn(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
         ctx.n_grad = n_grad
-        ctx.wp, ctx.bp = w, b  # flat gradient segments (agents/flat.py flatten_grads), if any
         return F.linear(x, w, b)
 
     @staticmethod
@@ -44,38 +43,25 @@ class _LinearFn(torch.autograd.Function):
                 torch.mm(gy_n, w, out=gx[:n])
             else:
                 gx = gy @ w
-        from .flat import grad_segment
-        gw = None
-        if ctx.needs_input_grad[1]:
-            gw = grad_segment(ctx.wp)
-            if gw is None:
-                gw = gy_n.t() @ x_n
-            else:  # straight into the flat gradient buffer (becomes .grad without a copy)
-                torch.mm(gy_n.t(), x_n, out=gw)
+        gw = gy_n.t() @ x_n if ctx.needs_input_grad[1] else None
         gb = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            gb = _bias_grad(gy_n, out=grad_segment(ctx.bp))
-        ctx.wp = ctx.bp = None
+            gb = _bias_grad(gy_n)
         return gx, gw, gb, None
 
 
-def _bias_grad(gy, out=None):
+def _bias_grad(gy):
     """db = dY^T 1: one HIP column-sum launch (mz_colsum_f32) for f32 rows whose width is a
-    multiple of 4; else a GEMV against ones. `out`: where to write it (a flat gradient segment)."""
+    multiple of 4; else a GEMV against ones."""
     m = gy.shape[1]
     if gy.dtype == torch.float32 and m % 4 == 0:
         from .. import _native as N
         g = gy if gy.is_contiguous() and gy.data_ptr() % 16 == 0 else gy.contiguous()
-        if out is None:
-            out = torch.empty(m, dtype=torch.float32, device=gy.device)
+        out = torch.empty(m, dtype=torch.float32, device=gy.device)
         N.check(N.load().mz_colsum_f32(g.data_ptr(), g.shape[0], m, m, out.data_ptr(),
                                        torch.cuda.current_stream(gy.device).cuda_stream))
         return out
-    r = torch.mv(gy.t(), torch.ones(gy.shape[0], dtype=gy.dtype, device=gy.device))
-    if out is not None:
-        out.copy_(r)
-        return out
-    return r
+    return torch.mv(gy.t(), torch.ones(gy.shape[0], dtype=gy.dtype, device=gy.device))
 
 
 class GraphSafeLinear(nn.Linear):

@@ -41,7 +41,6 @@ class _StemFn(torch.autograd.Function):
             ctx.save_for_backward(bits, code)
         ctx.p = float(p)
         ctx.n_grad = n if n_grad is None else max(0, min(int(n_grad), n))
-        ctx.wp, ctx.bp = weight, bias  # flat gradient segments (agents/flat.py), if any
         return feat
 
     @staticmethod
@@ -53,13 +52,8 @@ class _StemFn(torch.autograd.Function):
         gfeat = gfeat[:n].contiguous()
         dev = gfeat.device
         ws = torch.empty(max(1, L.mz_stem_workspace_floats(n)), dtype=torch.float32, device=dev)
-        from .flat import grad_segment
-        dw = grad_segment(ctx.wp, (32, 3, 3, 3))
-        db = grad_segment(ctx.bp, (32,))
-        ctx.wp = ctx.bp = None
-        if dw is None or db is None:
-            dw = torch.empty(32, 3, 3, 3, dtype=torch.float32, device=dev)
-            db = torch.empty(32, dtype=torch.float32, device=dev)
+        dw = torch.empty(32, 3, 3, 3, dtype=torch.float32, device=dev)
+        db = torch.empty(32, dtype=torch.float32, device=dev)
         st = torch.cuda.current_stream(dev).cuda_stream
         N.check(L.mz_stem_backward(bits.data_ptr(), code.data_ptr(), gfeat.data_ptr(), IN_DIM, n,
                                    ctx.p, ws.data_ptr(), dw.data_ptr(), db.data_ptr(), st))

@@ -46,12 +46,6 @@ class GradAllReduce:
         self._flat = None
 
     def pack(self, net):
-        from .agents.flat import grads_are_flat
-        if grads_are_flat(net):
-            # the backward wrote the gradients into one flat buffer (agents/flat.py
-            # flatten_grads): reduce it in place — no pack copies
-            self._flat = net._flat_grads
-            return
         grads = [p.grad for p in net.parameters()]
         n = sum(g.numel() for g in grads)
         if self._flat is None or self._flat.numel() != n or self._flat.device != grads[0].device:
@@ -65,12 +59,6 @@ class GradAllReduce:
         dist.all_reduce(self._flat, op=dist.ReduceOp.SUM, group=self.group)
 
     def unpack(self, net):
-        from .agents.flat import grads_are_flat
-        if grads_are_flat(net) and self._flat is getattr(net, "_flat_grads", None):
-            # reduced in place; the 1/N average is folded into the optimizer's AdamW launch
-            # (FlatAdamW.step reads net._allreduce_scale): no unpack kernels
-            net._allreduce_scale = 1.0 / self.world
-            return
         off = 0
         for p in net.parameters():
             g = p.grad

@@ -106,3 +106,29 @@ def test_flat_adamw_step_counts_are_independent_and_graph_safe():
     ob.step()
     torch.cuda.synchronize()
     assert float(oa.step_t) == 12.0 and float(ob.step_t) == 15.0
+
+
+def test_learner_gradients_land_in_the_flat_buffer():
+    """VectorDQNLearner's backward writes every source-net gradient into its segment of ONE flat
+    buffer (agents/flat.py flatten_grads: GraphSafeLinear's GEMM / column-sum outputs and the HIP
+    stem's weight gradients, kept by autograd as .grad without a copy) — eager and captured — so
+    FlatAdamW reads one contiguous gradient and a gradient all-reduce runs on it in place."""
+    from mazerl import VectorMazeEnv
+    from mazerl.agents.dqn import VectorDQNLearner
+    from mazerl.agents.flat import grads_are_flat
+    from test_learner_graph import _fill
+    env = VectorMazeEnv(4, 21, enrich=True, device="cuda", seed=1)
+    L = VectorDQNLearner(4, "cuda", variant="ddqn", batch_size=32, capacity=64, seed=3)
+    _fill(L)
+    for _ in range(5):  # 3 eager warm-up updates, the capture, a replay
+        L.update(env.expand_window)
+        torch.cuda.synchronize()
+        assert grads_are_flat(L.source)
+        g = L.source._flat_grads
+        assert float(g.abs().sum()) > 0
+        off = 0
+        for p, n in zip(L.source.parameters(), L.source._flat_sizes):
+            assert p.grad.data_ptr() == g.data_ptr() + 4 * off
+            off += n
+    assert L._graph is not None
+    env.close()
