@@ -259,13 +259,15 @@ __device__ inline bool ws_merge(WSet& dst, const WSet& src) {
 // set_insert_clean / set_table_resize / set_merge) step for step; a table that would grow past 32
 // slots makes the caller hand the hallway to the wave path.
 struct LSet {
-  uint16_t* t;  // 32 slots
+  uint16_t* t;  // 32 slots, slot j at t[j * st] (the lanes' tables interleave: conflict-free LDS)
+  int st;
   uint32_t occ;
   int mask, fill, used;
   bool small;
 };
-__device__ inline void ls_init(LSet& s, uint16_t* buf) {
+__device__ inline void ls_init(LSet& s, uint16_t* buf, int st) {
   s.t = buf;
+  s.st = st;
   s.occ = 0u;
   s.mask = 7;
   s.fill = s.used = 0;
@@ -279,7 +281,7 @@ __device__ inline int ls_probe(const LSet& s, uint32_t key, int node, bool* foun
     const int last = i + 9 <= s.mask ? i + 9 : i;
     for (int j = i; j <= last; ++j) {
       if (!((s.occ >> j) & 1u)) { *found = false; return j; }
-      if (s.t[j] == (uint16_t)node) { *found = true; return j; }
+      if (s.t[j * s.st] == (uint16_t)node) { *found = true; return j; }
     }
     perturb >>= 5;
     i = (int)(((uint32_t)i * 5u + 1u + perturb) & (uint32_t)s.mask);
@@ -298,14 +300,15 @@ __device__ inline bool ls_resize(LSet& s, int minused, uint16_t* tmp, const KEY&
   if (ns > 32) return false;
   int n = 0;
   for (int j = 0; j <= s.mask; ++j)
-    if ((s.occ >> j) & 1u) tmp[n++] = s.t[j];
+    if ((s.occ >> j) & 1u) tmp[n++ * s.st] = s.t[j * s.st];
   s.occ = 0u;
   s.mask = ns - 1;
   s.small = ns == 8;
   for (int k = 0; k < n; ++k) {  // insert_clean in the old table's order
     bool f;
-    const int j = ls_probe(s, key_of(tmp[k]), tmp[k], &f);
-    s.t[j] = tmp[k];
+    const int node = tmp[k * s.st];
+    const int j = ls_probe(s, key_of(node), node, &f);
+    s.t[j * s.st] = (uint16_t)node;
     s.occ |= 1u << j;
   }
   s.fill = s.used = n;
@@ -317,7 +320,7 @@ __device__ inline int ls_add(LSet& s, int node, uint16_t* tmp, const KEY& key_of
   const uint32_t key = key_of(node);
   const int j = ls_probe(s, key, node, &f);
   if (f) return 0;
-  s.t[j] = (uint16_t)node;
+  s.t[j * s.st] = (uint16_t)node;
   s.occ |= 1u << j;
   s.fill += 1;
   s.used += 1;
@@ -329,19 +332,20 @@ __device__ inline int ls_add(LSet& s, int node, uint16_t* tmp, const KEY& key_of
 template <class KEY>
 __device__ inline bool ls_copy(LSet& dst, uint16_t* dbuf, const LSet& src, uint16_t* tmp,
                                const KEY& key_of) {
-  ls_init(dst, dbuf);
+  ls_init(dst, dbuf, src.st);
   if (src.used == 0) return true;
   if (src.used * 5 >= dst.mask * 3 && !ls_resize(dst, src.used * 2, tmp, key_of)) return false;
   if (dst.mask == src.mask) {
-    for (int j = 0; j <= src.mask; ++j) dst.t[j] = src.t[j];
+    for (int j = 0; j <= src.mask; ++j) dst.t[j * dst.st] = src.t[j * src.st];
     dst.occ = src.occ;
     dst.small = src.small;
   } else {
     for (int j = 0; j <= src.mask; ++j) {
       if (!((src.occ >> j) & 1u)) continue;
       bool f;
-      const int k = ls_probe(dst, key_of(src.t[j]), src.t[j], &f);
-      dst.t[k] = src.t[j];
+      const int node = src.t[j * src.st];
+      const int k = ls_probe(dst, key_of(node), node, &f);
+      dst.t[k * dst.st] = (uint16_t)node;
       dst.occ |= 1u << k;
     }
   }
@@ -356,7 +360,7 @@ __device__ inline bool ls_merge(LSet& dst, const LSet& src, uint16_t* tmp, const
     return false;
   for (int j = 0; j <= src.mask; ++j)
     if ((src.occ >> j) & 1u)
-      if (ls_add(dst, src.t[j], tmp, key_of) < 0) return false;
+      if (ls_add(dst, src.t[j * src.st], tmp, key_of) < 0) return false;
   return true;
 }
 
@@ -367,7 +371,7 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
                                                  int mult) {
   extern __shared__ __align__(16) unsigned char lds[];
   __shared__ int wsum[T / WAVE];
-  __shared__ int s_bad, s_nsol, s_noff, s_open, s_edges, s_Hn, s_Bn;
+  __shared__ int s_bad, s_nsol, s_noff, s_open, s_edges, s_Hn, s_Bn, s_nl, s_nw, s_wq;
   const int i = blockIdx.x;
   if (i >= n) return;
   // a bank refill scores the candidates of its consumed slots only: min(*limit, n / mult) groups
@@ -826,6 +830,7 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
   uint32_t* hcur = bmin;    // [Hn + 2] counts, then scatter cursors
   if (Hn + 2 > MM) { fail(2); return; }
   for (int h = threadIdx.x; h <= Hn + 1; h += T) hcur[h] = 0;
+  if (threadIdx.x == 0) { s_nl = 0; s_nw = 0; s_wq = 0; }
   __syncthreads();
   for (int v = threadIdx.x; v < M; v += T)
     if (hid[v]) atomicAdd(&hcur[hid[v]], 1u);
@@ -849,7 +854,7 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
     if (hid[v]) hlist[atomicAdd(&hcur[hid[v]], 1u)] = (uint16_t)v;
   __syncthreads();
   {
-    const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
+    const int lane = threadIdx.x & (WAVE - 1);
     auto key_of = [&](int v) -> uint32_t {  // cantor_pairing((r, c)) (:7-20), also its hash
       const int q = nsq[v], r = q / N, c = q - r * N;
       return (uint32_t)((r + c) * (r + c + 1) / 2 + c);
@@ -862,7 +867,14 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
       for (int k = WAVE / 2; k; k >>= 1) x = min(x, __shfl_xor(x, k));
       return x;
     };
-    for (int h = 1 + wid; h <= Hn; h += T / WAVE) {
+    auto term = [](double& sum, long& D, int& nterm, int dd) {  // sum() from int 0, left to right
+      const double t = __ddiv_rn(1.0, __dmul_rn(2.0, (double)dd));
+      sum = nterm ? __dadd_rn(sum, t) : t;
+      D += dd;
+      ++nterm;
+    };
+    // the wave path: one hallway per wave, its sets in the wave's 128-slot tables
+    auto wave_hallway = [&](int h) {
       const int b0 = (int)hstart[h], nc = (int)hstart[h + 1] - b0;
       // adjacent_split_points (:208-214): each member's junction neighbours up to and including
       // the first solution junction (the reference's break); in a tree each such junction
@@ -998,6 +1010,158 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
       } else if (lane == 0) {
         Ch[h] = __dmul_rn((double)D, sum);
       }
+    };
+    // the lane path: one hallway per lane, <= 15 view nodes (every table stays within 32 slots:
+    // add() resizes at 19 of 32, set(s) / update() to 2 x 15 = 30 < 32), its three tables (the
+    // set being built, the set it is built from, the resize scratch) interleaved in the keys and
+    // Cb regions (both free until phase H)
+    auto lane_hallway = [&](int h, uint16_t* base, int st) -> bool {
+      const int b0 = (int)hstart[h], nc = (int)hstart[h + 1] - b0;
+      uint16_t* q = hlist + b0;  // the member list, then the BFS queue (the same nc nodes)
+      int first = 0x7FFFFFFF;
+      for (int i = 0; i < nc; ++i) first = min(first, (int)q[i]);
+      uint16_t* tA = base;
+      uint16_t* tB = base + 32 * st;
+      uint16_t* tT = base + 64 * st;
+      double sum = 0.0;
+      long D = 0;
+      int nterm = 0;
+      LSet S1, S2;
+      ls_init(S1, tA, st);
+      bool ok = ls_add(S1, first, tT, key_of) >= 0;
+      q[0] = (uint16_t)first;
+      int qn = 1;
+      for (int hd = 0; hd < qn && ok; ++hd) {  // _plain_bfs, as in the wave path
+        const int x = q[hd];
+        const int na = adjn[x];
+        int ord[4], no = 0;
+        for (int k = 0; k < na; ++k) {
+          const int u = adjp[4 * x + k];
+          if (u >= x) continue;
+          int j = no++;
+          while (j > 0 && ord[j - 1] > u) { ord[j] = ord[j - 1]; --j; }
+          ord[j] = u;
+        }
+        for (int k = 0; k < na; ++k) {
+          const int u = adjp[4 * x + k];
+          if (u > x) ord[no++] = u;
+        }
+        for (int k = 0; k < no && ok; ++k) {
+          const int u = ord[k];
+          if (!in_h(u)) continue;
+          const int r = ls_add(S1, u, tT, key_of);
+          if (r < 0 || (r == 1 && qn >= nc)) ok = false;
+          else if (r == 1) q[qn++] = (uint16_t)u;
+        }
+      }
+      ok = ok && ls_copy(S2, tB, S1, tT, key_of);
+      ls_init(S1, tA, st);
+      for (int j = 0; j <= S2.mask && ok; ++j) {
+        if (!((S2.occ >> j) & 1u)) continue;
+        const int m = S2.t[j * st];
+        for (int k = 0; k < adjn[m]; ++k) {
+          const int u = adjp[4 * m + k];
+          if (nfl[u] & N_JUNC) {
+            if (ls_add(S1, u, tT, key_of) < 0) ok = false;
+            if (nfl[u] & N_SOL) break;
+          }
+        }
+      }
+      ok = ok && ls_merge(S2, S1, tT, key_of);
+      ls_init(S1, tA, st);
+      for (int j = 0; j <= S2.mask && ok; ++j)
+        if ((S2.occ >> j) & 1u)
+          if (ls_add(S1, S2.t[j * st], tT, key_of) < 0) ok = false;
+      if (!ok) return false;
+      if (2 * S1.used < M) {
+        for (int j = 0; j <= S1.mask; ++j) {
+          if (!((S1.occ >> j) & 1u)) continue;
+          const int nn = S1.t[j * st];
+          for (int k = 0; k < adjn[nn]; ++k) {
+            const int u = adjp[4 * nn + k];
+            if (ls_find(S1, key_of(u), u) > j) term(sum, D, nterm, adjd[4 * nn + k]);
+          }
+        }
+      } else {
+        int last = -1;
+        for (int c = 0; c < S1.used; ++c) {
+          int nn = 0x7FFFFFFF;
+          for (int j = 0; j <= S1.mask; ++j)
+            if ((S1.occ >> j) & 1u) {
+              const int v = S1.t[j * st];
+              if (v > last) nn = min(nn, v);
+            }
+          for (int k = 0; k < adjn[nn]; ++k) {
+            const int u = adjp[4 * nn + k];
+            if (u > nn && ls_find(S1, key_of(u), u) >= 0) term(sum, D, nterm, adjd[4 * nn + k]);
+          }
+          last = nn;
+        }
+      }
+      Ch[h] = __dmul_rn((double)D, sum);
+      return true;
+    };
+    // G1: one thread per hallway classifies it — <= 3 view nodes: its sum now (the fast path);
+    // <= 15: the lane queue; else the wave queue (both in the phase-F bmin region, free now)
+    uint16_t* Lq = reinterpret_cast<uint16_t*>(bmin);
+    uint16_t* Wq = Lq + MM;
+    const int Lr = (int)((size_t)MM * 8 / (96 * sizeof(uint16_t)));  // lanes per region
+    const int L = min(2 * Lr, T / 2);
+    for (int h = 1 + threadIdx.x; h <= Hn; h += T) {
+      const int b0 = (int)hstart[h], nc = (int)hstart[h + 1] - b0;
+      int nasp = 0;
+      if (nc <= 15)
+        for (int i = 0; i < nc; ++i) {
+          const int m = hlist[b0 + i];
+          for (int k = 0; k < adjn[m]; ++k) {
+            const int u = adjp[4 * m + k];
+            if (nfl[u] & N_JUNC) {
+              ++nasp;
+              if (nfl[u] & N_SOL) break;
+            }
+          }
+        }
+      if (nc <= 15 && nc + nasp <= 3) {
+        double sum = 0.0;
+        long D = 0;
+        int nterm = 0;
+        for (int i = 0; i < nc; ++i) {
+          const int m = hlist[b0 + i];
+          bool jstop = false;
+          for (int k = 0; k < adjn[m]; ++k) {
+            const int u = adjp[4 * m + k];
+            if (in_h(u)) {
+              if (u > m) term(sum, D, nterm, adjd[4 * m + k]);
+            } else if ((nfl[u] & N_JUNC) && !jstop) {
+              term(sum, D, nterm, adjd[4 * m + k]);
+              if (nfl[u] & N_SOL) jstop = true;
+            }
+          }
+        }
+        Ch[h] = __dmul_rn((double)D, sum);
+      } else if (nc <= 15 && nc + nasp <= 15 && L > 0) {
+        Lq[atomicAdd(&s_nl, 1)] = (uint16_t)h;
+      } else {
+        Wq[atomicAdd(&s_nw, 1)] = (uint16_t)h;
+      }
+    }
+    __syncthreads();
+    // G2: the lane queue on the first L threads; every wave, once its lanes are done, takes the
+    // wave queue's hallways one at a time
+    const int nl = s_nl, nw = s_nw;
+    if ((int)threadIdx.x < L) {
+      const int l = threadIdx.x;
+      uint16_t* base = l < Lr ? reinterpret_cast<uint16_t*>(keys) + l
+                              : reinterpret_cast<uint16_t*>(Cb) + (l - Lr);
+      for (int k = l; k < nl; k += L)
+        if (!lane_hallway(Lq[k], base, Lr)) s_bad = 2;
+    }
+    for (;;) {
+      int k = 0;
+      if (lane == 0) k = atomicAdd(&s_wq, 1);
+      k = __shfl(k, 0);
+      if (k >= nw) break;
+      wave_hallway(Wq[k]);
     }
   }
   __syncthreads();

@@ -167,6 +167,8 @@ def learner_update(net, optimizer, loss, clamp=1.0, allreduce=None):
     if allreduce is not None:
         allreduce(net)  # average grads over ranks, then clamp (single-GPU semantics)
     learner_step(net, optimizer, clamp)
+    if allreduce is not None and hasattr(allreduce, "finish"):
+        allreduce.finish(net)  # sharded step: the updated parameter shards to every rank
 
 
 class _AgentBase:
@@ -311,6 +313,9 @@ class VectorDQNLearner:
         self.updates_per_epoch = updates_per_epoch
         self.act_bf16 = act_bf16
         self.allreduce = allreduce
+        if allreduce is not None and hasattr(allreduce, "attach"):
+            # reduce-scatter + AdamW over this rank's shard + all-gather (distributed.py)
+            allreduce.attach(self.source, self.opt)
         self.steps_done = torch.zeros(num_envs, dtype=torch.float32, device=self.device)
         self.n_updates = 0
         self.last_loss = torch.zeros((), device=self.device)
@@ -513,6 +518,7 @@ class VectorDQNLearner:
                 if self.allreduce is not None:
                     self.allreduce.reduce()
                     self._graph[1].replay()
+                    self.allreduce.gather(self.source)
                 self.n_updates += 1
                 if self.n_updates % self.target_every == 0:
                     self._sync_target()
@@ -721,6 +727,7 @@ class VectorDQNLearner:
         if ar is not None:
             ar.reduce()
             self._graph[1].replay()
+            ar.gather(self.source)
         self.last_loss = self._graph_loss
         if self.fused is not None:
             self.fused.invalidate()  # graph replays leave the params' _version untouched

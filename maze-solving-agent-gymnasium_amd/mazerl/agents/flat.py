@@ -21,6 +21,9 @@ import torch
 from .. import _native as N
 
 
+FLAT_ALIGN = 256
+
+
 def flatten_params(net):
     """Make `net`'s parameters views of one flat f32 buffer (idempotent); returns the buffer."""
     flat = getattr(net, "_flat_params", None)
@@ -33,7 +36,9 @@ def flatten_params(net):
     if any(p.device != dev or p.dtype != torch.float32 for p in params):
         raise ValueError("flatten_params needs f32 parameters on one device")
     sizes = [(p.numel() + 3) // 4 * 4 for p in params]  # 16-B aligned segments
-    flat = torch.zeros(sum(sizes), dtype=dt, device=dev)
+    # the buffer's length a multiple of FLAT_ALIGN floats (zero tail): it splits into equal,
+    # 16-B aligned shards over 2, 4, ... 64 ranks (distributed.GradAllReduce's sharded step)
+    flat = torch.zeros(-(-sum(sizes) // FLAT_ALIGN) * FLAT_ALIGN, dtype=dt, device=dev)
     off = 0
     with torch.no_grad():
         for p, n in zip(params, sizes):
@@ -135,7 +140,11 @@ class FlatAdamW(torch.optim.Optimizer):
         self.write_grad = bool(write_grad)
         self.lib = N.load()
         self._seg_len = (C.c_int64 * len(params))(*self.sizes)
-        self._one_len = (C.c_int64 * 1)(sum(self.sizes))
+        self._one_len = (C.c_int64 * 1)(flat.numel())
+        # (offset, length) of the flat buffer this rank updates: None = all of it; set by
+        # distributed.GradAllReduce when it shards the step (reduce-scatter of the gradients,
+        # AdamW over this rank's shard, all-gather of the parameters)
+        self.shard = None
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -148,13 +157,17 @@ class FlatAdamW(torch.optim.Optimizer):
         # (distributed.GradAllReduce) is folded into the launch's gradient scale
         scale = float(self.grad_scale) * float(getattr(self.net, "_allreduce_scale", 1.0))
         if grads_are_flat(self.net, g["params"]):  # one contiguous gradient segment
-            arr = (C.c_void_p * 1)(self.net._flat_grads.data_ptr())
-            N.check(self.lib.mz_adamw_flat(self.flat.data_ptr(), self.exp_avg.data_ptr(),
-                                           self.exp_avg_sq.data_ptr(), arr, self._one_len, 1,
+            o, ln = (0, self._one_len) if self.shard is None else (
+                4 * self.shard[0], (C.c_int64 * 1)(self.shard[1]))
+            arr = (C.c_void_p * 1)(self.net._flat_grads.data_ptr() + o)
+            N.check(self.lib.mz_adamw_flat(self.flat.data_ptr() + o, self.exp_avg.data_ptr() + o,
+                                           self.exp_avg_sq.data_ptr() + o, arr, ln, 1,
                                            g["lr"].data_ptr(), self._step_buf.data_ptr(), float(b1),
                                            float(b2), float(g["eps"]), float(g["weight_decay"]),
                                            self.clamp, scale, int(self.write_grad), st))
             return
+        if self.shard is not None:
+            raise RuntimeError("a sharded step needs the flat gradient buffer (flatten_grads)")
         ptrs = []
         for p, n in zip(g["params"], self.sizes):
             if p.grad is None:

@@ -5,7 +5,9 @@ learner's data-parallel gradient all-reduce over RCCL (torch.distributed backend
 Per update the source net's gradients (2,140,548 fp32 = 8.56 MB at full size) are flattened into
 ONE bucket and all-reduced once (xGMI ring: 2(N-1)/N x 8.56 MB per GPU, ~0.1 ms at ~153 GB/s per
 link), then averaged; grad.clamp_(-1, 1) runs after the average so N ranks reproduce the
-single-GPU update on the union batch (dqn_agent.py:152-153). Instance ids are global
+single-GPU update on the union batch (dqn_agent.py:152-153). The DQN / DDQN learners run that
+collective as a reduce-scatter, AdamW over each rank's 1/N shard, and an all-gather of the
+parameters (GradAllReduce.attach): the same bytes, 1/N of the optimizer's work per rank. Instance ids are global
 (rank * B + i) so maze seeds do not depend on the GPU count.
 """
 import os
@@ -38,12 +40,39 @@ class GradAllReduce:
 
     The three phases are also exposed separately so a HIP-graph-captured learner can replay
     "backward + pack" and "unpack + clamp + AdamW" as two graphs with the collective between
-    them (agents/dqn.py): pack / unpack are plain device copies, reduce is the one all-reduce."""
+    them (agents/dqn.py): pack / unpack are plain device copies, reduce is the one all-reduce.
 
-    def __init__(self, group=None):
+    Sharded step (`attach(net, opt)` with a FlatAdamW over flat gradients, the DQN / DDQN
+    learners): the all-reduce becomes a reduce-scatter of the flat gradient buffer (in place:
+    rank r receives the summed shard r), the optimizer's one launch runs over shard r only (the
+    clamp and AdamW are elementwise: each element's update is the one the full step computes),
+    and `gather(net)` all-gathers the updated parameter shards (in place). The same bytes cross
+    the links as with the all-reduce (a ring all-reduce IS a reduce-scatter + all-gather), but
+    each rank's AdamW reads / writes 1/N of the 2.14 M parameters and moments."""
+
+    def __init__(self, group=None, shard=None):
+        """shard: None = shard the step when attach() can and there are >= 2 ranks; True = also
+        with one rank (the collectives then run as local copies: tests); False = all-reduce."""
         self.group = group
         self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
         self._flat = None
+        self.shard_mode = shard
+        self.sharded = False
+
+    def attach(self, net, opt):
+        """Shard `opt`'s step over the ranks when it can be (FlatAdamW, flat gradients, a flat
+        buffer that splits into 16-B aligned shards); returns whether it does."""
+        from .agents.flat import FlatAdamW
+        g = getattr(net, "_flat_grads", None)
+        n = 0 if g is None else g.numel()
+        want = self.shard_mode is True or (self.shard_mode is None and self.world > 1)
+        if want and isinstance(opt, FlatAdamW) and g is not None and n % (4 * self.world) == 0:
+            S = n // self.world
+            opt.shard = (self.rank * S, S)
+            self._net, self._S = net, S
+            self.sharded = True
+        return self.sharded
 
     def pack(self, net):
         from .agents.flat import grads_are_flat
@@ -52,6 +81,8 @@ class GradAllReduce:
             # flatten_grads): reduce it in place — no pack copies
             self._flat = net._flat_grads
             return
+        if self.sharded:
+            raise RuntimeError("a sharded step needs the flat gradient buffer")
         grads = [p.grad for p in net.parameters()]
         n = sum(g.numel() for g in grads)
         if self._flat is None or self._flat.numel() != n or self._flat.device != grads[0].device:
@@ -62,7 +93,20 @@ class GradAllReduce:
             off += g.numel()
 
     def reduce(self):
+        if self.sharded:
+            g, S, r = self._flat, self._S, self.rank
+            dist.reduce_scatter_tensor(g[r * S:(r + 1) * S], g, op=dist.ReduceOp.SUM,
+                                       group=self.group)
+            return
         dist.all_reduce(self._flat, op=dist.ReduceOp.SUM, group=self.group)
+
+    def gather(self, net):
+        """After the optimizer step: every rank's updated parameter shard to every rank (no-op
+        unless sharded)."""
+        if not self.sharded:
+            return
+        p, S, r = net._flat_params, self._S, self.rank
+        dist.all_gather_into_tensor(p, p[r * S:(r + 1) * S], group=self.group)
 
     def unpack(self, net):
         from .agents.flat import grads_are_flat
@@ -81,6 +125,10 @@ class GradAllReduce:
         self.pack(net)
         self.reduce()
         self.unpack(net)
+
+    def finish(self, net):
+        """The step after __call__ + the optimizer: the parameter all-gather when sharded."""
+        self.gather(net)
 
 
 def broadcast_params(net, src=0, group=None):

@@ -2,8 +2,8 @@
 maze_complexity_evaluation.py:38-329): ComplexityEvaluation(maze, start_pos, goal_pos) with
 difficulty_of_maze() and complexity_of_maze(), computed by libmazerl's native restatement
 (mz_maze_complexity: the turn-decomposed graph, hallways and branches in networkx's insertion /
-adjacency order) instead of networkx. Values: bit-exact or within 1 ulp of the reference on the
-golden mazes (tests/test_difficulty.py, tests/test_metrics.py)."""
+adjacency order, each hallway summed in its CPython set order) instead of networkx. Values:
+bit-exact (==) with the reference's on every golden maze (tests/test_difficulty.py)."""
 import ctypes as C
 
 import numpy as np

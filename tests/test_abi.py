@@ -46,3 +46,27 @@ def test_header_compiles_as_c():
                         "-I", os.path.join(ROOT, "include")], input=src, text=True,
                        capture_output=True)
     assert r.returncode == 0, r.stderr
+
+
+def test_difficulty_lds_limits_match_the_header():
+    """mz_difficulty_batch's pitch limits as include/mazerl.h states them (odd pitches P > 91,
+    toroidal P > 89), derived from the kernel's own LDS plan (the host function
+    mz_mcclendon_lds(P, toroidal, &MM) in libmazerl.so; 160 KB of LDS per workgroup)."""
+    from mazerl import _build
+    L = ctypes.CDLL(_build.build())
+    plan = L._Z16mz_mcclendon_ldsibPi
+    plan.restype = ctypes.c_size_t
+    plan.argtypes = [ctypes.c_int, ctypes.c_bool, ctypes.POINTER(ctypes.c_int)]
+    mm = ctypes.c_int()
+
+    def largest_fit(tor):
+        fit = [P for P in range(5, 200, 2) if plan(P, tor, ctypes.byref(mm)) <= 160 * 1024]
+        # monotone: every pitch up to the largest fitting one fits
+        assert fit == list(range(5, fit[-1] + 1, 2))
+        return fit[-1]
+
+    txt = open(HEADER).read()
+    m = re.search(r"odd pitches: P > (\d+); toroidal P > (\d+)", txt)
+    assert m, "the header states the limits"
+    assert largest_fit(False) == int(m.group(1))
+    assert largest_fit(True) == int(m.group(2))

@@ -122,3 +122,48 @@ def test_ppo_pool_update_two_ranks_agree_on_rows_and_weights():
     assert r0.pop("kept") == r1.pop("kept") == 40 - 7  # the smaller kept count on both ranks
     for k in r0:
         assert torch.equal(r0[k], r1[k]), k  # same schedule, same averaged gradients
+
+
+def _shard_worker(rank, world, port, outdir):
+    """GradAllReduce's sharded step on CPU (gloo): the in-place reduce-scatter leaves rank r's
+    shard of the flat gradient buffer = the ranks' sum (what the all-reduce gives there); an
+    elementwise step on that shard followed by the in-place all-gather leaves every rank with the
+    step the all-reduce path computes over the whole buffer."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from mazerl.agents.flat import FLAT_ALIGN
+    from mazerl.distributed import GradAllReduce, init_from_env
+    init_from_env("gloo")
+    n = 3 * FLAT_ALIGN  # a flat buffer as flatten_params lays it out (multiple of FLAT_ALIGN)
+    g = torch.Generator().manual_seed(40 + rank)
+    grads = torch.randn(n, generator=g)
+    params0 = torch.randn(n, generator=torch.Generator().manual_seed(7))  # replicas agree
+    net = type("Net", (), {})()
+    net._flat_grads, net._flat_params = grads.clone(), params0.clone()
+    ar = GradAllReduce(shard=True)
+    ar.sharded, ar._S, ar._flat = True, n // world, net._flat_grads  # (attach needs FlatAdamW)
+    ar.reduce()
+    S = n // world
+    sl = slice(rank * S, (rank + 1) * S)
+    step = lambda p, gr: p - 0.1 * torch.clamp(gr / world, -1, 1)  # noqa: E731 (elementwise)
+    net._flat_params[sl] = step(net._flat_params[sl], net._flat_grads[sl])
+    ar.gather(net)
+    full = grads.clone()  # the all-reduce path
+    dist.all_reduce(full)
+    torch.save({"sharded": net._flat_params.clone(), "allreduce": step(params0, full),
+                "shard_sum": net._flat_grads[sl].clone(), "full_sum": full[sl].clone()},
+               os.path.join(outdir, f"s{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_step_equals_allreduce_step(world):
+    torch.set_num_threads(1)
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_shard_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        rs = [torch.load(os.path.join(d, f"s{k}.pt"), weights_only=True) for k in range(world)]
+    for r in rs:
+        assert torch.equal(r["shard_sum"], r["full_sum"])
+        assert torch.equal(r["sharded"], r["allreduce"])
+        assert torch.equal(r["sharded"], rs[0]["sharded"])

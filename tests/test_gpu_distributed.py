@@ -25,7 +25,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, outdir, overlap, backend="gloo"):
+def _worker(rank, world, port, outdir, overlap, backend="gloo", shard=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK="0")
     import torch.distributed as dist
@@ -44,9 +44,13 @@ def _worker(rank, world, port, outdir, overlap, backend="gloo"):
     mk = lambda g, ov: VectorDQNLearner(4, "cuda", variant="ddqn", batch_size=32, capacity=64,  # noqa: E731
                                         updates_per_step=1, target_every=4, updates_per_epoch=2,
                                         seed=5 + rank, use_graph=g, overlap=ov,
-                                        allreduce=GradAllReduce())
+                                        allreduce=GradAllReduce(shard=shard))
     A, B = mk(True, overlap), mk(False, False)
     assert A.use_graph and not B.use_graph
+    # the graph learner's step: reduce-scatter + AdamW over this rank's shard + all-gather
+    # (distributed.GradAllReduce.attach), unless shard=False (the flat-bucket all-reduce)
+    assert A.allreduce.sharded == (shard is not False and (world > 1 or shard is True))
+    assert not B.allreduce.sharded  # torch's AdamW: the all-reduce path
     broadcast_params(A.source)  # rank 1 started from other weights (seed 5 + rank)
     A.target.load_state_dict(A.source.state_dict())
     B.source.load_state_dict(A.source.state_dict())
@@ -75,10 +79,11 @@ def _worker(rank, world, port, outdir, overlap, backend="gloo"):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("shard", [None, False], ids=["sharded", "allreduce"])
 @pytest.mark.parametrize("overlap", [False, True], ids=["sequential", "overlapped"])
-def test_graph_allreduce_update_tracks_eager_two_ranks(overlap):
+def test_graph_allreduce_update_tracks_eager_two_ranks(overlap, shard):
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(2, _free_port(), d, overlap), nprocs=2, join=True)
+        mp.spawn(_worker, args=(2, _free_port(), d, overlap, "gloo", shard), nprocs=2, join=True)
         r = [torch.load(os.path.join(d, f"r{k}.pt"), weights_only=True) for k in range(2)]
     for k in range(2):
         for la, lb in r[k]["losses"]:
@@ -93,15 +98,17 @@ def test_graph_allreduce_update_tracks_eager_two_ranks(overlap):
     assert r[0]["losses"][0][0] != r[1]["losses"][0][0]
 
 
+@pytest.mark.parametrize("shard", [True, False], ids=["sharded", "allreduce"])
 @pytest.mark.parametrize("overlap", [False, True], ids=["sequential", "overlapped"])
-def test_graph_allreduce_update_over_rccl_one_rank(overlap):
+def test_graph_allreduce_update_over_rccl_one_rank(overlap, shard):
     """The same learner path with the all-reduce over RCCL ("nccl" backend, RCCL 2.26 on ROCm):
     a gpurun box has one GPU and RCCL refuses two ranks on one device ("Duplicate GPU detected",
     profiles/r03z_rccl_probe.txt), so this runs one rank — the RCCL communicator bound to cuda:0,
     the flat-bucket all-reduce issued between the two captured graphs (and, overlapped, on the
-    side stream) — and checks it against the eager update as above."""
+    side stream; sharded: the reduce-scatter and all-gather around the shard's AdamW, here over
+    one shard) — and checks it against the eager update as above."""
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(1, _free_port(), d, overlap, "nccl"), nprocs=1, join=True)
+        mp.spawn(_worker, args=(1, _free_port(), d, overlap, "nccl", shard), nprocs=1, join=True)
         r = torch.load(os.path.join(d, "r0.pt"), weights_only=True)
     for la, lb in r["losses"]:
         assert la == pytest.approx(lb, rel=1e-4, abs=1e-7)
