@@ -508,6 +508,33 @@ int mz_q_loss(const float* q_dev, int32_t ldq, const float* q_next_dev, int32_t 
 int mz_q_loss_backward(const float* grad_dev, const float* diff_dev, const int64_t* action_dev,
                        int32_t b, int32_t rows, float* dq_dev, void* stream);
 
+/* The Q head and the loss of optimize_model in one launch, from the second hidden layer's
+ * pre-activation rows z2 (f32, row stride lds / ldt floats, `hidden` columns, a multiple of 4) of
+ * the source and the target net: h = act(z2) (act 0: LeakyReLU(0.01), DQN; 1: ReLU, DDQN),
+ * q = W3 h + b3 (fc3: W3 [4][hidden], b3 [4]); with `stacked` the source rows are DDQN's [s; s']
+ * (2b rows: V(s') = q_t[argmax q_s(s')], first maximum), else b rows and V(s') = max q_t; then
+ * diff_dev / *loss_dev exactly as mz_q_loss (dqn_agent.py:129-147, ddqn_agent.py:121-143).
+ * part_dev: mz_head_loss_workspace_floats(b) floats; ticket_dev: a zeroed uint32 the launch
+ * leaves zero (one per concurrently running call). Replaces the activation, fc3 and loss launches
+ * of both nets. */
+int mz_head_loss_workspace_floats(int32_t b);
+int mz_head_loss(const float* z2s_dev, int32_t lds, const float* w3s_dev, const float* b3s_dev,
+                 const float* z2t_dev, int32_t ldt, const float* w3t_dev, const float* b3t_dev,
+                 int32_t hidden, int32_t act, int32_t stacked, const int64_t* action_dev,
+                 const float* reward_dev, double gamma, int32_t b, float* part_dev,
+                 uint32_t* ticket_dev, float* loss_dev, float* diff_dev, void* stream);
+
+/* Its backward through fc3 and the activation for the source rows i < b: dz2_dev[i][j] =
+ * act'(z2[i][j]) * g_i W3[a_i][j], g_i = diff[i] * (2 / b) * (*grad_dev) (rows >= b untouched),
+ * and per block of rows the partial sums of dW3 (row-major [4][hidden]) and db3 [4] into part_dev
+ * ([blocks][4 hidden + 4], mz_head_loss_backward_workspace_floats floats): their column sums
+ * (mz_colsum_f32 over blocks rows of 4 hidden + 4) are fc3's weight and bias gradients. */
+int mz_head_loss_backward_workspace_floats(int32_t b, int32_t hidden);
+int mz_head_loss_backward(const float* grad_dev, const float* diff_dev, const int64_t* action_dev,
+                          int32_t b, const float* z2s_dev, int32_t lds, const float* w3s_dev,
+                          int32_t hidden, int32_t act, float* dz2_dev, int32_t ldd,
+                          float* part_dev, void* stream);
+
 /* PPO's optimizer step (ppo_agent.py:232-236, optimize_model): clip_grad_norm_(params, max_norm)
  * (coef = min(max_norm / (||g||_2 + 1e-6), 1) over every gradient, the gradients scaled in place;
  * max_norm <= 0: no clipping), then AdamW (torch's defaults: betas, eps, weight_decay given) with

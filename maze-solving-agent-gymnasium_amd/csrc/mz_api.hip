@@ -1124,6 +1124,44 @@ int mz_q_loss_backward(const float* grad_dev, const float* diff_dev, const int64
   return MZ_OK;
 }
 
+int mz_head_loss_workspace_floats(int32_t b) {
+  return b <= 0 ? 0 : mz_head_loss_blocks(b);
+}
+
+int mz_head_loss(const float* z2s_dev, int32_t lds, const float* w3s_dev, const float* b3s_dev,
+                 const float* z2t_dev, int32_t ldt, const float* w3t_dev, const float* b3t_dev,
+                 int32_t hidden, int32_t act, int32_t stacked, const int64_t* action_dev,
+                 const float* reward_dev, double gamma, int32_t b, float* part_dev,
+                 uint32_t* ticket_dev, float* loss_dev, float* diff_dev, void* stream) {
+  if (b <= 0 || hidden <= 0 || hidden % 4 || (act != 0 && act != 1) || !z2s_dev || !w3s_dev ||
+      !b3s_dev || !z2t_dev || !w3t_dev || !b3t_dev || !action_dev || !reward_dev || !part_dev ||
+      !ticket_dev || !loss_dev || !diff_dev || lds < hidden || ldt < hidden)
+    return fail(MZ_EINVAL, "bad arguments");
+  MzHeadLoss p{z2s_dev, w3s_dev, b3s_dev, z2t_dev, w3t_dev, b3t_dev, lds, ldt, stacked ? 1 : 0, b,
+               hidden, act, action_dev, reward_dev, (float)gamma, part_dev, ticket_dev, loss_dev,
+               diff_dev};
+  MZ_HIP(mz_launch_head_loss(p, static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
+int mz_head_loss_backward_workspace_floats(int32_t b, int32_t hidden) {
+  return b <= 0 ? 0 : mz_head_loss_bwd_blocks(b) * (4 * hidden + 4);
+}
+
+int mz_head_loss_backward(const float* grad_dev, const float* diff_dev, const int64_t* action_dev,
+                          int32_t b, const float* z2s_dev, int32_t lds, const float* w3s_dev,
+                          int32_t hidden, int32_t act, float* dz2_dev, int32_t ldd,
+                          float* part_dev, void* stream) {
+  if (b <= 0 || hidden <= 0 || hidden % 4 || (act != 0 && act != 1) || !grad_dev || !diff_dev ||
+      !action_dev || !z2s_dev || !w3s_dev || !dz2_dev || !part_dev || lds < hidden || ldd < hidden)
+    return fail(MZ_EINVAL, "bad arguments");
+  const float norm = (float)(2.0 / (double)b);  // mse_loss backward: 2 / numel
+  MZ_HIP(mz_launch_head_loss_bwd(grad_dev, diff_dev, action_dev, b, norm, z2s_dev, lds, w3s_dev,
+                                 hidden, act, dz2_dev, ldd, part_dev,
+                                 static_cast<hipStream_t>(stream)));
+  return MZ_OK;
+}
+
 int mz_adamw_groups(float* param_dev, float* exp_avg_dev, float* exp_avg_sq_dev,
                     const float* const* grads_dev, const int64_t* seg_len,
                     const int32_t* seg_group, int32_t nseg, const float* lr_dev, float* step_dev,

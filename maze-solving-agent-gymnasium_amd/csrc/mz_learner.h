@@ -59,6 +59,23 @@ hipError_t mz_launch_q_loss(const float* q, int ldq, const float* qn, int ldn, c
                             float* loss, float* diff, hipStream_t s);
 hipError_t mz_launch_q_loss_bwd(const float* g, const float* diff, const int64_t* action, int b,
                                 int rows, float norm, float* dq, hipStream_t s);
+// the Q head (act(z2) -> fc3) of the source's and the target's rows + the loss (mz_trainer.hip)
+struct MzHeadLoss {
+  const float *z2s, *w3s, *b3s, *z2t, *w3t, *b3t;
+  int lds, ldt, dbl, b, H, act;
+  const int64_t* action;
+  const float* reward;
+  float gamma;
+  float* part;      // [mz_head_loss_blocks(b)]
+  unsigned* ticket; // zero; the launch leaves it zero
+  float *loss, *diff;
+};
+int mz_head_loss_blocks(int b);
+int mz_head_loss_bwd_blocks(int b);
+hipError_t mz_launch_head_loss(const MzHeadLoss& p, hipStream_t s);
+hipError_t mz_launch_head_loss_bwd(const float* g, const float* diff, const int64_t* action, int b,
+                                   float norm, const float* z2s, int lds, const float* w3s, int H,
+                                   int act, float* dz2, int ldd, float* part, hipStream_t s);
 hipError_t mz_launch_adamw_groups(float* p, float* m, float* v, const float* const* grads,
                                   const int64_t* seg_len, const int32_t* seg_group, int nseg,
                                   const float* lr, float* step, double b1, double b2, double eps,

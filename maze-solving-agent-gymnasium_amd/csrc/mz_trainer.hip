@@ -239,6 +239,149 @@ __global__ void k_q_loss_bwd(const float* __restrict__ g, const float* __restric
   dq[t] = v;
 }
 
+// ---- the Q head + loss as one launch forward, one (+ a column sum) backward -------------------
+// Per update the learner's heads did: the second hidden layer's activation, fc3 (a GEMM with 4
+// outputs), for the source's stacked [s; s'] rows and the target's s' rows, then the loss; and
+// backward the loss gradient, fc3's dX and dW GEMMs and bias column sum, the activation's
+// backward — 10 launches of little work each (config 4's 512-row updates are a chain of such
+// launches). Here, from the pre-activation z2 = fc2(...) of both nets:
+//   k_head_loss       one wave per row i < b: h = act(z2), q_s(i) = W3 h + b3 (4 dot products of
+//                     H), DDQN's q_s(b + i) -> first argmax, the target's q_t(i), the TD error
+//                     diff_i (k_q_loss_fwd's f32 ops and NaN rules), the loss = sum diff^2 / b
+//                     summed per workgroup and then over workgroups in order by the last one (a
+//                     ticket it resets): deterministic;
+//   k_head_loss_bwd   g_i = diff_i * (2 / b) * grad (k_q_loss_bwd's order); dz2[i][j] =
+//                     act'(z2[i][j]) * (g_i W3[a_i][j]) — dq has one nonzero per row, so this IS
+//                     fc3's dX GEMM value (the other terms are exact zeros) — for i < b; the
+//                     per-block partials of dW3[k][j] = sum_i [a_i = k] g_i act(z2[i][j]) and of
+//                     db3[k] = sum_i [a_i = k] g_i, summed over blocks in order by mz_colsum_f32.
+// act: 0 = LeakyReLU(0.01) (DQN), 1 = ReLU (DDQN); torch's forward / backward rules at 0 and NaN.
+constexpr int HL_T = 256;  // 4 waves, 4 rows per workgroup (forward)
+constexpr int HB_RB = 16;  // rows per workgroup (backward)
+constexpr int HB_T = 256;
+
+template <int ACT>
+__device__ inline float head_act(float z) {
+  if (ACT == 0) return z > 0.0f ? z : __fmul_rn(z, 0.01f);
+  return z > 0.0f ? z : (isnan(z) ? z : 0.0f);  // clamp_min(z, 0): NaN propagates
+}
+template <int ACT>
+__device__ inline float head_act_grad(float z, float g) {
+  if (ACT == 0) return z > 0.0f ? g : __fmul_rn(g, 0.01f);  // leaky_relu_backward(grad, self)
+  return (z > 0.0f || isnan(z)) ? g : 0.0f;                  // threshold_backward(grad, out, 0)
+}
+
+__device__ inline float wave_sum_f(float x) {
+  for (int o = W / 2; o; o >>= 1) x = __fadd_rn(x, __shfl_xor(x, o));
+  return x;
+}
+
+template <int ACT>
+__global__ __launch_bounds__(HL_T) void k_head_loss(
+    const float* __restrict__ z2s, int lds, const float* __restrict__ w3s,
+    const float* __restrict__ b3s, const float* __restrict__ z2t, int ldt,
+    const float* __restrict__ w3t, const float* __restrict__ b3t, int dbl,
+    const int64_t* __restrict__ action, const float* __restrict__ reward, float gamma, int b, int H,
+    float* __restrict__ part, unsigned* ticket, float* __restrict__ loss, float* __restrict__ diff) {
+  __shared__ float wpart[HL_T / W];
+  __shared__ bool last;
+  const int lane = threadIdx.x & (W - 1), w = threadIdx.x / W;
+  const int i = blockIdx.x * (HL_T / W) + w;
+  float d2 = 0.0f;
+  if (i < b) {
+    float as[4] = {0.f, 0.f, 0.f, 0.f}, an[4] = {0.f, 0.f, 0.f, 0.f}, at[4] = {0.f, 0.f, 0.f, 0.f};
+    const float* rs = z2s + (size_t)i * lds;
+    const float* rn = z2s + (size_t)(b + i) * lds;
+    const float* rt = z2t + (size_t)i * ldt;
+    for (int j = lane; j < H; j += W) {
+      const float hs = head_act<ACT>(rs[j]), ht = head_act<ACT>(rt[j]);
+      const float hn = dbl ? head_act<ACT>(rn[j]) : 0.0f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        as[k] = __fmaf_rn(hs, w3s[k * H + j], as[k]);
+        at[k] = __fmaf_rn(ht, w3t[k * H + j], at[k]);
+        if (dbl) an[k] = __fmaf_rn(hn, w3s[k * H + j], an[k]);
+      }
+    }
+    float qs[4], qn[4], qt[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      qs[k] = __fadd_rn(wave_sum_f(as[k]), b3s[k]);
+      qt[k] = __fadd_rn(wave_sum_f(at[k]), b3t[k]);
+      qn[k] = dbl ? __fadd_rn(wave_sum_f(an[k]), b3s[k]) : 0.0f;
+    }
+    float v;
+    if (dbl) {  // argmax over q_s(s') (first maximum; the first NaN wins, as torch.argmax)
+      int best = 0;
+      for (int k = 1; k < 4; ++k)
+        if (!isnan(qn[best]) && (isnan(qn[k]) || qn[k] > qn[best])) best = k;
+      v = qt[best];
+    } else {  // max(1)[0] of the target's row (any NaN propagates)
+      v = qt[0];
+      for (int k = 1; k < 4; ++k)
+        if (!isnan(v) && (isnan(qt[k]) || qt[k] > v)) v = qt[k];
+    }
+    const float expected = __fadd_rn(__fmul_rn(v, gamma), reward[i]);
+    const float d = __fsub_rn(qs[(int)action[i]], expected);
+    if (lane == 0) diff[i] = d;
+    d2 = __fmul_rn(d, d);
+  }
+  if (lane == 0) wpart[w] = d2;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.0f;
+    for (int k = 0; k < HL_T / W; ++k) s = __fadd_rn(s, wpart[k]);
+    part[blockIdx.x] = s;
+    __threadfence();
+    last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (last && threadIdx.x == 0) {  // every other workgroup's partial is visible
+    __threadfence();
+    const volatile float* vp = part;
+    float s = 0.0f;
+    for (unsigned k = 0; k < gridDim.x; ++k) s = __fadd_rn(s, vp[k]);
+    *loss = __fdiv_rn(s, (float)b);
+    *ticket = 0u;
+  }
+}
+
+template <int ACT>
+__global__ __launch_bounds__(HB_T) void k_head_loss_bwd(
+    const float* __restrict__ g, const float* __restrict__ diff, const int64_t* __restrict__ action,
+    int b, float norm, const float* __restrict__ z2s, int lds, const float* __restrict__ w3s, int H,
+    float* __restrict__ dz2, int ldd, float* __restrict__ part) {
+  // part: [gridDim.x][4 H + 4] — this block's dW3 (row-major [4][H]) and db3 partials
+  const int r0 = blockIdx.x * HB_RB, r1 = min(b, r0 + HB_RB);
+  const float gg = *g;
+  float* pw = part + (size_t)blockIdx.x * (4 * H + 4);
+  for (int j = threadIdx.x; j < H; j += HB_T) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    for (int i = r0; i < r1; ++i) {
+      const int a = (int)action[i];
+      const float s = __fmul_rn(__fmul_rn(diff[i], norm), gg);
+      const float z = z2s[(size_t)i * lds + j];
+      dz2[(size_t)i * ldd + j] = head_act_grad<ACT>(z, __fmul_rn(s, w3s[a * H + j]));
+      const float t = __fmul_rn(s, head_act<ACT>(z));
+      a0 = a == 0 ? __fadd_rn(a0, t) : a0;
+      a1 = a == 1 ? __fadd_rn(a1, t) : a1;
+      a2 = a == 2 ? __fadd_rn(a2, t) : a2;
+      a3 = a == 3 ? __fadd_rn(a3, t) : a3;
+    }
+    pw[j] = a0;
+    pw[H + j] = a1;
+    pw[2 * H + j] = a2;
+    pw[3 * H + j] = a3;
+  }
+  if (threadIdx.x < 4) {
+    float sb = 0.0f;
+    for (int i = r0; i < r1; ++i)
+      if ((int)action[i] == (int)threadIdx.x)
+        sb = __fadd_rn(sb, __fmul_rn(__fmul_rn(diff[i], norm), gg));
+    pw[4 * H + threadIdx.x] = sb;
+  }
+}
+
 }  // namespace
 
 hipError_t mz_launch_q_loss(const float* q, int ldq, const float* qn, int ldn, const float* qt,
@@ -253,6 +396,37 @@ hipError_t mz_launch_q_loss_bwd(const float* g, const float* diff, const int64_t
                                 int rows, float norm, float* dq, hipStream_t s) {
   hipLaunchKernelGGL(k_q_loss_bwd, dim3((rows * 4 + 255) / 256), dim3(256), 0, s, g, diff, action,
                      b, rows, norm, dq);
+  return hipGetLastError();
+}
+
+hipError_t mz_launch_head_loss(const MzHeadLoss& p, hipStream_t s) {
+  if (p.b <= 0 || p.H <= 0 || p.H % 4) return hipErrorInvalidValue;
+  const int blocks = (p.b + HL_T / W - 1) / (HL_T / W);
+  if (p.act == 0)
+    hipLaunchKernelGGL(k_head_loss<0>, dim3(blocks), dim3(HL_T), 0, s, p.z2s, p.lds, p.w3s, p.b3s,
+                       p.z2t, p.ldt, p.w3t, p.b3t, p.dbl, p.action, p.reward, p.gamma, p.b, p.H,
+                       p.part, p.ticket, p.loss, p.diff);
+  else
+    hipLaunchKernelGGL(k_head_loss<1>, dim3(blocks), dim3(HL_T), 0, s, p.z2s, p.lds, p.w3s, p.b3s,
+                       p.z2t, p.ldt, p.w3t, p.b3t, p.dbl, p.action, p.reward, p.gamma, p.b, p.H,
+                       p.part, p.ticket, p.loss, p.diff);
+  return hipGetLastError();
+}
+
+int mz_head_loss_blocks(int b) { return (b + HL_T / W - 1) / (HL_T / W); }
+int mz_head_loss_bwd_blocks(int b) { return (b + HB_RB - 1) / HB_RB; }
+
+hipError_t mz_launch_head_loss_bwd(const float* g, const float* diff, const int64_t* action, int b,
+                                   float norm, const float* z2s, int lds, const float* w3s, int H,
+                                   int act, float* dz2, int ldd, float* part, hipStream_t s) {
+  if (b <= 0 || H <= 0 || H % 4) return hipErrorInvalidValue;
+  const int blocks = mz_head_loss_bwd_blocks(b);
+  if (act == 0)
+    hipLaunchKernelGGL(k_head_loss_bwd<0>, dim3(blocks), dim3(HB_T), 0, s, g, diff, action, b, norm,
+                       z2s, lds, w3s, H, dz2, ldd, part);
+  else
+    hipLaunchKernelGGL(k_head_loss_bwd<1>, dim3(blocks), dim3(HB_T), 0, s, g, diff, action, b, norm,
+                       z2s, lds, w3s, H, dz2, ldd, part);
   return hipGetLastError();
 }
 

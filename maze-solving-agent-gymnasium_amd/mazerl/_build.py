@@ -4,7 +4,10 @@ hipcc cross-compiles for gfx950 without a GPU. -ffp-contract=off keeps every dou
 score / max_steps expression rounded like CPython (the kernels also use explicit __d*_rn ops).
 Each source compiles to its own object (in parallel), so a file can carry extra flags:
 mz_qnet.hip (bf16 acting stem, no double / NaN semantics involved) is built with
--ffinite-math-only, which drops the NaN canonicalisation fmaxf puts on every MFMA result.
+-ffinite-math-only, which drops the NaN canonicalisation fmaxf puts on every MFMA result;
+mz_qact.hip with MFMA results in VGPRs (-amdgpu-mfma-vgpr-form): k_qconv's accumulators then need
+no v_accvgpr_read before its VALU epilogue (32 of the 445 VALU instructions of its chunk loop);
+the other acting kernels compile to the same registers either way.
 """
 import os
 import subprocess
@@ -18,7 +21,8 @@ LIB = os.path.join(LIBDIR, "libmazerl.so")
 SOURCES = ["mz_env.hip", "mz_api.hip", "mz_difficulty.hip", "mz_qnet.hip", "mz_metrics.hip",
            "mz_stem.hip", "mz_optim.hip", "mz_trainer.hip", "mz_ppo.hip",
            "mz_qact.hip", "mz_mcclendon.hip"]
-EXTRA_FLAGS = {"mz_qnet.hip": ["-ffinite-math-only"]}
+EXTRA_FLAGS = {"mz_qnet.hip": ["-ffinite-math-only"],
+               "mz_qact.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 BASE_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall"]
 DEPS = SOURCES + ["mz_common.h", "mz_kernels.h", "mz_build.inc.h", "mz_pygen.inc.h",
                   "mz_mcclendon.h", "mz_learner.h"]

@@ -45,7 +45,9 @@ EXPORTS = ["mz_last_error", "mz_device_count", "mz_create", "mz_destroy", "mz_lo
            "mz_pair_surrogate", "mz_leaky_relu_bf16", "mz_colsum_f32",
            "mz_replay_gather", "mz_host_alloc", "mz_host_free", "mz_q_front_rows", "mz_greedy_rows",
            "mz_trainer_tick", "mz_greedy_scatter", "mz_head_bf16", "mz_replay_push",
-           "mz_replay_sample_idx", "mz_q_loss", "mz_q_loss_backward", "mz_adamw_groups",
+           "mz_replay_sample_idx", "mz_q_loss", "mz_q_loss_backward", "mz_head_loss",
+           "mz_head_loss_backward", "mz_head_loss_workspace_floats",
+           "mz_head_loss_backward_workspace_floats", "mz_adamw_groups",
            "mz_ppo_act", "mz_ppo_scan", "mz_ppo_finish", "mz_ppo_head_loss", "mz_qact_prepare", "mz_qact",
            "mz_qact_workspace_floats"]
 
@@ -129,6 +131,12 @@ def load(build_if_missing=True):
     L.mz_q_loss.argtypes = [vp, C.c_int32, vp, C.c_int32, vp, C.c_int32, vp, vp, C.c_double,
                             C.c_int32, vp, vp, vp]
     L.mz_q_loss_backward.argtypes = [vp, vp, vp, C.c_int32, C.c_int32, vp, vp]
+    L.mz_head_loss.argtypes = [vp, C.c_int32, vp, vp, vp, C.c_int32, vp, vp, C.c_int32, C.c_int32,
+                               C.c_int32, vp, vp, C.c_double, C.c_int32, vp, vp, vp, vp, vp]
+    L.mz_head_loss_backward.argtypes = [vp, vp, vp, C.c_int32, vp, C.c_int32, vp, C.c_int32,
+                                        C.c_int32, vp, C.c_int32, vp, vp]
+    L.mz_head_loss_workspace_floats.argtypes = [C.c_int32]
+    L.mz_head_loss_backward_workspace_floats.argtypes = [C.c_int32, C.c_int32]
     L.mz_stem_forward.argtypes = [vp, vp, C.c_int32, vp, vp, C.c_float, vp, C.c_uint32, vp,
                                   C.c_int32, vp, vp]
     L.mz_stem_backward.argtypes = [vp, vp, vp, C.c_int32, C.c_int32, C.c_float, vp, vp, vp, vp]

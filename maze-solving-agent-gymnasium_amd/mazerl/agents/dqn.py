@@ -37,6 +37,9 @@ STACK_ROWS = True  # DDQN on packed windows (GPU): source(s) and source(s') as o
 K_BLOCK = os.environ.get("MZ_K_BLOCK", "0") != "0"
 # GPU: the loss and its gradient w.r.t. the Q rows as two HIP launches (MZ_FUSED_LOSS=0: torch ops)
 FUSED_LOSS = os.environ.get("MZ_FUSED_LOSS", "1") != "0"
+# GPU: both nets' second activation + fc3 + the loss as one launch, its backward through fc3 and
+# the activation as one launch + a column sum (MZ_FUSED_HEAD=0: the Q rows, then FUSED_LOSS)
+FUSED_HEAD = os.environ.get("MZ_FUSED_HEAD", "1") != "0"
 
 
 class _QLossFn(torch.autograd.Function):
@@ -71,6 +74,86 @@ class _QLossFn(torch.autograd.Function):
         return dq, None, None, None, None, None, None
 
 
+class _HeadLossFn(torch.autograd.Function):
+    """mse_loss(Q(s,a), V(s') * gamma + r) from the second hidden layer's pre-activations z2 of
+    the source rows (DDQN: the stacked [s; s'] rows) and of the target's s' rows, through the
+    activation and fc3 (mz_head_loss / mz_head_loss_backward): one launch forward, one launch +
+    one column sum backward — instead of both nets' activation and fc3 launches, the loss, its
+    backward, fc3's two GEMMs and bias sum and the activation's backward. Gradients: z2 rows < b
+    (the rest are left unwritten, the forward_rows contract), fc3's weight and bias (written into
+    their flat gradient segments when the net has them, agents/flat.py)."""
+
+    @staticmethod
+    def forward(ctx, z2s, w3s, b3s, z2t, w3t, b3t, action, reward, gamma, b, act, stacked, ticket):
+        from .. import _native as N
+        L = N.load()
+        dev = z2s.device
+        H = z2s.shape[1]
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        diff = torch.empty(b, dtype=torch.float32, device=dev)
+        part = torch.empty(max(1, L.mz_head_loss_workspace_floats(b)), dtype=torch.float32, device=dev)
+        N.check(L.mz_head_loss(z2s.data_ptr(), z2s.stride(0), w3s.data_ptr(), b3s.data_ptr(),
+                               z2t.data_ptr(), z2t.stride(0), w3t.data_ptr(), b3t.data_ptr(), H,
+                               act, int(stacked), action.data_ptr(), reward.data_ptr(), float(gamma),
+                               b, part.data_ptr(), ticket.data_ptr(), loss.data_ptr(),
+                               diff.data_ptr(), torch.cuda.current_stream(dev).cuda_stream))
+        ctx.save_for_backward(z2s, w3s, diff, action)
+        ctx.b, ctx.act, ctx.H = b, act, H
+        ctx.wp, ctx.bp = w3s, b3s
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        from .. import _native as N
+        from .flat import grad_segment
+        L = N.load()
+        z2s, w3s, diff, action = ctx.saved_tensors
+        dev, b, H = z2s.device, ctx.b, ctx.H
+        st = torch.cuda.current_stream(dev).cuda_stream
+        g = g.contiguous()
+        dz2 = torch.empty(z2s.shape, dtype=torch.float32, device=dev)
+        nblk = L.mz_head_loss_backward_workspace_floats(b, H) // (4 * H + 4)
+        part = torch.empty(nblk, 4 * H + 4, dtype=torch.float32, device=dev)
+        N.check(L.mz_head_loss_backward(g.data_ptr(), diff.data_ptr(), action.data_ptr(), b,
+                                        z2s.data_ptr(), z2s.stride(0), w3s.data_ptr(), H, ctx.act,
+                                        dz2.data_ptr(), dz2.stride(0), part.data_ptr(), st))
+        gw, gb = grad_segment(ctx.wp), grad_segment(ctx.bp)
+        # [dW3 | db3] as one column sum when the two flat segments are adjacent (fc3's bias
+        # follows its weight in the flat layout), else into a fresh row
+        if gw is not None and gb is not None and gb.data_ptr() == gw.data_ptr() + 4 * 4 * H:
+            out = gw.view(-1)
+            N.check(L.mz_colsum_f32(part.data_ptr(), nblk, 4 * H + 4, 4 * H + 4, out.data_ptr(), st))
+        else:
+            row = torch.empty(4 * H + 4, dtype=torch.float32, device=dev)
+            N.check(L.mz_colsum_f32(part.data_ptr(), nblk, 4 * H + 4, 4 * H + 4, row.data_ptr(), st))
+            gw = row[:4 * H].view(4, H) if gw is None else gw.copy_(row[:4 * H].view(4, H))
+            gb = row[4 * H:] if gb is None else gb.copy_(row[4 * H:])
+        ctx.wp = ctx.bp = None
+        return dz2, gw, gb, None, None, None, None, None, None, None, None, None, None
+
+
+_HEAD_TICKETS = {}
+
+
+def _head_ticket(dev):
+    t = _HEAD_TICKETS.get(dev)
+    if t is None:
+        t = _HEAD_TICKETS[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
+    return t
+
+
+def _head_ok(source, target, state, action, reward):
+    from .linear import GraphSafeLinear
+    if not (FUSED_HEAD and FUSED_LOSS and state[1].is_cuda and state[1].dtype == torch.int32
+            and hasattr(source, "trunk") and hasattr(target, "trunk")):
+        return False
+    fc3 = source.fc[4]
+    return (isinstance(fc3, GraphSafeLinear) and fc3.out_features == 4 and fc3.bias is not None
+            and fc3.in_features % 4 == 0 and action.dtype == torch.int64 and action.is_contiguous()
+            and reward.dtype == torch.float32 and reward.is_contiguous()
+            and torch.is_grad_enabled() and fc3.weight.requires_grad)
+
+
 def _fused_ok(q, action, reward, *others):
     return (FUSED_LOSS and q.is_cuda and q.dtype == torch.float32 and q.dim() == 2 and
             q.shape[1] == 4 and q.stride(1) == 1 and action.dtype == torch.int64 and
@@ -97,6 +180,20 @@ def q_loss(source, target, state, action, reward, next_state, gamma, double):
     at twice the rows; the backward reads the first B rows only — the s' rows feed an argmax,
     which the reference computes under no_grad)."""
     q_next = None
+    if (not double or STACK_ROWS) and _head_ok(source, target, state, action, reward):
+        # the trunks (stem -> fc1 -> act -> fc2), then one head + loss launch for both nets
+        act = 1 if source.variant == "ddqn" else 0
+        b = action.shape[0]
+        if double and STACK_ROWS:
+            z2 = source.trunk((_stacked(state[0], next_state[0]),
+                               _stacked(state[1], next_state[1])), b)
+        else:
+            z2 = source.trunk(state)
+        with torch.no_grad():
+            z2t = target.trunk(next_state)
+        f3s, f3t = source.fc[4], target.fc[4]
+        return _HeadLossFn.apply(z2, f3s.weight, f3s.bias, z2t, f3t.weight, f3t.bias, action,
+                                 reward, gamma, b, act, bool(double), _head_ticket(z2.device))
     if double and STACK_ROWS and hasattr(source, "forward_rows") and state[1].is_cuda \
             and state[1].dtype == torch.int32:
         b = action.shape[0]

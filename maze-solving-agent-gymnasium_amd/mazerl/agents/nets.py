@@ -85,6 +85,21 @@ class QNet(nn.Module):
             h = m(h, n_grad) if isinstance(m, GraphSafeLinear) else m(h)
         return h
 
+    def trunk(self, x, n_grad=None):
+        """Packed windows on the GPU: the second hidden layer's pre-activation z2 = fc.2(act(fc.0(
+        stem))) — everything but the last activation and fc.4, which the learner's fused head
+        + loss launch applies (agents/dqn.py _HeadLossFn). `n_grad`: as forward_rows."""
+        s, w = x
+        if not (w.dtype == torch.int32 and w.dim() == 2 and w.is_cuda):
+            raise ValueError("trunk() takes packed windows on the GPU")
+        if n_grad is not None and torch.is_anomaly_enabled():
+            raise RuntimeError("trunk(n_grad) leaves gradient rows >= n_grad unwritten; "
+                               "anomaly mode would read them")
+        h = self._bit_stem(s, w, n_grad)
+        for m in list(self.fc)[:3]:
+            h = m(h, n_grad) if isinstance(m, GraphSafeLinear) else m(h)
+        return h
+
     def _bit_stem(self, s, bits, n_grad=None):
         from .stem import stem_features
         p = 0.0

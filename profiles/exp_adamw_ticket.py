@@ -31,7 +31,11 @@ def main(iters=500):
         opt.step()
     e.record()
     torch.cuda.synchronize()
-    print(json.dumps({"lib": os.path.basename(os.environ.get("MZ_LIB_OVERRIDE", "default")),
+    import hashlib
+    h = hashlib.sha256()
+    for t in (opt.flat, opt.exp_avg, opt.exp_avg_sq):
+        h.update(t.cpu().numpy().tobytes())
+    print(json.dumps({"checksum": h.hexdigest()[:16],"lib": os.path.basename(os.environ.get("MZ_LIB_OVERRIDE", "default")),
                       "params": sum(p.numel() for p in net.parameters()),
                       "us_per_step": s.elapsed_time(e) * 1e3 / iters,
                       "step_count": float(opt.step_t.item())}), flush=True)

@@ -20,8 +20,10 @@ for lib in old new old new; do
   if [ $lib = old ]; then export MZ_LIB_OVERRIDE=profiles/_bin/lib_mc_old.so; else unset MZ_LIB_OVERRIDE; fi
   timeout -k 10 300 python -u profiles/exp_mcclendon_wg.py >> $O/mc_ab.jsonl || exit 1
 done
-for lib in old new; do
-  if [ $lib = old ]; then export MZ_LIB_OVERRIDE=profiles/_bin/lib_qact_old.so; else unset MZ_LIB_OVERRIDE; fi
+# r04 (patch rows 17, LUT), pr20 (rows 20, no LUT, MFMA results in AGPRs), new (+ VGPR form)
+for lib in old pr20 new new pr20; do
+  case $lib in old) export MZ_LIB_OVERRIDE=profiles/_bin/lib_qact_old.so;;
+    pr20) export MZ_LIB_OVERRIDE=profiles/_bin/lib_qact_pr20.so;; *) unset MZ_LIB_OVERRIDE;; esac
   timeout -k 10 200 python -u profiles/exp_qact_checksum.py > $O/qact_checksum_$lib.json || exit 1
   timeout -k 10 200 python -u profiles/exp_qact.py $lib >> $O/qact_timing.jsonl || exit 1
 done
@@ -35,5 +37,10 @@ timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -f csv -d $Q/fetch -o run -- python3 profiles/exp_qact.py prof > $O/fetch.log 2>&1 || exit 1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -f csv -d $Q/write -o run -- python3 profiles/exp_qact.py prof > $O/write.log 2>&1 || exit 1
 python3 profiles/summarize_qact_pmc.py $Q > $O/qact_pmc.json
+for lib in old new old new; do
+  if [ $lib = old ]; then export MZ_LIB_OVERRIDE=profiles/_bin/lib_adamw_old.so; else unset MZ_LIB_OVERRIDE; fi
+  timeout -k 10 120 python -u profiles/exp_adamw_ticket.py >> $O/adamw_ab.jsonl || exit 1
+done
+unset MZ_LIB_OVERRIDE
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --curriculum-steps 0 \
   --config-legs "" --candidates 6 > $O/bench_c6.json 2> $O/bench_c6.err || exit 1
