@@ -884,11 +884,17 @@ __global__ __launch_bounds__(512) void k_qact2(MzQAct q) {
 // 8 (lane / 16) + e] (kernel feature order q * 32 + c, obs6 at 1568, zero pad to 1600); the fc2 image
 // is [chunk 32][wave 8][j][lane][8]. A wave's B fragments for one chunk are then 4 KB contiguous
 // per image: one fully coalesced 1 KB load per 16-column tile instead of 16 rows x 64 B.
-// fc1: one workgroup per half of a 16-row fragment block (output tile, wave, j): its 8 contiguous
-// rows of W1 (50 KB) are read coalesced into LDS, then each thread turns 8 features of one lane of
-// one chunk into a 16-B hi and a 16-B lo store. (A per-element version — W1 gathered at the conv
+// fc1: one workgroup per PREP_ROWS rows of a 16-row fragment block (output tile, wave, j): its
+// contiguous rows of W1 (6.3 KB each) are read coalesced into LDS, then each thread turns 8
+// features of one lane of one chunk into a 16-B hi and a 16-B lo store. (A per-element version — W1 gathered at the conv
 // features' stride of 49 floats, 2-B stores — took 23 us per update inside training.)
-constexpr int PREP_ROWS = 8;
+// PREP_ROWS rows of one 16-row fragment block per workgroup: 4 -> 256 workgroups, one per CU (8
+// rows gave 128 — half the chip idle while the learner's update waits on the images)
+#ifndef MZ_PREP_ROWS
+#define MZ_PREP_ROWS 4
+#endif
+constexpr int PREP_ROWS = MZ_PREP_ROWS;
+static_assert(16 % PREP_ROWS == 0, "rows of a fragment block per workgroup");
 constexpr int PREP_LD = CONV_OUT + 6;  // 1574: W1's row length
 __global__ __launch_bounds__(256) void k_qact_prep1(const float* __restrict__ w1,
                                                     uint16_t* __restrict__ w1h,
@@ -899,10 +905,13 @@ __global__ __launch_bounds__(256) void k_qact_prep1(const float* __restrict__ w1
   for (int i = threadIdx.x; i < PREP_ROWS * PREP_LD / 4; i += 256)
     reinterpret_cast<float4*>(rows)[i] = src[i];
   __syncthreads();
-  const int nt = r0 / NT1, cq = (r0 % NT1) / 64, j = (r0 % 64) / 16, half = (r0 % 16) / 8;
-  for (int p = threadIdx.x; p < NCH * 32; p += 256) {  // (chunk, lane of this half) pairs
-    const int c = p >> 5, lane = ((p >> 3) & 3) * 16 + half * 8 + (p & 7);
-    const float* row = rows + (lane & 7) * PREP_LD;
+  const int nt = r0 / NT1, cq = (r0 % NT1) / 64, j = (r0 % 64) / 16, sub = (r0 % 16) / PREP_ROWS;
+  // (chunk, lane) pairs of this workgroup's rows: lanes whose row in the block (lane % 16) is one
+  // of them, for each of the 4 lane groups (lane / 16: the chunk's 8-feature slice)
+  for (int p = threadIdx.x; p < NCH * 4 * PREP_ROWS; p += 256) {
+    const int c = p / (4 * PREP_ROWS), rr = p % PREP_ROWS;
+    const int lane = ((p / PREP_ROWS) & 3) * 16 + sub * PREP_ROWS + rr;
+    const float* row = rows + rr * PREP_LD;
     uint32_t hi[4], lo[4];
 #pragma unroll
     for (int e = 0; e < 8; e += 2) {

@@ -95,10 +95,13 @@ class WinSchedule:
     def before_reset(self, term):
         """change_algorithm for this vector step's winners (`term`: the step's terminated flags,
         device) — sets the algorithm of their next maze before the reset regenerates it."""
-        if self.rule is None:
-            return
         t = term.bool()
         w = t.to(torch.int32)
+        if self.rule is None:  # growth only: the win counts (summary) still advance
+            if self.growth is not None:
+                self.total_wins += w.sum()
+                self.inst_wins += w
+            return
         dfs, pk = ALGOS["dfs"], ALGOS["prim&kill"]
         if self.rule == "global":
             # global win numbers of this step's winners, in instance order

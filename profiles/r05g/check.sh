@@ -14,7 +14,7 @@ timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method threa
   > $O/tests.log 2>&1 || exit 1
 timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
   tests/test_gpu_distributed.py tests/test_learner.py tests/test_learner_graph.py tests/test_flat_optim.py \
-  tests/test_checkpoint_gpu.py > $O/tests_learner.log 2>&1 || exit 1
+  tests/test_checkpoint_gpu.py tests/test_head_loss.py > $O/tests_learner.log 2>&1 || exit 1
 timeout -k 10 300 python -u profiles/exp_update_collective.py > $O/update_collective.json 2> $O/update_collective.err || exit 1
 for lib in old new old new; do
   if [ $lib = old ]; then export MZ_LIB_OVERRIDE=profiles/_bin/lib_mc_old.so; else unset MZ_LIB_OVERRIDE; fi

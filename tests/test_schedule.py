@@ -84,6 +84,9 @@ def test_growth_rule_sizes_keep_and_retire():
         s.after_reset(t)
     assert s.dim.tolist() == [23, 19, 15] and s.next_dim.tolist() == [0, 23, 19]
     assert not s.retired.any() and not s.all_retired()
+    # growth without a curriculum rule still counts the wins (summary()["total_wins"])
+    assert int(s.total_wins) == 5 and s.inst_wins.tolist() == [4, 1, 0]
+    assert s.summary()["total_wins"] == 5
     env2 = FakeEnv(2, max_dim=23)
     s2 = WinSchedule(env2, None, growth=(15, 23))
     for won in ([1, 1], [1, 0]):
