@@ -163,9 +163,15 @@ __host__ __device__ inline void mz_philox(uint64_t key, uint64_t ctr_hi, uint64_
 struct MzRng {
   uint64_t key, n;
   uint32_t buf[4];
+  // the word by selects, not buf[n & 3]: a dynamic index put buf in scratch memory, and every
+  // draw of a build's serial carve chain then waited on a scratch load
   __device__ inline uint32_t u32() {
-    if ((n & 3) == 0) mz_philox(key, MZ_GEN_STREAM, n >> 2, buf);
-    return buf[(n++) & 3];
+    const uint32_t k = (uint32_t)n & 3u;
+    if (k == 0) mz_philox(key, MZ_GEN_STREAM, n >> 2, buf);
+    ++n;
+    const uint32_t lo = (k & 1u) ? buf[1] : buf[0];
+    const uint32_t hi = (k & 1u) ? buf[3] : buf[2];
+    return (k & 2u) ? hi : lo;
   }
   __device__ inline uint32_t below(uint32_t m) { return (uint32_t)(((uint64_t)u32() * m) >> 32); }
 };

@@ -26,7 +26,10 @@ def main(B=65536):
                 env.generate(algorithm=algo, seed=2, rng=rng)
                 torch.cuda.synchronize()
                 dt = time.perf_counter() - t0
-                print(json.dumps({"grid": dim, "toroidal": tor, "rng": rng, "algo": algo,
+                import hashlib
+                h = hashlib.sha256(env.meta().cpu().numpy().tobytes()).hexdigest()[:12]
+                print(json.dumps({"lib": os.path.basename(os.environ.get("MZ_LIB_OVERRIDE", "default")),
+                                  "meta_hash": h, "grid": dim, "toroidal": tor, "rng": rng, "algo": algo,
                                   "mazes": B, "seconds": round(dt, 4),
                                   "mazes_per_s": round(B / dt)}), flush=True)
         env.close()
