@@ -529,9 +529,12 @@ __device__ inline MzCellLds mz_cell_lds(uint8_t* base, int P, int N) {
   return L;
 }
 
+// Bit-set and passage updates as LDS atomics whose result is unused (ds_or_b32 / ds_and_b32 with
+// no return): the carve is one serial chain per maze, and a read-modify-write made it wait an LDS
+// round trip per update; a wave's LDS operations execute in order, so later reads see them.
 __device__ inline bool cs_bit(const uint32_t* b, int q) { return (b[q >> 5] >> (q & 31)) & 1u; }
-__device__ inline void cs_set(uint32_t* b, int q) { b[q >> 5] |= 1u << (q & 31); }
-__device__ inline void cs_clr(uint32_t* b, int q) { b[q >> 5] &= ~(1u << (q & 31)); }
+__device__ inline void cs_set(uint32_t* b, int q) { atomicOr(&b[q >> 5], 1u << (q & 31)); }
+__device__ inline void cs_clr(uint32_t* b, int q) { atomicAnd(&b[q >> 5], ~(1u << (q & 31))); }
 
 // neighbour cell of q in direction k — 0 up, 1 down, 2 left, 3 right (the generators' order
 // (-2,0),(2,0),(0,-2),(0,2), maze_generation.py:72) — or -1 outside the grid
@@ -542,12 +545,12 @@ __device__ inline int cs_nb(int q, int k, int W) {
   if (k == 2) return c > 0 ? q - 1 : -1;
   return c + 1 < W ? q + 1 : -1;
 }
-// open the passage from q in direction k
+// open the passage from q in direction k (an atomic OR on the byte's 32-bit word: pas is 16-B
+// aligned)
 __device__ inline void cs_link(const MzCellLds& L, int q, int k) {
-  if (k == 0) L.pas[q - L.W] |= 2;
-  else if (k == 1) L.pas[q] |= 2;
-  else if (k == 2) L.pas[q - 1] |= 1;
-  else L.pas[q] |= 1;
+  const int c = k == 0 ? q - L.W : (k == 2 ? q - 1 : q);
+  const uint32_t v = k < 2 ? 2u : 1u;
+  atomicOr(reinterpret_cast<uint32_t*>(L.pas) + (c >> 2), v << (8 * (c & 3)));
 }
 // whether the passage from q in direction k is open (the neighbour exists)
 __device__ inline bool cs_open_dir(const MzCellLds& L, int q, int k) {
@@ -572,22 +575,34 @@ __device__ void mz_cs_rprim(const MzCellLds& L, int s, MzRng& rng) {
     const int i = (int)rng.below((uint32_t)nf);
     const int f = L.list[i];
     L.list[i] = L.list[--nf];
+    // the neighbours' in-maze / frontier words and depths, all loaded before any is used (one
+    // LDS round trip); this step changes only f's bits and depth, and f is none of them
+    int j[4], dp[4];
+    uint32_t w0[4], w1[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      j[k] = cs_nb(f, k, W);
+      const int jj = j[k] >= 0 ? j[k] : f;
+      w0[k] = L.b0[jj >> 5] >> (jj & 31);
+      w1[k] = L.b1[jj >> 5] >> (jj & 31);
+      dp[k] = L.dep[jj];
+    }
     uint64_t nb = 0;  // in-maze neighbours: cell | direction from f << 12
     int cnt = 0;
-    for (int k = 0; k < 4; ++k) {
-      const int j = cs_nb(f, k, W);
-      if (j >= 0 && cs_bit(L.b0, j)) mz_k4_push(nb, cnt, j | (k << 12));
-    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (j[k] >= 0 && (w0[k] & 1u)) mz_k4_push(nb, cnt, j[k] | (k << 12));
     if (cnt) {
-      const int v = mz_k4(nb, (int)rng.below((uint32_t)cnt)), nn = v & 0xFFF;
+      const int v = mz_k4(nb, (int)rng.below((uint32_t)cnt)), kk = v >> 12;
       cs_set(L.b0, f);
-      cs_link(L, f, v >> 12);
-      L.dep[f] = (uint16_t)(L.dep[nn] + 2);
+      cs_link(L, f, kk);
+      const int dn = kk == 0 ? dp[0] : (kk == 1 ? dp[1] : (kk == 2 ? dp[2] : dp[3]));
+      L.dep[f] = (uint16_t)(dn + 2);
+#pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const int j = cs_nb(f, k, W);
-        if (j >= 0 && !cs_bit(L.b0, j) && !cs_bit(L.b1, j)) {
-          L.list[nf++] = (uint16_t)j;
-          cs_set(L.b1, j);
+        if (j[k] >= 0 && !(w0[k] & 1u) && !(w1[k] & 1u)) {
+          L.list[nf++] = (uint16_t)j[k];
+          cs_set(L.b1, j[k]);
         }
       }
     }
@@ -602,22 +617,39 @@ __device__ void mz_cs_dfs(const MzCellLds& L, int s, MzRng& rng) {
   L.list[sp++] = (uint16_t)s;
   cs_set(L.b0, s);
   L.dep[s] = 0;
+  // the stack top and its depth stay in registers while the walk advances (a push makes the new
+  // cell the top at depth + 2); only a backtrack reads them back
+  int top = s, dtop = 0;
   while (sp > 0) {
-    const int top = L.list[sp - 1];
+    int j[4];
+    uint32_t w0[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // left, right, up, down
+      j[k] = cs_nb(top, k == 0 ? 2 : (k == 1 ? 3 : k - 2), W);
+      const int jj = j[k] >= 0 ? j[k] : top;
+      w0[k] = L.b0[jj >> 5] >> (jj & 31);
+    }
     uint64_t cand = 0;
     int cnt = 0;
-    for (int k = 0; k < 4; ++k) {
-      const int j = cs_nb(top, k == 0 ? 2 : (k == 1 ? 3 : k - 2), W);
-      if (j >= 0 && !cs_bit(L.b0, j)) mz_k4_push(cand, cnt, k);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (j[k] >= 0 && !(w0[k] & 1u)) mz_k4_push(cand, cnt, k);
+    if (!cnt) {
+      if (--sp > 0) {
+        top = L.list[sp - 1];
+        dtop = L.dep[top];
+      }
+      continue;
     }
-    if (!cnt) { --sp; continue; }
     const int k = mz_k4(cand, (int)rng.below((uint32_t)cnt));
     const int dir = k == 0 ? 2 : (k == 1 ? 3 : k - 2);
-    const int j = cs_nb(top, dir, W);
+    const int jn = k == 0 ? j[0] : (k == 1 ? j[1] : (k == 2 ? j[2] : j[3]));
     cs_link(L, top, dir);
-    cs_set(L.b0, j);
-    L.dep[j] = (uint16_t)(L.dep[top] + 2);
-    L.list[sp++] = (uint16_t)j;
+    cs_set(L.b0, jn);
+    dtop += 2;
+    L.dep[jn] = (uint16_t)dtop;
+    L.list[sp++] = (uint16_t)jn;
+    top = jn;
   }
 }
 
