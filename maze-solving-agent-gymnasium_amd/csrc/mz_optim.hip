@@ -42,9 +42,6 @@
 #ifndef MZ_ADAMW_TPB
 #define MZ_ADAMW_TPB 512
 #endif
-#ifndef MZ_ADAMW_U
-#define MZ_ADAMW_U 4
-#endif
 
 namespace {
 
@@ -90,55 +87,38 @@ __global__ __launch_bounds__(MZ_ADAMW_TPB) void k_adamw(float* __restrict__ p, f
   const float decay = (float)(1.0 - lr * wd);
   const float w1 = (float)(1.0 - b1), b2f = (float)b2, w2 = (float)(1.0 - b2), eps = (float)eps_d;
   const int64_t n4 = segs.off[segs.n] >> 2;  // every segment length is a multiple of 4
-  // MZ_ADAMW_U float4s per thread and pass, every load issued before any arithmetic: the 256
-  // workgroups the ticket allows then keep ~4x the bytes in flight (one pass covers the
-  // 2.14 M-parameter net) instead of one dependent load / compute / store round per float4
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t q0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q0 < n4; q0 += stride * MZ_ADAMW_U) {
-    float4 g4[MZ_ADAMW_U], p4[MZ_ADAMW_U], m4[MZ_ADAMW_U], v4[MZ_ADAMW_U];
-    float4* gp[MZ_ADAMW_U];
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = q << 2;
+    int k = 0;
+    while (k + 1 < segs.n && e >= segs.off[k + 1]) ++k;
+    float4* gp = reinterpret_cast<float4*>(const_cast<float*>(segs.g[k]) + (e - segs.off[k]));
+    float4 g4 = *gp;
+    float4 p4 = reinterpret_cast<float4*>(p)[q];
+    float4 m4 = reinterpret_cast<float4*>(m)[q];
+    float4 v4 = reinterpret_cast<float4*>(v)[q];
+    float* gs = &g4.x;
+    float* ps = &p4.x;
+    float* ms = &m4.x;
+    float* vs = &v4.x;
 #pragma unroll
-    for (int u = 0; u < MZ_ADAMW_U; ++u) {
-      const int64_t q = q0 + u * stride;
-      gp[u] = nullptr;
-      if (q < n4) {
-        const int64_t e = q << 2;
-        int k = 0;
-        while (k + 1 < segs.n && e >= segs.off[k + 1]) ++k;
-        gp[u] = reinterpret_cast<float4*>(const_cast<float*>(segs.g[k]) + (e - segs.off[k]));
-        g4[u] = *gp[u];
-        p4[u] = reinterpret_cast<float4*>(p)[q];
-        m4[u] = reinterpret_cast<float4*>(m)[q];
-        v4[u] = reinterpret_cast<float4*>(v)[q];
-      }
+    for (int j = 0; j < 4; ++j) {
+      float g = gs[j] * gscale;
+      g = g < -clamp ? -clamp : (g > clamp ? clamp : g);
+      gs[j] = g;
+      float pj = ps[j] * decay;
+      float mj = ms[j] + w1 * (g - ms[j]);
+      float vj = vs[j] * b2f + w2 * (g * g);
+      const float denom = sqrtf(vj) / bc2_sqrt + eps;
+      pj = pj - step_size * (mj / denom);
+      ps[j] = pj;
+      ms[j] = mj;
+      vs[j] = vj;
     }
-#pragma unroll
-    for (int u = 0; u < MZ_ADAMW_U; ++u) {
-      const int64_t q = q0 + u * stride;
-      if (q >= n4) continue;
-      float* gs = &g4[u].x;
-      float* ps = &p4[u].x;
-      float* ms = &m4[u].x;
-      float* vs = &v4[u].x;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float g = gs[j] * gscale;
-        g = g < -clamp ? -clamp : (g > clamp ? clamp : g);
-        gs[j] = g;
-        float pj = ps[j] * decay;
-        float mj = ms[j] + w1 * (g - ms[j]);
-        float vj = vs[j] * b2f + w2 * (g * g);
-        const float denom = sqrtf(vj) / bc2_sqrt + eps;
-        pj = pj - step_size * (mj / denom);
-        ps[j] = pj;
-        ms[j] = mj;
-        vs[j] = vj;
-      }
-      reinterpret_cast<float4*>(p)[q] = p4[u];
-      reinterpret_cast<float4*>(m)[q] = m4[u];
-      reinterpret_cast<float4*>(v)[q] = v4[u];
-      if (write_grad) *gp[u] = g4[u];  // the clamped gradient stays visible, as with clamp_ in place
-    }
+    reinterpret_cast<float4*>(p)[q] = p4;
+    reinterpret_cast<float4*>(m)[q] = m4;
+    reinterpret_cast<float4*>(v)[q] = v4;
+    if (write_grad) *gp = g4;  // the clamped gradient stays visible, as with clamp_ in place
   }
   publish_step(step_dev, ticket, t_next);
 }
