@@ -336,13 +336,20 @@ __global__ __launch_bounds__(HL_T) void k_head_loss(
     last = atomicAdd(ticket, 1u) == gridDim.x - 1;
   }
   __syncthreads();
-  if (last && threadIdx.x == 0) {  // every other workgroup's partial is visible
-    __threadfence();
-    const volatile float* vp = part;
+  if (last) {  // every other workgroup's partial is visible: sum them in a fixed order, all
+    __threadfence();  // threads loading at once (a serial loop waited one round trip per partial)
     float s = 0.0f;
-    for (unsigned k = 0; k < gridDim.x; ++k) s = __fadd_rn(s, vp[k]);
-    *loss = __fdiv_rn(s, (float)b);
-    *ticket = 0u;
+    for (unsigned k = threadIdx.x; k < gridDim.x; k += HL_T)
+      s = __fadd_rn(s, __hip_atomic_load(&part[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    s = wave_sum_f(s);
+    if (lane == 0) wpart[w] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float t = 0.0f;
+      for (int k = 0; k < HL_T / W; ++k) t = __fadd_rn(t, wpart[k]);
+      *loss = __fdiv_rn(t, (float)b);
+      *ticket = 0u;
+    }
   }
 }
 

@@ -570,7 +570,13 @@ class VectorDQNLearner:
                 copy_flat(a, self.source)
                 f.refresh()
         K, b = self.updates_per_step, self.batch_size
-        self._idx = [torch.zeros(K, b, dtype=torch.int64, device=self.device) for _ in range(2)]
+        # the index buffers are allocated once: the K-update graphs read them by address, and a
+        # restart (finish() at the end of every train() call, then the next update) that gave
+        # them new storage left those graphs copying whatever reused the old one — the round-4
+        # K-update graph's irreproducible runs
+        if getattr(self, "_idx", None) is None or tuple(self._idx[0].shape) != (K, b):
+            self._idx = [torch.zeros(K, b, dtype=torch.int64, device=self.device) for _ in range(2)]
+            self._graphK = [None, None]
         self._idx_ev = [None, None]
         self._acting, self._par = 0, 1  # the first update writes the slot greedy() does not read
         self._published.clear()

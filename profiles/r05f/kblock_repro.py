@@ -43,14 +43,19 @@ def main(pkg, steps=2400):
                          greedy_rows=True, acting="x3", seed=1)
     tr = VectorOffPolicyTrainer(env, L, seed=11, curriculum=curriculum)
     tr.train(20)
-    tr.train(int(steps))
+    trail = []  # source-net digest every 100 vector steps: where two runs part
+    for k in range(0, int(steps), 100):
+        tr.train(min(100, int(steps) - k))
+        torch.cuda.synchronize()
+        trail.append(hashlib.sha256(L.source._flat_params.detach().cpu().numpy().tobytes()).hexdigest()[:6])
     torch.cuda.synchronize()
     h = hashlib.sha256()
     for t in (L.source._flat_params, L.target._flat_params, L.opt.exp_avg, L.opt.exp_avg_sq,
               L.steps_done, L.replay.sw[:L.replay.size], L.replay.r[:L.replay.size]):
         h.update(t.detach().cpu().numpy().tobytes())
     print(json.dumps({"pkg": pkg, "k_block": os.environ.get("MZ_K_BLOCK"), "digest": h.hexdigest()[:16],
-                      "wins": int(tr.wins), "episodes": int(tr.episodes), "n_updates": L.n_updates}),
+                      "wins": int(tr.wins), "episodes": int(tr.episodes), "n_updates": L.n_updates,
+                      "trail": trail}),
           flush=True)
     env.close()
 

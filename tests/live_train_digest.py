@@ -2,7 +2,8 @@
 updates of 1,024 per vector step, per-instance curriculum, maze bank) printing one JSON line with
 a digest of everything the run produced: the source / target nets, the optimizer moments, the
 replay rows, steps_done, win / episode counters. tests/test_determinism_gpu.py runs it twice in
-fresh processes and compares the lines. MZ_K_BLOCK selects the K-update graph (agents/dqn.py)."""
+fresh processes and compares the lines. MZ_K_BLOCK selects the K-update graph (agents/dqn.py).
+Training runs as train() calls of 100 vector steps, each ending with the learner's finish()."""
 import hashlib
 import json
 import os
@@ -25,7 +26,10 @@ def main(steps=600, envs=4096, dim=41):
                          eps_decay=400.0, gamma=0.7, batch_size=1024, capacity=1 << 20,
                          updates_per_step=4, target_every=13, overlap=True, seed=1)
     tr = VectorOffPolicyTrainer(env, L, seed=11, curriculum="per-instance")
-    tr.train(int(steps))
+    # in chunks: every train() call ends with learner.finish() and the next one restarts the
+    # overlapped learner (what the K-update graph's index buffers must survive)
+    for k in range(0, int(steps), 100):
+        tr.train(min(100, int(steps) - k))
     torch.cuda.synchronize()
     h = hashlib.sha256()
     parts = {}
@@ -37,7 +41,7 @@ def main(steps=600, envs=4096, dim=41):
         d = hashlib.sha256(t.detach().cpu().numpy().tobytes()).hexdigest()[:16]
         parts[name] = d
         h.update(d.encode())
-    rec = {"k_block": os.environ.get("MZ_K_BLOCK", "1"), "digest": h.hexdigest()[:16],
+    rec = {"digest": h.hexdigest()[:16],
            "parts": parts, "wins": int(tr.wins), "episodes": int(tr.episodes),
            "n_updates": L.n_updates}
     print(json.dumps(rec), flush=True)
