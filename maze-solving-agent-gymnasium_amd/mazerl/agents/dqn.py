@@ -33,8 +33,9 @@ from .nets import QNet
 
 
 STACK_ROWS = True  # DDQN on packed windows (GPU): source(s) and source(s') as one pass
-# the overlapped learner's K updates of a vector step as one graph replay (MZ_K_BLOCK=1; 0: K replays)
-K_BLOCK = os.environ.get("MZ_K_BLOCK", "0") != "0"
+# the overlapped learner's K updates of a vector step as one graph replay (MZ_K_BLOCK=0: K replays;
+# bit-identical results either way, tests/test_determinism_gpu.py)
+K_BLOCK = os.environ.get("MZ_K_BLOCK", "1") != "0"
 # GPU: the loss and its gradient w.r.t. the Q rows as two HIP launches (MZ_FUSED_LOSS=0: torch ops)
 FUSED_LOSS = os.environ.get("MZ_FUSED_LOSS", "1") != "0"
 # GPU: both nets' second activation + fc3 + the loss as one launch, its backward through fc3 and
