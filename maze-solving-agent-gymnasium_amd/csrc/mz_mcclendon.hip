@@ -315,9 +315,8 @@ __device__ inline bool ls_resize(LSet& s, int minused, uint16_t* tmp, const KEY&
   return true;
 }
 template <class KEY>
-__device__ inline int ls_add(LSet& s, int node, uint16_t* tmp, const KEY& key_of) {
+__device__ inline int ls_add_k(LSet& s, int node, uint32_t key, uint16_t* tmp, const KEY& key_of) {
   bool f;
-  const uint32_t key = key_of(node);
   const int j = ls_probe(s, key, node, &f);
   if (f) return 0;
   s.t[j * s.st] = (uint16_t)node;
@@ -327,6 +326,10 @@ __device__ inline int ls_add(LSet& s, int node, uint16_t* tmp, const KEY& key_of
   if (s.fill * 5 >= s.mask * 3 && !ls_resize(s, s.used > 50000 ? s.used * 2 : s.used * 4, tmp, key_of))
     return -1;
   return 1;
+}
+template <class KEY>
+__device__ inline int ls_add(LSet& s, int node, uint16_t* tmp, const KEY& key_of) {
+  return ls_add_k(s, node, key_of(node), tmp, key_of);
 }
 // dst = set(src) (set_merge into an empty set; dst's buffer distinct from src's)
 template <class KEY>
@@ -855,9 +858,22 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
   __syncthreads();
   {
     const int lane = threadIdx.x & (WAVE - 1);
-    auto key_of = [&](int v) -> uint32_t {  // cantor_pairing((r, c)) (:7-20), also its hash
+    // cantor_pairing((r, c)) (:7-20) of every node, also its hash: < 2^16 for N <= 130, one LDS
+    // load per lookup instead of nsq + a division (br is free from here on)
+    uint16_t* nkey = br;
+    for (int v = threadIdx.x; v < M; v += T) {
       const int q = nsq[v], r = q / N, c = q - r * N;
-      return (uint32_t)((r + c) * (r + c + 1) / 2 + c);
+      nkey[v] = (uint16_t)((r + c) * (r + c + 1) / 2 + c);
+    }
+    __syncthreads();
+    auto key_of = [&](int v) -> uint32_t { return nkey[v]; };
+    // a node's neighbours: its 4 adjacency slots in one 8-B load
+    auto nbrs4 = [&](int x, int (&nb)[4]) {
+      const uint2 w = *reinterpret_cast<const uint2*>(adjp + 4 * x);
+      nb[0] = (int)(w.x & 0xFFFFu);
+      nb[1] = (int)(w.x >> 16);
+      nb[2] = (int)(w.y & 0xFFFFu);
+      nb[3] = (int)(w.y >> 16);
     };
     auto wave_sum = [&](int x) {
       for (int k = WAVE / 2; k; k >>= 1) x += __shfl_xor(x, k);
@@ -1034,22 +1050,40 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
       for (int hd = 0; hd < qn && ok; ++hd) {  // _plain_bfs, as in the wave path
         const int x = q[hd];
         const int na = adjn[x];
-        int ord[4], no = 0;
-        for (int k = 0; k < na; ++k) {
-          const int u = adjp[4 * x + k];
-          if (u >= x) continue;
-          int j = no++;
-          while (j > 0 && ord[j - 1] > u) { ord[j] = ord[j - 1]; --j; }
-          ord[j] = u;
+        int nb[4];
+        nbrs4(x, nb);
+        // the neighbours' flags and keys, loaded together (one LDS round trip)
+        uint32_t fk[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int u = k < na ? nb[k] : x;
+          fk[k] = ((uint32_t)nfl[u] << 16) | nkey[u];
         }
-        for (int k = 0; k < na; ++k) {
-          const int u = adjp[4 * x + k];
-          if (u > x) ord[no++] = u;
+        // visiting order: earlier neighbours ascending, then later ones in G's order (sort key:
+        // the node id, or 2^16 + slot; unused slots last), by a 4-element sorting network with
+        // (flags | key) << 16 | node carried along — static indices only (registers)
+        uint32_t sk[4];
+        uint64_t pl[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          sk[k] = k >= na ? 0x20000u : (nb[k] < x ? (uint32_t)nb[k] : 0x10000u + k);
+          pl[k] = ((uint64_t)fk[k] << 16) | (uint32_t)nb[k];
         }
-        for (int k = 0; k < no && ok; ++k) {
-          const int u = ord[k];
-          if (!in_h(u)) continue;
-          const int r = ls_add(S1, u, tT, key_of);
+        auto cx = [&](int a, int b) {
+          const bool sw = sk[b] < sk[a];
+          const uint32_t ta = sk[a], tb = sk[b];
+          const uint64_t pa = pl[a], pb = pl[b];
+          sk[a] = sw ? tb : ta; sk[b] = sw ? ta : tb;
+          pl[a] = sw ? pb : pa; pl[b] = sw ? pa : pb;
+        };
+        cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (k >= na || !ok) continue;
+          const int u = (int)(pl[k] & 0xFFFFu);
+          const uint32_t f = (uint32_t)(pl[k] >> 32) & 0xFFu;
+          if ((f & N_SOL) || (f & 7) == 3) continue;  // in_h(u)
+          const int r = ls_add_k(S1, u, (uint32_t)(pl[k] >> 16) & 0xFFFFu, tT, key_of);
           if (r < 0 || (r == 1 && qn >= nc)) ok = false;
           else if (r == 1) q[qn++] = (uint16_t)u;
         }
@@ -1059,11 +1093,22 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
       for (int j = 0; j <= S2.mask && ok; ++j) {
         if (!((S2.occ >> j) & 1u)) continue;
         const int m = S2.t[j * st];
-        for (int k = 0; k < adjn[m]; ++k) {
-          const int u = adjp[4 * m + k];
-          if (nfl[u] & N_JUNC) {
-            if (ls_add(S1, u, tT, key_of) < 0) ok = false;
-            if (nfl[u] & N_SOL) break;
+        const int na = adjn[m];
+        int nb[4];
+        nbrs4(m, nb);
+        uint32_t fk[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int u = k < na ? nb[k] : m;
+          fk[k] = ((uint32_t)nfl[u] << 16) | nkey[u];
+        }
+        bool stop = false;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t f = fk[k] >> 16;
+          if (k < na && !stop && (f & N_JUNC)) {
+            if (ls_add_k(S1, nb[k], fk[k] & 0xFFFFu, tT, key_of) < 0) ok = false;
+            if (f & N_SOL) stop = true;
           }
         }
       }
@@ -1077,10 +1122,15 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
         for (int j = 0; j <= S1.mask; ++j) {
           if (!((S1.occ >> j) & 1u)) continue;
           const int nn = S1.t[j * st];
-          for (int k = 0; k < adjn[nn]; ++k) {
-            const int u = adjp[4 * nn + k];
-            if (ls_find(S1, key_of(u), u) > j) term(sum, D, nterm, adjd[4 * nn + k]);
-          }
+          const int na = adjn[nn];
+          int nb[4];
+          nbrs4(nn, nb);
+          uint32_t ky[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) ky[k] = nkey[k < na ? nb[k] : nn];
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (k < na && ls_find(S1, ky[k], nb[k]) > j) term(sum, D, nterm, adjd[4 * nn + k]);
         }
       } else {
         int last = -1;
