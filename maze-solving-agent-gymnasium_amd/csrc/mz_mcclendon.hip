@@ -369,6 +369,12 @@ __device__ inline bool ls_merge(LSet& dst, const LSet& src, uint16_t* tmp, const
 
 typedef unsigned __int128 u128;
 
+// phase G: waves that run the lane path (the rest start on the wave queue)
+#ifndef MZ_MC_LANE_WAVES
+#define MZ_MC_LANE_WAVES 12
+#endif
+constexpr int MC_LANE_WAVES = MZ_MC_LANE_WAVES;
+
 __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, int n, int MM,
                                                  double* out, int32_t* status, const int* limit,
                                                  int mult) {
@@ -1196,15 +1202,21 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
       }
     }
     __syncthreads();
-    // G2: the lane queue on the first L threads; every wave, once its lanes are done, takes the
-    // wave queue's hallways one at a time
+    // G2: the lane queue over the first MC_LANE_WAVES waves, item v to lane v / MC_LANE_WAVES of
+    // wave v % MC_LANE_WAVES — a few active lanes per wave, so each LDS instruction of the lane
+    // path's lookup chains serves few random addresses (fewer bank conflicts) and many waves keep
+    // chains in flight; the other waves start on the wave queue at once, and every wave, once its
+    // lanes are done, takes the wave queue's hallways one at a time
     const int nl = s_nl, nw = s_nw;
-    if ((int)threadIdx.x < L) {
-      const int l = threadIdx.x;
-      uint16_t* base = l < Lr ? reinterpret_cast<uint16_t*>(keys) + l
-                              : reinterpret_cast<uint16_t*>(Cb) + (l - Lr);
-      for (int k = l; k < nl; k += L)
-        if (!lane_hallway(Lq[k], base, Lr)) s_bad = 2;
+    const int wid = threadIdx.x / WAVE;
+    if (wid < MC_LANE_WAVES) {
+      const int l = lane * MC_LANE_WAVES + wid;  // virtual lane: its table slot
+      if (l < L) {
+        uint16_t* base = l < Lr ? reinterpret_cast<uint16_t*>(keys) + l
+                                : reinterpret_cast<uint16_t*>(Cb) + (l - Lr);
+        for (int k = l; k < nl; k += L)
+          if (!lane_hallway(Lq[k], base, Lr)) s_bad = 2;
+      }
     }
     for (;;) {
       int k = 0;
