@@ -409,9 +409,19 @@ def config_legs(a, dev, rank=0, world=1):
             L.target.load_state_dict(L.source.state_dict())
         tr = VectorOffPolicyTrainer(env, L, seed=7919 * rank, bank_candidates=C)
         tr.train(20)
+        w0 = tr.inst_wins.clone()
         secs = timed_train(tr, a.cfg4_steps, "config 4 leg")
+        # the training distribution per algorithm: wins in the timed steps
+        dw = (tr.inst_wins - w0).long().cpu()
+        names = ["r-prim", "dfs", "prim&kill"]  # ids: vector_env.ALGOS
+        wins_by = {names[k]: int(dw[algo == k].sum()) for k in range(3)}
+        if world > 1:
+            t = torch.tensor([wins_by[n] for n in names], dtype=torch.int64, device=dev)
+            dist.all_reduce(t)
+            wins_by = dict(zip(names, t.tolist()))
         env.close()
         rec = {"envs_per_gpu": B, "grid": dim, "algo": "mixed (global id mod 3)",
+               "train_wins_by_algorithm": wins_by,
                "vector_steps": a.cfg4_steps, "seconds": round(secs, 3),
                "env_steps_per_s": B * a.cfg4_steps * world / secs, "updates": L.n_updates,
                "batch": 512, "updates_per_vector_step": 4, "training_mazes_candidates": C,

@@ -1229,15 +1229,19 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
   __syncthreads();
   if (s_bad) { fail(2); return; }
   MC_PROBE_AT(7)
-  // hallway 0: the solution branch, edges in path order
+  // hallway 0: the solution branch, edges in path order — the terms 1 / (2 d) by all threads (into
+  // Cb, free until phase H), then one thread adds them left to right (a dfs maze's solution has
+  // ~1,000 nodes: the f64 divisions in that thread's loop were most of phase H)
+  for (int v = 1 + threadIdx.x; v < nsol; v += T)
+    Cb[v] = __ddiv_rn(1.0, __dmul_rn(2.0, (double)gpd[v]));
+  __syncthreads();
   if (threadIdx.x == 0) {
     double s = 0.0;
     long D = 0;
+#pragma unroll 8
     for (int v = 1; v < nsol; ++v) {
-      const int dd = gpd[v];
-      const double t = __ddiv_rn(1.0, __dmul_rn(2.0, (double)dd));
-      s = v == 1 ? t : __dadd_rn(s, t);
-      D += dd;
+      s = v == 1 ? Cb[v] : __dadd_rn(s, Cb[v]);
+      D += gpd[v];
     }
     Ch[0] = __dmul_rn((double)D, s);
   }

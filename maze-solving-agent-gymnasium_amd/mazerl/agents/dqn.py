@@ -433,7 +433,9 @@ class VectorDQNLearner:
         self.overlap = bool(overlap) and self.use_graph and self.fused is not None
         self._async = False
         if self.overlap:
-            self.side = torch.cuda.Stream(self.device)
+            # MZ_LEARNER_PRIORITY: the side stream's priority (default: torch's default, 0)
+            self.side = torch.cuda.Stream(self.device,
+                                          priority=int(os.environ.get("MZ_LEARNER_PRIORITY", "0")))
             # two actor snapshots of the source net (ping-pong) with their own fused heads and
             # dropout streams; the source net itself is only touched on `side`
             from .flat import flatten_params
