@@ -673,17 +673,63 @@ __device__ inline void mz_cs_pk_mark(const MzCellLds& L, int p) {
     if (n >= 0 && cs_bit(L.b0, n) && mz_cs_pk_nbrs(L, n, tmp) == 0) cs_clr(L.b1, n);
   }
 }
+// mz_cs_pk_mark for the walk, from the marked bits of the 5 x 5 cells around p (cells outside the
+// grid read as marked: never an unmarked neighbour), loaded together — one LDS round trip where
+// the mark's neighbour-of-neighbour scans made several dependent ones. Returns p's unmarked
+// neighbours (what the walk's next mz_cs_pk_nbrs(p) would read: the mark changes p's bit only).
+__device__ inline int mz_cs_pk_mark_w(const MzCellLds& L, int p, uint64_t& out) {
+  const int W = L.W, r = p / W, c = p - r * W;
+  uint32_t rows[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const int rr = r - 2 + i;
+    if (rr < 0 || rr >= W) { rows[i] = 0x1Fu; continue; }
+    const int lo = max(c - 2, 0), hi = min(c + 2, W - 1);
+    const int qlo = rr * W + lo, qhi = rr * W + hi;
+    const uint64_t cat = ((uint64_t)L.b0[qhi >> 5] << 32) | L.b0[qlo >> 5];
+    const uint32_t len = (uint32_t)(hi - lo + 1), at = (uint32_t)(lo - (c - 2));
+    const uint32_t v = (uint32_t)(cat >> (qlo & 31)) & ((1u << len) - 1u);
+    rows[i] = (v << at) | (0x1Fu & ~(((1u << len) - 1u) << at));
+  }
+  cs_set(L.b0, p);
+  rows[2] |= 1u << 2;
+  auto mk = [&](int i, int j) -> bool { return (rows[i] >> j) & 1u; };
+  auto free_nbrs = [&](int i, int j) -> int {
+    return (int)!mk(i - 1, j) + (int)!mk(i + 1, j) + (int)!mk(i, j - 1) + (int)!mk(i, j + 1);
+  };
+  int cnt = 0;
+  out = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {  // up, down, left, right
+    const int i = 2 + (k == 0 ? -1 : (k == 1 ? 1 : 0)), j = 2 + (k == 2 ? -1 : (k == 3 ? 1 : 0));
+    if (!mk(i, j)) mz_k4_push(out, cnt, cs_nb(p, k, W) | (k << 12));
+  }
+  if (cnt > 0) cs_set(L.b1, p); else cs_clr(L.b1, p);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int i = 2 + (k == 0 ? -1 : (k == 1 ? 1 : 0)), j = 2 + (k == 2 ? -1 : (k == 3 ? 1 : 0));
+    const int n = cs_nb(p, k, W);
+    if (n >= 0 && mk(i, j) && free_nbrs(i, j) == 0) cs_clr(L.b1, n);
+  }
+  return cnt;
+}
+// the walk: its depth and the unmarked count stay in registers, the next step's neighbour list
+// comes from the mark
 __device__ void mz_cs_pk_walk(const MzCellLds& L, int cur, MzRng& rng) {
   uint64_t nb;
-  int cnt;
-  while ((cnt = mz_cs_pk_nbrs(L, cur, nb)) != 0) {
+  int cnt = mz_cs_pk_nbrs(L, cur, nb);
+  if (!cnt) return;
+  int dcur = L.dep[cur], left = L.sh[1];
+  while (cnt) {
     const int v = mz_k4(nb, (int)rng.below((uint32_t)cnt)), nx = v & 0xFFF;
     cs_link(L, cur, v >> 12);
-    L.dep[nx] = (uint16_t)(L.dep[cur] + 2);
+    dcur += 2;
+    L.dep[nx] = (uint16_t)dcur;
     cur = nx;
-    mz_cs_pk_mark(L, cur);
-    L.sh[1] -= 1;
+    cnt = mz_cs_pk_mark_w(L, cur, nb);
+    --left;
   }
+  L.sh[1] = left;
 }
 __device__ void mz_cs_primkill(const MzCellLds& L, int s, MzRng& rng) {
   const int lane = threadIdx.x, nw = (L.Q + 31) / 32;
