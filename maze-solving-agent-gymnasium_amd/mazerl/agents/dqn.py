@@ -133,13 +133,13 @@ class _HeadLossFn(torch.autograd.Function):
         return dz2, gw, gb, None, None, None, None, None, None, None, None, None, None
 
 
-_HEAD_TICKETS = {}
-
-
-def _head_ticket(dev):
-    t = _HEAD_TICKETS.get(dev)
-    if t is None:
-        t = _HEAD_TICKETS[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
+def _head_ticket(net, dev):
+    """The mz_head_loss ticket of this source net (one per learner: two learners' updates may run
+    at once on their own side streams, and a shared ticket would mix their workgroup counts)."""
+    t = getattr(net, "_head_ticket", None)
+    if t is None or t.device != dev:
+        t = torch.zeros(1, dtype=torch.int32, device=dev)
+        net._head_ticket = t
     return t
 
 
@@ -194,7 +194,7 @@ def q_loss(source, target, state, action, reward, next_state, gamma, double):
             z2t = target.trunk(next_state)
         f3s, f3t = source.fc[4], target.fc[4]
         return _HeadLossFn.apply(z2, f3s.weight, f3s.bias, z2t, f3t.weight, f3t.bias, action,
-                                 reward, gamma, b, act, bool(double), _head_ticket(z2.device))
+                                 reward, gamma, b, act, bool(double), _head_ticket(source, z2.device))
     if double and STACK_ROWS and hasattr(source, "forward_rows") and state[1].is_cuda \
             and state[1].dtype == torch.int32:
         b = action.shape[0]
