@@ -407,7 +407,7 @@ def config_legs(a, dev, rank=0, world=1):
         if world > 1:
             broadcast_params(L.source)
             L.target.load_state_dict(L.source.state_dict())
-        tr = VectorOffPolicyTrainer(env, L, seed=7919 * rank, bank_candidates=C)
+        tr = VectorOffPolicyTrainer(env, L, seed=7919 * rank, bank_candidates=C, track_wins=True)
         tr.train(20)
         w0 = tr.inst_wins.clone()
         secs = timed_train(tr, a.cfg4_steps, "config 4 leg")

@@ -35,8 +35,12 @@ class VectorOffPolicyTrainer:
     bank_candidates: best-of-C maze bank (1 = one Philox maze per slot)."""
 
     def __init__(self, env, learner, seed=0, regen_won=True, curriculum=False, allreduce_stats=None,
-                 bank=True, fused=True, growth=None, algorithm="r-prim", bank_candidates=1):
+                 bank=True, fused=True, growth=None, algorithm="r-prim", bank_candidates=1,
+                 track_wins=False):
         self.env, self.learner = env, learner
+        # inst_wins (per-instance win counts) is kept by the win schedule; track_wins keeps it
+        # without one (one more launch per vector step)
+        self.track_wins = bool(track_wins)
         rule = curriculum_rule(curriculum)
         self.schedule = (WinSchedule(env, rule, growth, learner, algorithm)
                          if (rule is not None or growth is not None) else None)
@@ -110,6 +114,8 @@ class VectorOffPolicyTrainer:
             won = env.terminated.bool()
             self.inst_wins += won.to(torch.int32)
             sch.before_reset(won)
+        elif self.track_wins:
+            self.inst_wins += env.terminated.to(torch.int32)
         if ring:
             rp.push_rest(env.actions, env.reward, env.obs6, env.window_bits)
         else:
