@@ -94,6 +94,73 @@ __device__ void bitonic(uint64_t* a, int S) {
     }
 }
 
+__device__ inline uint64_t shfl_xor64(uint64_t v, int m) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
+  const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
+  return ((uint64_t)hi << 32) | lo;
+}
+// bitonic stages j = jmax .. 1 of merge size k on a wave's 128-element block [b, b + 128), held as
+// x0 = element b + lane, x1 = element b + 64 + lane: j = 64 within the lane, j < 64 by shuffles
+__device__ inline void bitonic_regs(uint64_t& x0, uint64_t& x1, int b, int k, int jmax) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  for (int j = jmax; j > 0; j >>= 1) {
+    if (j == 64) {
+      const bool up = ((b + lane) & k) == 0;
+      const uint64_t lo = x0 < x1 ? x0 : x1, hi = x0 < x1 ? x1 : x0;
+      x0 = up ? lo : hi;
+      x1 = up ? hi : lo;
+      continue;
+    }
+    const uint64_t p0 = shfl_xor64(x0, j), p1 = shfl_xor64(x1, j);
+    const int i0 = b + lane, i1 = b + 64 + lane;
+    const bool u0 = ((i0 & k) == 0) == ((i0 & j) == 0), u1 = ((i1 & k) == 0) == ((i1 & j) == 0);
+    x0 = u0 ? (x0 < p0 ? x0 : p0) : (x0 < p0 ? p0 : x0);
+    x1 = u1 ? (x1 < p1 ? x1 : p1) : (x1 < p1 ? p1 : x1);
+  }
+}
+// the same sort for 256 <= S <= 2 T with far fewer barriers: every stage whose pairs lie inside a
+// 128-element block runs in the wave's registers (shuffles), only the j >= 128 stages go through
+// LDS — ~15 workgroup barriers for S = 2,048 instead of 66
+__device__ void bitonic_waves(uint64_t* a, int S) {
+  const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE, b = w * 128;
+  const bool act = b < S;
+  uint64_t x0 = 0, x1 = 0;
+  if (act) {
+    x0 = a[b + lane];
+    x1 = a[b + 64 + lane];
+    for (int k = 2; k <= 128; k <<= 1) bitonic_regs(x0, x1, b, k, k >> 1);
+    a[b + lane] = x0;
+    a[b + 64 + lane] = x1;
+  }
+  __syncthreads();
+  for (int k = 256; k <= S; k <<= 1) {
+    for (int j = k >> 1; j >= 128; j >>= 1) {
+      for (int p = threadIdx.x; p < S / 2; p += T) {  // pair p: i has bit j clear, l = i + j
+        const int i = (p / j) * 2 * j + (p % j), l = i + j;
+        const bool up = (i & k) == 0;
+        const uint64_t x = a[i], y = a[l];
+        if ((x > y) == up) {
+          a[i] = y;
+          a[l] = x;
+        }
+      }
+      __syncthreads();
+    }
+    if (act) {
+      x0 = a[b + lane];
+      x1 = a[b + 64 + lane];
+      bitonic_regs(x0, x1, b, k, 64);
+      a[b + lane] = x0;
+      a[b + 64 + lane] = x1;
+    }
+    __syncthreads();
+  }
+}
+__device__ inline void sort_keys(uint64_t* a, int S) {
+  if (S >= 256 && S <= 2 * T) bitonic_waves(a, S);
+  else bitonic(a, S);
+}
+
 // exclusive prefix sum of v over the workgroup (one value per thread); *total = the sum
 __device__ inline int block_excl(int v, int* wsum, int* total) {
   const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
@@ -690,7 +757,7 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
   const int S1 = next_pow2(noff > 1 ? noff : 2);
   for (int k = noff + threadIdx.x; k < S1; k += T) keys[k] = ~0ull;
   __syncthreads();
-  bitonic(keys, S1);
+  sort_keys(keys, S1);
   for (int k = threadIdx.x; k < noff; k += T) {
     const int q = (int)(keys[k] & 0x7FFFu);
     pos[q] = (uint16_t)(nsol + k);
@@ -1253,7 +1320,7 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
   for (int k = Hn + threadIdx.x; k < S3; k += T) keys[k] = ~0ull;
   for (int b = threadIdx.x; b < Bn; b += T) pref[b] = NONE;
   __syncthreads();
-  bitonic(keys, S3);
+  sort_keys(keys, S3);
   for (int k = threadIdx.x; k < Hn; k += T) {
     const int b = (int)(keys[k] >> 16);
     if (k == 0 || (int)(keys[k - 1] >> 16) != b) pref[b] = (uint16_t)k;
