@@ -55,7 +55,8 @@ namespace {
 constexpr int T = MZ_MC_T;  // threads per maze workgroup
 // MZ_MC_PROBE = k (timing experiments only, wrong results): the kernel returns after phase k
 // (1 A squares, 2 B solution path, 3 C dead ends / first(), 4 D node order, 5 E edges,
-// 6 F components, 7 G hallway sums)
+// 6 F components, 7 G hallway sums; 71 / 72 after G's member lists / classification, 73 / 74
+// the whole kernel without G's lane path / wave queue)
 #ifndef MZ_MC_PROBE
 #define MZ_MC_PROBE 0
 #endif
@@ -442,7 +443,7 @@ typedef unsigned __int128 u128;
 #endif
 constexpr int MC_LANE_WAVES = MZ_MC_LANE_WAVES;
 
-__global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, int n, int MM,
+__global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, int n, int MM, int MK,
                                                  double* out, int32_t* status, const int* limit,
                                                  int mult) {
   extern __shared__ __align__(16) unsigned char lds[];
@@ -484,8 +485,8 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
   const size_t sq_bytes = tor ? tor_off + (((size_t)NNP * 2 + 15) & ~(size_t)15) : tor_off,
                ph2_bytes = (size_t)MM * 36;
   unsigned char* nb = lds + (sq_bytes > ph2_bytes ? sq_bytes : ph2_bytes);  // node region
-  uint64_t* keys = reinterpret_cast<uint64_t*>(nb);                  // [MM] sort buffer
-  uint16_t* nsq = reinterpret_cast<uint16_t*>(keys + MM);            // [MM] node -> square
+  uint64_t* keys = reinterpret_cast<uint64_t*>(nb);                  // [MK] sort buffer
+  uint16_t* nsq = reinterpret_cast<uint16_t*>(keys + MK);            // [MM] node -> square
   uint16_t* adjp = nsq + MM;                                         // [MM][4] neighbours (pos)
   uint16_t* adjd = adjp + 4 * MM;                                    // [MM][4] edge d
   uint16_t* gpar = adjd + 4 * MM;                                    // [MM] parent node (pos)
@@ -939,6 +940,7 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
       nkey[v] = (uint16_t)((r + c) * (r + c + 1) / 2 + c);
     }
     __syncthreads();
+    MC_PROBE_AT(71)
     auto key_of = [&](int v) -> uint32_t { return nkey[v]; };
     // a node's neighbours: its 4 adjacency slots in one 8-B load
     auto nbrs4 = [&](int x, int (&nb)[4]) {
@@ -1228,8 +1230,9 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
     // <= 15: the lane queue; else the wave queue (both in the phase-F bmin region, free now)
     uint16_t* Lq = reinterpret_cast<uint16_t*>(bmin);
     uint16_t* Wq = Lq + MM;
-    const int Lr = (int)((size_t)MM * 8 / (96 * sizeof(uint16_t)));  // lanes per region
-    const int L = min(2 * Lr, T / 2);
+    const int Lr = (int)((size_t)MK * 8 / (96 * sizeof(uint16_t)));  // lanes in the keys region
+    const int Lc = (int)((size_t)MM * 8 / (96 * sizeof(uint16_t)));  // lanes in the Cb region
+    const int L = min(Lr + Lc, T / 2);
     for (int h = 1 + threadIdx.x; h <= Hn; h += T) {
       const int b0 = (int)hstart[h], nc = (int)hstart[h + 1] - b0;
       int nasp = 0;
@@ -1269,6 +1272,7 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
       }
     }
     __syncthreads();
+    MC_PROBE_AT(72)
     // G2: the lane queue over the first MC_LANE_WAVES waves, item v to lane v / MC_LANE_WAVES of
     // wave v % MC_LANE_WAVES — a few active lanes per wave, so each LDS instruction of the lane
     // path's lookup chains serves few random addresses (fewer bank conflicts) and many waves keep
@@ -1276,20 +1280,21 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
     // lanes are done, takes the wave queue's hallways one at a time
     const int nl = s_nl, nw = s_nw;
     const int wid = threadIdx.x / WAVE;
-    if (wid < MC_LANE_WAVES) {
+    if (wid < MC_LANE_WAVES && MZ_MC_PROBE != 73) {
       const int l = lane * MC_LANE_WAVES + wid;  // virtual lane: its table slot
       if (l < L) {
         uint16_t* base = l < Lr ? reinterpret_cast<uint16_t*>(keys) + l
                                 : reinterpret_cast<uint16_t*>(Cb) + (l - Lr);
+        const int st = l < Lr ? Lr : Lc;
         for (int k = l; k < nl; k += L)
-          if (!lane_hallway(Lq[k], base, Lr)) s_bad = 2;
+          if (!lane_hallway(Lq[k], base, st)) s_bad = 2;
       }
     }
     for (;;) {
       int k = 0;
       if (lane == 0) k = atomicAdd(&s_wq, 1);
       k = __shfl(k, 0);
-      if (k >= nw) break;
+      if (k >= nw || MZ_MC_PROBE == 74) break;
       wave_hallway(Wq[k]);
     }
   }
@@ -1356,13 +1361,17 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
 size_t mz_mcclendon_lds(int P, bool toroidal, int* mm) {
   const int Pb = toroidal ? P + 2 : P;  // a toroidal maze is scored on its bordered grid
   const int cells = ((Pb - 1) / 2) * ((Pb - 1) / 2) + 4;
-  int MM = 16;
-  while (MM < cells) MM <<= 1;
+  // the sort buffer holds a power of two (the bitonic sorts); every other node array the node
+  // count rounded up to 64 (a power of two there left ~20 % of a workgroup's LDS unused, and LDS
+  // is what decides whether the trainer's kernels can share a CU with this one)
+  const int MM = (cells + 63) & ~63;
+  int MK = 16;
+  while (MK < MM) MK <<= 1;
   *mm = MM;
   const size_t NNP = (size_t)Pb * Pb;
   size_t sq = (NNP * 9 + 16 + 15) & ~(size_t)15;
   if (toroidal) sq += (NNP * 2 + 15) & ~(size_t)15;  // the distance field
-  const size_t node = (size_t)MM * (8 + 2 + 8 + 8 + 2 + 2 + 2 + 1 + 1);
+  const size_t node = (size_t)MK * 8 + (size_t)MM * (2 + 8 + 8 + 2 + 2 + 2 + 1 + 1);
   const size_t ph2 = (size_t)MM * (2 * 6 + 4 * 2 + 8 * 2);
   return (sq > ph2 ? sq : ph2) + node;
 }
@@ -1378,7 +1387,9 @@ hipError_t mz_launch_mcclendon(const MzDev& d, const int32_t* ids, int n, double
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(k_mcclendon, dim3(n), dim3(T), bytes, s, d, ids, n, MM, out, status, limit,
+  int MK = 16;
+  while (MK < MM) MK <<= 1;
+  hipLaunchKernelGGL(k_mcclendon, dim3(n), dim3(T), bytes, s, d, ids, n, MM, MK, out, status, limit,
                      mult < 1 ? 1 : mult);
   return hipGetLastError();
 }
