@@ -435,6 +435,80 @@ __device__ inline bool ls_merge(LSet& dst, const LSet& src, uint16_t* tmp, const
   return true;
 }
 
+
+// ---- the lane path's sets from their occupancy masks alone (MZ_MC_LANE2) ---------------------
+// In a tree every insertion of the lane path is of a key not yet in its set (a BFS visits a node
+// once; a junction neighbours one member of a hallway; members and junctions are disjoint), so
+// CPython's set_add_entry / set_insert_clean put it in the first empty slot of its probe
+// sequence — a function of the occupancy mask and the key only, computed in registers. An entry
+// is one word: slot << 25 | key << 11 | node (keys < 2^14 and nodes < 2^11 up to pitch 91, the
+// kernel's LDS limit); a set's iteration order comes from its slots' ranks in the mask
+// (popcount below the slot), by a scatter through LDS.
+#ifndef MZ_MC_LANE2
+#define MZ_MC_LANE2 1
+#endif
+__device__ inline uint32_t lw_key(uint32_t w) { return (w >> 11) & 0x3FFFu; }
+__device__ inline int lw_node(uint32_t w) { return (int)(w & 0x7FFu); }
+__device__ inline int lw_slot(uint32_t w) { return (int)(w >> 25); }
+__device__ inline uint32_t lw_with_slot(uint32_t w, int sl) { return (w & 0x1FFFFFFu) | ((uint32_t)sl << 25); }
+__device__ inline int lw_free(uint32_t occ, uint32_t key, int mask) {
+  uint32_t perturb = key;
+  int i = (int)(key & (uint32_t)mask);
+  for (;;) {
+    if (i + 9 <= mask) {
+      const uint32_t fr = (~occ >> i) & 0x3FFu;
+      if (fr) return i + __builtin_ctz(fr);
+    } else if (!((occ >> i) & 1u)) {
+      return i;
+    }
+    perturb >>= 5;
+    i = (int)(((uint32_t)i * 5u + 1u + perturb) & (uint32_t)mask);
+  }
+}
+// insert_clean / add of a key known to be absent: its slot into the word, the mask updated
+__device__ inline void lw_put(uint32_t& w, uint32_t& occ, int mask) {
+  const int t = lw_free(occ, lw_key(w), mask);
+  occ |= 1u << t;
+  w = lw_with_slot(w, t);
+}
+// a set built by add() from p[0..n) (n <= 15; distinct keys): slots into the words, occupancy,
+// mask. set_add_entry resizes after the insertion that makes fill * 5 >= mask * 3: the 5th of an
+// 8-slot table (to 32 = the smallest power of two above 4 * 5, re-inserting in slot order); a
+// 32-slot table would resize at the 19th
+__device__ inline void lw_layout_add(uint32_t (&p)[16], int n, uint32_t& occ, int& mask) {
+  occ = 0u;
+  mask = 7;
+#pragma unroll
+  for (int i = 0; i < 5; ++i)
+    if (i < n) lw_put(p[i], occ, 7);
+  if (n < 5) return;
+  int rk[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) rk[i] = __popc(occ & ((1u << lw_slot(p[i])) - 1u));
+  uint32_t o2 = 0u;
+#pragma unroll
+  for (int r = 0; r < 5; ++r) {
+    uint32_t kr = 0u;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) kr = rk[i] == r ? lw_key(p[i]) : kr;
+    const int t = lw_free(o2, kr, 31);
+    o2 |= 1u << t;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) p[i] = rk[i] == r ? lw_with_slot(p[i], t) : p[i];
+  }
+#pragma unroll
+  for (int i = 5; i < 16; ++i)
+    if (i < n) lw_put(p[i], o2, 31);
+  occ = o2;
+  mask = 31;
+}
+// set_table_resize's size for minused: the smallest power of two above it, at least 8; -1 = mask
+__device__ inline int lw_mask_for(int minused) {
+  int ns = 8;
+  while (ns <= minused) ns <<= 1;
+  return ns - 1;
+}
+
 typedef unsigned __int128 u128;
 
 // phase G: waves that run the lane path (the rest start on the wave queue)
@@ -449,6 +523,11 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
   extern __shared__ __align__(16) unsigned char lds[];
   __shared__ int wsum[T / WAVE];
   __shared__ int s_bad, s_nsol, s_noff, s_open, s_edges, s_Hn, s_Bn, s_nl, s_nw, s_wq;
+#if MZ_MC_PROBE == 80
+  // timing probe: the lane path's passes summed over the lane waves, the waves' G2 durations
+  __shared__ unsigned long long s_pt[8];
+  __shared__ unsigned int s_tmax[2];
+#endif
   const int i = blockIdx.x;
   if (i >= n) return;
   // a bank refill scores the candidates of its consumed slots only: min(*limit, n / mult) groups
@@ -908,6 +987,14 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
   if (Hn + 2 > MM) { fail(2); return; }
   for (int h = threadIdx.x; h <= Hn + 1; h += T) hcur[h] = 0;
   if (threadIdx.x == 0) { s_nl = 0; s_nw = 0; s_wq = 0; }
+#if MZ_MC_PROBE == 80
+  if (threadIdx.x < 8) s_pt[threadIdx.x] = 0ull;
+  if (threadIdx.x < 2) s_tmax[threadIdx.x] = 0u;
+  unsigned long long pt[6] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull}, tl = 0ull;
+#define MC_T(k) do { const unsigned long long t_ = clock64(); pt[k] += t_ - tl; tl = t_; } while (0)
+#else
+#define MC_T(k) do { } while (0)
+#endif
   __syncthreads();
   for (int v = threadIdx.x; v < M; v += T)
     if (hid[v]) atomicAdd(&hcur[hid[v]], 1u);
@@ -928,7 +1015,11 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
   for (int h = threadIdx.x; h <= Hn + 1; h += T) hcur[h] = hstart[h];
   __syncthreads();
   for (int v = threadIdx.x; v < M; v += T)
-    if (hid[v]) hlist[atomicAdd(&hcur[hid[v]], 1u)] = (uint16_t)v;
+    if (hid[v]) {
+      const uint32_t at = atomicAdd(&hcur[hid[v]], 1u);
+      hlist[at] = (uint16_t)v;
+      pref[v] = (uint16_t)(at - hstart[hid[v]]);  // the member's index in its hallway's list
+    }
   __syncthreads();
   {
     const int lane = threadIdx.x & (WAVE - 1);
@@ -1109,6 +1200,9 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
     auto lane_hallway = [&](int h, uint16_t* base, int st) -> bool {
       const int b0 = (int)hstart[h], nc = (int)hstart[h + 1] - b0;
       uint16_t* q = hlist + b0;  // the member list, then the BFS queue (the same nc nodes)
+#if MZ_MC_PROBE == 80
+      tl = clock64();
+#endif
       int first = 0x7FFFFFFF;
       for (int i = 0; i < nc; ++i) first = min(first, (int)q[i]);
       uint16_t* tA = base;
@@ -1163,7 +1257,9 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
           else if (r == 1) q[qn++] = (uint16_t)u;
         }
       }
+      MC_T(0);
       ok = ok && ls_copy(S2, tB, S1, tT, key_of);
+      MC_T(1);
       ls_init(S1, tA, st);
       for (int j = 0; j <= S2.mask && ok; ++j) {
         if (!((S2.occ >> j) & 1u)) continue;
@@ -1187,11 +1283,14 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
           }
         }
       }
+      MC_T(2);
       ok = ok && ls_merge(S2, S1, tT, key_of);
+      MC_T(3);
       ls_init(S1, tA, st);
       for (int j = 0; j <= S2.mask && ok; ++j)
         if ((S2.occ >> j) & 1u)
           if (ls_add(S1, S2.t[j * st], tT, key_of) < 0) ok = false;
+      MC_T(4);
       if (!ok) return false;
       if (2 * S1.used < M) {
         for (int j = 0; j <= S1.mask; ++j) {
@@ -1224,6 +1323,194 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
         }
       }
       Ch[h] = __dmul_rn((double)D, sum);
+      MC_T(5);
+      return true;
+    };
+    // the lane path, ALU edition: the same sets as lane_hallway, laid out by lw_layout_add /
+    // lw_free in registers; per-lane LDS (base, stride st: 96 u16) holds only the scatter buffers
+    // that turn slots into iteration order
+    auto lane_hallway2 = [&](int h, uint32_t* base, int st) -> bool {
+      const int b0 = (int)hstart[h], nc = (int)hstart[h + 1] - b0;
+      uint16_t* q = hlist + b0;
+      uint32_t* xs = base;            // [16] scatter buffer (entry words)
+      uint32_t* as = base + 16 * st;  // [16] split points in insertion order
+      // _plain_bfs from the first member in node order; seen = a bit per member index (pref)
+      int first = 0x7FFFFFFF;
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (i < nc) first = min(first, (int)q[i]);
+      uint32_t vis = 1u << pref[first];
+      q[0] = (uint16_t)first;
+      int qn = 1;
+      for (int hd = 0; hd < qn; ++hd) {
+        const int x = q[hd];
+        const int na = adjn[x];
+        int nb[4];
+        nbrs4(x, nb);
+        uint32_t fm[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int u = k < na ? nb[k] : x;
+          fm[k] = ((uint32_t)nfl[u] << 24) | ((uint32_t)(pref[u] & 0xFFu) << 16) | (uint32_t)u;
+        }
+        uint32_t sk[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sk[k] = k >= na ? 0x20000u : (nb[k] < x ? (uint32_t)nb[k] : 0x10000u + k);
+        auto cx = [&](int a, int b) {
+          const bool sw = sk[b] < sk[a];
+          const uint32_t ta = sk[a], tb = sk[b], fa = fm[a], fb = fm[b];
+          sk[a] = sw ? tb : ta; sk[b] = sw ? ta : tb;
+          fm[a] = sw ? fb : fa; fm[b] = sw ? fa : fb;
+        };
+        cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (k >= na) continue;
+          const uint32_t f = fm[k] >> 24, mi = (fm[k] >> 16) & 0xFFu;
+          if ((f & N_SOL) || (f & 7) == 3) continue;  // not in the hallway
+          if (mi >= 16 || ((vis >> mi) & 1u)) continue;
+          vis |= 1u << mi;
+          if (qn < nc) q[qn] = (uint16_t)(fm[k] & 0xFFFFu);
+          ++qn;
+        }
+      }
+      if (qn != nc) return false;
+      // S1: seen, built by add() in BFS order
+      uint32_t P[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) P[i] = i < nc ? (uint32_t)q[i] : 0u;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) P[i] |= (i < nc ? (uint32_t)nkey[P[i]] : 0u) << 11;
+      uint32_t occ;
+      int mask;
+      lw_layout_add(P, nc, occ, mask);
+      // the entries A[0..n) of a set with occupancy o -> A in the set's iteration order (by rank)
+      auto order = [&](uint32_t (&A)[16], int n, uint32_t o) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (i < n) {
+            const int r = __popc(o & ((1u << lw_slot(A[i])) - 1u));
+            xs[r * st] = A[i];
+          }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) A[i] = i < n ? xs[i * st] : 0u;
+      };
+      // S2 = set(S1): set_merge into an empty set — resize to (used * 2) when used * 5 >= 21,
+      // then S1's layout if the sizes agree, else insert_clean in S1's order
+      order(P, nc, occ);  // P: S1's order (slots kept in the words)
+      const int mask2 = nc * 5 >= 21 ? lw_mask_for(nc * 2) : 7;
+      if (mask2 != mask) {
+        occ = 0u;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (i < nc) lw_put(P[i], occ, mask2);
+        order(P, nc, occ);  // P: S2's order
+      }
+      // adjacent_split_points: for each member in S2's order, its junction neighbours in G's order
+      // up to and including the first solution junction — a set built by add()
+      int nasp = 0;
+#pragma unroll
+      for (int c0 = 0; c0 < 16; c0 += 4) {
+        int nbv[4][4], nav[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int m = c0 + c < nc ? lw_node(P[c0 + c]) : first;
+          nav[c] = c0 + c < nc ? (int)adjn[m] : 0;
+          nbrs4(m, nbv[c]);
+        }
+        uint32_t fk[4][4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int u = k < nav[c] ? nbv[c][k] : first;
+            fk[c][k] = ((uint32_t)nfl[u] << 16) | nkey[u];
+          }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          bool stop = false;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t f = fk[c][k] >> 16;
+            if (k < nav[c] && !stop && (f & N_JUNC)) {
+              if (nasp < 16) as[nasp * st] = ((fk[c][k] & 0xFFFFu) << 11) | (uint32_t)nbv[c][k];
+              ++nasp;
+              if (f & N_SOL) stop = true;
+            }
+          }
+        }
+      }
+      if (nc + nasp > 15) return false;
+      uint32_t A[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        A[i] = i < nasp ? as[i * st] : 0u;
+      uint32_t occa;
+      int maska;
+      lw_layout_add(A, nasp, occa, maska);
+      order(A, nasp, occa);  // A: the split points' set order
+      // all_nodes = S2.union(asp): a copy of S2 (S2's layout), set_merge of asp: resize to
+      // (used + asp) * 2 first when (fill + asp) * 5 >= mask * 3 (S2's entries re-inserted in its
+      // order), then asp's entries added in its order
+      int maskm = mask2;
+      uint32_t occm = occ;
+      if (nasp > 0 && (nc + nasp) * 5 >= mask2 * 3) {
+        maskm = lw_mask_for((nc + nasp) * 2);
+        occm = 0u;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (i < nc) lw_put(P[i], occm, maskm);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (i < nasp) lw_put(A[i], occm, maskm);
+      // the union's order: both parts scattered by rank into one buffer
+      const int nv = nc + nasp;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if (i < nc) xs[__popc(occm & ((1u << lw_slot(P[i])) - 1u)) * st] = P[i] & 0x1FFFFFFu;
+        if (i < nasp) xs[__popc(occm & ((1u << lw_slot(A[i])) - 1u)) * st] = A[i] & 0x1FFFFFFu;
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) P[i] = i < nv ? xs[i * st] : 0u;
+      // show_nodes(nbunch_iter(all_nodes)): a set built by add() in the union's order
+      lw_layout_add(P, nv, occ, mask);
+      order(P, nv, occ);  // P: the view's order
+      constexpr int EB = 2;
+      // EdgeDataView: for each view node in order, its neighbours in G's order that are in the
+      // view and not yet iterated (2 * nv < M: the classifier's condition)
+      double sum = 0.0;
+      long D = 0;
+      int nterm = 0;
+#pragma unroll
+      for (int c0 = 0; c0 < 16; c0 += EB) {
+        int nbv[EB][4], nav[EB];
+        uint2 dv[EB];
+#pragma unroll
+        for (int c = 0; c < EB; ++c) {
+          const int nn = c0 + c < nv ? lw_node(P[c0 + c]) : first;
+          nav[c] = c0 + c < nv ? (int)adjn[nn] : 0;
+          nbrs4(nn, nbv[c]);
+          dv[c] = *reinterpret_cast<const uint2*>(adjd + 4 * nn);
+        }
+#pragma unroll
+        for (int c = 0; c < EB; ++c) {
+          const int j = c0 + c;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            if (k >= nav[c]) continue;
+            const int u = nbv[c][k];
+            bool later = false;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) later |= e > j && e < nv && lw_node(P[e]) == u;
+            if (later) {
+              const uint32_t w = k < 2 ? dv[c].x : dv[c].y;
+              term(sum, D, nterm, (int)((k & 1) ? (w >> 16) : (w & 0xFFFFu)));
+            }
+          }
+        }
+      }
+      Ch[h] = __dmul_rn((double)D, sum);
       return true;
     };
     // G1: one thread per hallway classifies it — <= 3 view nodes: its sum now (the fast path);
@@ -1232,7 +1519,10 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
     uint16_t* Wq = Lq + MM;
     const int Lr = (int)((size_t)MK * 8 / (96 * sizeof(uint16_t)));  // lanes in the keys region
     const int Lc = (int)((size_t)MM * 8 / (96 * sizeof(uint16_t)));  // lanes in the Cb region
-    const int L = min(Lr + Lc, T / 2);
+#ifndef MZ_MC_LMAX
+#define MZ_MC_LMAX 1024
+#endif
+    const int L = min(min(Lr + Lc, T / 2), MZ_MC_LMAX);
     for (int h = 1 + threadIdx.x; h <= Hn; h += T) {
       const int b0 = (int)hstart[h], nc = (int)hstart[h + 1] - b0;
       int nasp = 0;
@@ -1265,7 +1555,8 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
           }
         }
         Ch[h] = __dmul_rn((double)D, sum);
-      } else if (nc <= 15 && nc + nasp <= 15 && L > 0) {
+      } else if (nc <= 15 && nc + nasp <= 15 && L > 0 && 2 * (nc + nasp) < M &&
+                 (!MZ_MC_LANE2 || (MM <= 2048 && N <= 91))) {
         Lq[atomicAdd(&s_nl, 1)] = (uint16_t)h;
       } else {
         Wq[atomicAdd(&s_nw, 1)] = (uint16_t)h;
@@ -1280,15 +1571,34 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
     // lanes are done, takes the wave queue's hallways one at a time
     const int nl = s_nl, nw = s_nw;
     const int wid = threadIdx.x / WAVE;
+#if MZ_MC_PROBE == 80
+    const unsigned long long tg0 = clock64();
+#endif
     if (wid < MC_LANE_WAVES && MZ_MC_PROBE != 73) {
       const int l = lane * MC_LANE_WAVES + wid;  // virtual lane: its table slot
       if (l < L) {
         uint16_t* base = l < Lr ? reinterpret_cast<uint16_t*>(keys) + l
                                 : reinterpret_cast<uint16_t*>(Cb) + (l - Lr);
         const int st = l < Lr ? Lr : Lc;
+        // (the ALU edition's buffers: u32 words, interleaved by lane the same way, 32 per lane)
+        uint32_t* base32 = l < Lr ? reinterpret_cast<uint32_t*>(keys) + l
+                                  : reinterpret_cast<uint32_t*>(Cb) + (l - Lr);
         for (int k = l; k < nl; k += L)
-          if (!lane_hallway(Lq[k], base, st)) s_bad = 2;
+          if (!(MZ_MC_LANE2 ? lane_hallway2(Lq[k], base32, st) : lane_hallway(Lq[k], base, st)))
+            s_bad = 2;
       }
+#if MZ_MC_PROBE == 80
+      for (int k = 0; k < 6; ++k) {  // the wave's pass times (every lane holds the same sums)
+        unsigned long long v = pt[k];
+        for (int o = WAVE / 2; o; o >>= 1) {
+          const unsigned long long w_ = ((unsigned long long)__shfl_xor((int)(v >> 32), o) << 32) |
+                                        (unsigned int)__shfl_xor((int)(unsigned int)v, o);
+          v = v > w_ ? v : w_;
+        }
+        if (lane == 0) atomicAdd(&s_pt[k], v);
+      }
+      if (lane == 0) atomicMax(&s_tmax[0], (unsigned int)(clock64() - tg0));
+#endif
     }
     for (;;) {
       int k = 0;
@@ -1297,8 +1607,23 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
       if (k >= nw || MZ_MC_PROBE == 74) break;
       wave_hallway(Wq[k]);
     }
+#if MZ_MC_PROBE == 80
+    if (lane == 0) atomicMax(&s_tmax[1], (unsigned int)(clock64() - tg0));
+#endif
   }
   __syncthreads();
+#if MZ_MC_PROBE == 80
+  if (threadIdx.x == 0) {
+    auto f17 = [&](int k) -> double {  // mean per lane wave, 16-cycle units, 17 bits
+      const unsigned long long v = s_pt[k] / (16ull * MC_LANE_WAVES);
+      return (double)(v < 131071ull ? v : 131071ull);
+    };
+    out[2 * i] = f17(0) + f17(1) * 131072.0 + f17(2) * 17179869184.0;
+    out[2 * i + 1] = f17(3) + f17(4) * 131072.0 + f17(5) * 17179869184.0;
+    status[i] = (int)(min(s_tmax[0] / 64u, 32767u) | (min(s_tmax[1] / 64u, 32767u) << 16));
+  }
+  return;
+#endif
   if (s_bad) { fail(2); return; }
   MC_PROBE_AT(7)
   // hallway 0: the solution branch, edges in path order — the terms 1 / (2 d) by all threads (into
