@@ -31,11 +31,14 @@
 
 #include "mz_learner.h"
 
-// k_adamw's grid: every workgroup takes one same-address ticket (publish_step), and those atomics
-// serialise at ~30 ns each — 2,048 workgroups of 256 made the launch 78 us alone (106 us per
-// vector step inside training) for ~60 MB of traffic. 256 workgroups of 512 (grid-stride beyond):
+// k_adamw's grid: every workgroup takes one same-address ticket (publish_step), ~20 ns each at
+// the end of the launch — 2,048 workgroups of 256 made the launch 78 us alone (106 us per vector
+// step inside training) for ~60 MB of traffic; 256 workgroups of 512 (grid-stride beyond):
 // 20.4 us alone, DDQN training 60.8 -> 63-64 M env steps/s (profiles/r02z_adamw/,
-// profiles/exp_adamw_ticket.sh).
+// profiles/exp_adamw_ticket.sh). The cost is each workgroup's fence + atomic round trip, not the
+// shared address: two-level tickets (16 group counters 128 B apart, then a root counter) measured
+// 8.8 vs 7.9 us at 256 workgroups, 12.9 vs 13.7 at 512 (profiles/ubench_ticket.hip,
+// profiles/r05u/ticket.jsonl), and k_adamw / k_head_loss unchanged with them.
 #ifndef MZ_ADAMW_MAXWG
 #define MZ_ADAMW_MAXWG 256
 #endif
@@ -354,52 +357,55 @@ hipError_t mz_launch_pair_surrogate(const float* lp_new, const float* lp_old, co
 // ------------------------------------------------------------------------------------------
 // Column sums of a row-major f32 matrix g[n][ld] over its first m columns: the Linear bias
 // gradient db = dY^T 1 of the learners' captured updates (agents/linear.py). rocBLAS's GEMV
-// against a ones vector took ~20 us for [2,048 x 1,024] (plus the ones fill); here 64 columns
-// per workgroup, 16-B loads (4 columns per lane), 64 row groups summed in LDS in a fixed order
-// (deterministic).
+// against a ones vector took ~20 us for [2,048 x 1,024] (plus the ones fill). Here 4 * CQ columns
+// per workgroup of 1,024 threads (16-B loads, 4 columns per lane) and RG = 256 / CQ row groups,
+// each summing rows rg, rg + RG, ... with 8 loads in flight; then the row groups' partials by a
+// fixed-order tree in LDS (deterministic). 64 columns per workgroup (16 workgroups for fc1's 1,024
+// bias columns, 64 serial partial adds at the end) kept most CUs idle: ~4 us per call.
 #ifndef MZ_COLSUM_CQ
-#define MZ_COLSUM_CQ 16  // column quads per workgroup (64 row groups each)
+#define MZ_COLSUM_CQ 4  // column quads per workgroup
 #endif
-static __global__ __launch_bounds__(64 * MZ_COLSUM_CQ) void k_colsum(const float* __restrict__ g,
-                                                                    int n, int m, int ld,
-                                                                    float* __restrict__ out) {
-  __shared__ float4 part[64][MZ_COLSUM_CQ];
+constexpr int CS_T = 1024;
+constexpr int CS_RG = CS_T / MZ_COLSUM_CQ;  // row groups
+static __global__ __launch_bounds__(CS_T) void k_colsum(const float* __restrict__ g, int n, int m,
+                                                        int ld, float* __restrict__ out) {
+  __shared__ float4 part[CS_RG][MZ_COLSUM_CQ];
   const int cq = threadIdx.x % MZ_COLSUM_CQ, rg = threadIdx.x / MZ_COLSUM_CQ;
   const int c = blockIdx.x * (4 * MZ_COLSUM_CQ) + cq * 4;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (c < m) {
-    // 8 rows' loads in flight before their adds (same summation order): a load-add chain waited
-    // a round trip per row — 22 vs 9 us per call once the acting kernels share the chip
+    // 8 rows' loads in flight before their adds: a load-add chain waited a round trip per row
     int r = rg;
-    for (; r + 7 * 64 < n; r += 8 * 64) {
+    for (; r + 7 * CS_RG < n; r += 8 * CS_RG) {
       float4 v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(g + (size_t)(r + 64 * u) * ld + c);
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(g + (size_t)(r + CS_RG * u) * ld + c);
 #pragma unroll
       for (int u = 0; u < 8; ++u) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
     }
-    for (; r < n; r += 64) {
+    for (; r < n; r += CS_RG) {
       const float4 v = *reinterpret_cast<const float4*>(g + (size_t)r * ld + c);
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
   }
   part[rg][cq] = s;
   __syncthreads();
-  if (rg == 0 && c < m) {
-    float4 t = part[0][cq];
-    for (int k = 1; k < 64; ++k) {
-      const float4 u = part[k][cq];
-      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+#pragma unroll
+  for (int h = CS_RG / 2; h; h >>= 1) {
+    if (rg < h) {
+      const float4 u = part[rg + h][cq];
+      s.x += u.x; s.y += u.y; s.z += u.z; s.w += u.w;
+      part[rg][cq] = s;
     }
-    *reinterpret_cast<float4*>(out + c) = t;
+    __syncthreads();
   }
+  if (rg == 0 && c < m) *reinterpret_cast<float4*>(out + c) = s;
 }
 
 hipError_t mz_launch_colsum(const float* g, int n, int m, int ld, float* out, hipStream_t s) {
   if (m <= 0) return hipSuccess;
   constexpr int cols = 4 * MZ_COLSUM_CQ;
-  hipLaunchKernelGGL(k_colsum, dim3((m + cols - 1) / cols), dim3(64 * MZ_COLSUM_CQ), 0, s, g, n, m,
-                     ld, out);
+  hipLaunchKernelGGL(k_colsum, dim3((m + cols - 1) / cols), dim3(CS_T), 0, s, g, n, m, ld, out);
   return hipGetLastError();
 }
 
