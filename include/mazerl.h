@@ -514,9 +514,9 @@ int mz_q_loss_backward(const float* grad_dev, const float* diff_dev, const int64
  * q = W3 h + b3 (fc3: W3 [4][hidden], b3 [4]); with `stacked` the source rows are DDQN's [s; s']
  * (2b rows: V(s') = q_t[argmax q_s(s')], first maximum), else b rows and V(s') = max q_t; then
  * diff_dev / *loss_dev exactly as mz_q_loss (dqn_agent.py:129-147, ddqn_agent.py:121-143).
- * part_dev: mz_head_loss_workspace_floats(b) floats; ticket_dev: a zeroed uint32 the launch
- * leaves zero (one per concurrently running call). Replaces the activation, fc3 and loss launches
- * of both nets. */
+ * part_dev: mz_head_loss_workspace_floats(b) floats (one per concurrently running call);
+ * ticket_dev: unused since round 5 (the per-workgroup partials are summed by a second launch on
+ * `stream`), may be NULL. Replaces the activation, fc3 and loss launches of both nets. */
 int mz_head_loss_workspace_floats(int32_t b);
 int mz_head_loss(const float* z2s_dev, int32_t lds, const float* w3s_dev, const float* b3s_dev,
                  const float* z2t_dev, int32_t ldt, const float* w3t_dev, const float* b3t_dev,

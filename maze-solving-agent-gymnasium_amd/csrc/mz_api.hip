@@ -1135,7 +1135,7 @@ int mz_head_loss(const float* z2s_dev, int32_t lds, const float* w3s_dev, const 
                  uint32_t* ticket_dev, float* loss_dev, float* diff_dev, void* stream) {
   if (b <= 0 || hidden <= 0 || hidden % 4 || (act != 0 && act != 1) || !z2s_dev || !w3s_dev ||
       !b3s_dev || !z2t_dev || !w3t_dev || !b3t_dev || !action_dev || !reward_dev || !part_dev ||
-      !ticket_dev || !loss_dev || !diff_dev || lds < hidden || ldt < hidden)
+      !loss_dev || !diff_dev || lds < hidden || ldt < hidden)
     return fail(MZ_EINVAL, "bad arguments");
   MzHeadLoss p{z2s_dev, w3s_dev, b3s_dev, z2t_dev, w3t_dev, b3t_dev, lds, ldt, stacked ? 1 : 0, b,
                hidden, act, action_dev, reward_dev, (float)gamma, part_dev, ticket_dev, loss_dev,

@@ -67,7 +67,7 @@ struct MzHeadLoss {
   const float* reward;
   float gamma;
   float* part;      // [mz_head_loss_blocks(b)]
-  unsigned* ticket; // zero; the launch leaves it zero
+  unsigned* ticket; // unused since round 5 (the partials are summed by a second launch)
   float *loss, *diff;
 };
 int mz_head_loss_blocks(int b);

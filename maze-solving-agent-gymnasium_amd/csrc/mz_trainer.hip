@@ -248,8 +248,8 @@ __global__ void k_q_loss_bwd(const float* __restrict__ g, const float* __restric
 //   k_head_loss       one wave per row i < b: h = act(z2), q_s(i) = W3 h + b3 (4 dot products of
 //                     H), DDQN's q_s(b + i) -> first argmax, the target's q_t(i), the TD error
 //                     diff_i (k_q_loss_fwd's f32 ops and NaN rules), the loss = sum diff^2 / b
-//                     summed per workgroup and then over workgroups in order by the last one (a
-//                     ticket it resets): deterministic;
+//                     summed per workgroup, then over workgroups in order by k_loss_sum (a
+//                     one-workgroup launch): deterministic;
 //   k_head_loss_bwd   g_i = diff_i * (2 / b) * grad (k_q_loss_bwd's order); dz2[i][j] =
 //                     act'(z2[i][j]) * (g_i W3[a_i][j]) — dq has one nonzero per row, so this IS
 //                     fc3's dX GEMM value (the other terms are exact zeros) — for i < b; the
@@ -276,15 +276,22 @@ __device__ inline float wave_sum_f(float x) {
   return x;
 }
 
+// Per lane the row's columns j = lane, lane + 64, ... in that order (the f32 FMA chains of the
+// round-4 kernel, bit for bit), HL_U of them with all their loads (z2 of the three rows, W3 of
+// both nets) issued before the first FMA: a loop that loaded one column per iteration waited one
+// round trip per 64 columns (38.6 us for 2,048 DDQN rows, 25.5 us for 512). The per-workgroup
+// partials of sum diff^2 are summed by k_loss_sum, a second one-workgroup launch: a last-workgroup
+// ticket cost each workgroup a fence + atomic round trip at the end of the launch (~11 us at 512
+// workgroups, profiles/r05u/ticket.jsonl).
+constexpr int HL_U = 4;
 template <int ACT>
 __global__ __launch_bounds__(HL_T) void k_head_loss(
     const float* __restrict__ z2s, int lds, const float* __restrict__ w3s,
     const float* __restrict__ b3s, const float* __restrict__ z2t, int ldt,
     const float* __restrict__ w3t, const float* __restrict__ b3t, int dbl,
     const int64_t* __restrict__ action, const float* __restrict__ reward, float gamma, int b, int H,
-    float* __restrict__ part, unsigned* ticket, float* __restrict__ loss, float* __restrict__ diff) {
+    float* __restrict__ part, float* __restrict__ diff) {
   __shared__ float wpart[HL_T / W];
-  __shared__ bool last;
   const int lane = threadIdx.x & (W - 1), w = threadIdx.x / W;
   const int i = blockIdx.x * (HL_T / W) + w;
   float d2 = 0.0f;
@@ -293,14 +300,32 @@ __global__ __launch_bounds__(HL_T) void k_head_loss(
     const float* rs = z2s + (size_t)i * lds;
     const float* rn = z2s + (size_t)(b + i) * lds;
     const float* rt = z2t + (size_t)i * ldt;
-    for (int j = lane; j < H; j += W) {
-      const float hs = head_act<ACT>(rs[j]), ht = head_act<ACT>(rt[j]);
-      const float hn = dbl ? head_act<ACT>(rn[j]) : 0.0f;
+    for (int j0 = lane; j0 < H; j0 += HL_U * W) {
+      float xs[HL_U], xt[HL_U], xn[HL_U], ws[HL_U][4], wt[HL_U][4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        as[k] = __fmaf_rn(hs, w3s[k * H + j], as[k]);
-        at[k] = __fmaf_rn(ht, w3t[k * H + j], at[k]);
-        if (dbl) an[k] = __fmaf_rn(hn, w3s[k * H + j], an[k]);
+      for (int u = 0; u < HL_U; ++u) {
+        const int j = j0 + u * W;
+        const bool ok = j < H;
+        xs[u] = ok ? rs[j] : 0.0f;
+        xt[u] = ok ? rt[j] : 0.0f;
+        xn[u] = ok && dbl ? rn[j] : 0.0f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          ws[u][k] = ok ? w3s[k * H + j] : 0.0f;
+          wt[u][k] = ok ? w3t[k * H + j] : 0.0f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < HL_U; ++u) {
+        if (j0 + u * W >= H) break;
+        const float hs = head_act<ACT>(xs[u]), ht = head_act<ACT>(xt[u]);
+        const float hn = dbl ? head_act<ACT>(xn[u]) : 0.0f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          as[k] = __fmaf_rn(hs, ws[u][k], as[k]);
+          at[k] = __fmaf_rn(ht, wt[u][k], at[k]);
+          if (dbl) an[k] = __fmaf_rn(hn, ws[u][k], an[k]);
+        }
       }
     }
     float qs[4], qn[4], qt[4];
@@ -332,44 +357,62 @@ __global__ __launch_bounds__(HL_T) void k_head_loss(
     float s = 0.0f;
     for (int k = 0; k < HL_T / W; ++k) s = __fadd_rn(s, wpart[k]);
     part[blockIdx.x] = s;
-    __threadfence();
-    last = atomicAdd(ticket, 1u) == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (last) {  // every other workgroup's partial is visible: sum them in a fixed order, all
-    __threadfence();  // threads loading at once (a serial loop waited one round trip per partial)
-    float s = 0.0f;
-    for (unsigned k = threadIdx.x; k < gridDim.x; k += HL_T)
-      s = __fadd_rn(s, __hip_atomic_load(&part[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    s = wave_sum_f(s);
-    if (lane == 0) wpart[w] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      float t = 0.0f;
-      for (int k = 0; k < HL_T / W; ++k) t = __fadd_rn(t, wpart[k]);
-      *loss = __fdiv_rn(t, (float)b);
-      *ticket = 0u;
-    }
   }
 }
 
+// the loss = (sum of the workgroups' partials, in a fixed order) / b — the order the round-4
+// kernel's last workgroup used: thread t sums partials t, t + 256, ..., then the waves' butterflies
+// and the four wave sums in order
+__global__ __launch_bounds__(HL_T) void k_loss_sum(const float* __restrict__ part, int nblk, int b,
+                                                  float* __restrict__ loss) {
+  __shared__ float wpart[HL_T / W];
+  const int lane = threadIdx.x & (W - 1), w = threadIdx.x / W;
+  float s = 0.0f;
+  for (int k = threadIdx.x; k < nblk; k += HL_T) s = __fadd_rn(s, part[k]);
+  s = wave_sum_f(s);
+  if (lane == 0) wpart[w] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.0f;
+    for (int k = 0; k < HL_T / W; ++k) t = __fadd_rn(t, wpart[k]);
+    *loss = __fdiv_rn(t, (float)b);
+  }
+}
+
+// The block's rows' g_i and a_i are formed once into LDS, and per column j the 16 rows' z2 and
+// W3's four rows are loaded before any arithmetic: the round-4 loop read action[i], then
+// W3[a_i][j] (a dependent load), then z2[i][j] row after row (39.7 us average per launch inside
+// training, profiles/r05u). Same f32 operations in the same order: the same bits.
 template <int ACT>
 __global__ __launch_bounds__(HB_T) void k_head_loss_bwd(
     const float* __restrict__ g, const float* __restrict__ diff, const int64_t* __restrict__ action,
     int b, float norm, const float* __restrict__ z2s, int lds, const float* __restrict__ w3s, int H,
     float* __restrict__ dz2, int ldd, float* __restrict__ part) {
   // part: [gridDim.x][4 H + 4] — this block's dW3 (row-major [4][H]) and db3 partials
-  const int r0 = blockIdx.x * HB_RB, r1 = min(b, r0 + HB_RB);
+  __shared__ float gs[HB_RB];
+  __shared__ int as_[HB_RB];
+  const int r0 = blockIdx.x * HB_RB, nr = min(b, r0 + HB_RB) - r0;
   const float gg = *g;
+  if ((int)threadIdx.x < nr) {
+    gs[threadIdx.x] = __fmul_rn(__fmul_rn(diff[r0 + threadIdx.x], norm), gg);
+    as_[threadIdx.x] = (int)action[r0 + threadIdx.x];
+  }
+  __syncthreads();
   float* pw = part + (size_t)blockIdx.x * (4 * H + 4);
   for (int j = threadIdx.x; j < H; j += HB_T) {
+    float z[HB_RB];
+    const float w0 = w3s[j], w1 = w3s[H + j], w2 = w3s[2 * H + j], w3 = w3s[3 * H + j];
+#pragma unroll
+    for (int i = 0; i < HB_RB; ++i) z[i] = i < nr ? z2s[(size_t)(r0 + i) * lds + j] : 0.0f;
     float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    for (int i = r0; i < r1; ++i) {
-      const int a = (int)action[i];
-      const float s = __fmul_rn(__fmul_rn(diff[i], norm), gg);
-      const float z = z2s[(size_t)i * lds + j];
-      dz2[(size_t)i * ldd + j] = head_act_grad<ACT>(z, __fmul_rn(s, w3s[a * H + j]));
-      const float t = __fmul_rn(s, head_act<ACT>(z));
+#pragma unroll
+    for (int i = 0; i < HB_RB; ++i) {
+      if (i >= nr) break;
+      const int a = as_[i];
+      const float sg = gs[i];
+      const float wa = a == 0 ? w0 : (a == 1 ? w1 : (a == 2 ? w2 : w3));
+      dz2[(size_t)(r0 + i) * ldd + j] = head_act_grad<ACT>(z[i], __fmul_rn(sg, wa));
+      const float t = __fmul_rn(sg, head_act<ACT>(z[i]));
       a0 = a == 0 ? __fadd_rn(a0, t) : a0;
       a1 = a == 1 ? __fadd_rn(a1, t) : a1;
       a2 = a == 2 ? __fadd_rn(a2, t) : a2;
@@ -382,9 +425,8 @@ __global__ __launch_bounds__(HB_T) void k_head_loss_bwd(
   }
   if (threadIdx.x < 4) {
     float sb = 0.0f;
-    for (int i = r0; i < r1; ++i)
-      if ((int)action[i] == (int)threadIdx.x)
-        sb = __fadd_rn(sb, __fmul_rn(__fmul_rn(diff[i], norm), gg));
+    for (int i = 0; i < nr; ++i)
+      if (as_[i] == (int)threadIdx.x) sb = __fadd_rn(sb, gs[i]);
     pw[4 * H + threadIdx.x] = sb;
   }
 }
@@ -412,11 +454,12 @@ hipError_t mz_launch_head_loss(const MzHeadLoss& p, hipStream_t s) {
   if (p.act == 0)
     hipLaunchKernelGGL(k_head_loss<0>, dim3(blocks), dim3(HL_T), 0, s, p.z2s, p.lds, p.w3s, p.b3s,
                        p.z2t, p.ldt, p.w3t, p.b3t, p.dbl, p.action, p.reward, p.gamma, p.b, p.H,
-                       p.part, p.ticket, p.loss, p.diff);
+                       p.part, p.diff);
   else
     hipLaunchKernelGGL(k_head_loss<1>, dim3(blocks), dim3(HL_T), 0, s, p.z2s, p.lds, p.w3s, p.b3s,
                        p.z2t, p.ldt, p.w3t, p.b3t, p.dbl, p.action, p.reward, p.gamma, p.b, p.H,
-                       p.part, p.ticket, p.loss, p.diff);
+                       p.part, p.diff);
+  hipLaunchKernelGGL(k_loss_sum, dim3(1), dim3(HL_T), 0, s, p.part, blocks, p.b, p.loss);
   return hipGetLastError();
 }
 

@@ -655,12 +655,20 @@ class VectorDQNLearner:
                    for j in range(1, K))
 
     def _capture_k_block(self, slot):
+        # each update's gather reads its row of the slot's index buffer in place (the buffers are
+        # allocated once, _start_async): no copy into idx_static between the K updates — four
+        # blit launches per vector step on the update stream (~13.6 us each inside best-of-6
+        # training, profiles/r05u/train_kernel_stats.csv)
         rp, K = self.replay, self.updates_per_step
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            for k in range(K):
-                rp.idx_static.copy_(self._idx[slot][k])
-                loss = self._one_update(None, static=True)
+        keep = rp.idx_static
+        try:
+            with torch.cuda.graph(g):
+                for k in range(K):
+                    rp.idx_static = self._idx[slot][k]
+                    loss = self._one_update(None, static=True)
+        finally:
+            rp.idx_static = keep
         self._graphK[slot] = g
         self._graphK_loss[slot] = loss
 
