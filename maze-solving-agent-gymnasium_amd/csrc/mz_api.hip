@@ -41,6 +41,7 @@ struct MzBankStore {  // two banks x the enabled algorithms x sizes x K slots (m
   uint32_t* meta1 = nullptr;
   int* heads = nullptr;        // [2][3][nD] consumed slots per (algorithm id, size)
   int* slot = nullptr;         // [3][nD][ceil(B / 64)] winners' first slot per group (k_reset_done)
+  int8_t* code = nullptr;      // [B] each instance's winner code before a reset launch (MzDev::bk_code)
   // scratch the build writes and nobody reads: [K] ...
   uint32_t *s_posw = nullptr, *s_stw = nullptr, *s_curw = nullptr;
   uint8_t *s_last = nullptr, *s_algo = nullptr;
@@ -584,7 +585,8 @@ int mz_bank_create_ex(mz_handle* h, int32_t slots, const int32_t* dims, int32_t 
   if ((rc = alloc(h, &b.cells, S * d.P * d.P)) || (rc = alloc(h, &b.planes, S * d.PW)) ||
       (rc = alloc(h, &b.meta0, S)) || (rc = alloc(h, &b.meta1, S)) ||
       (rc = alloc(h, &b.heads, (size_t)6 * ndims)) ||
-      (rc = alloc(h, &b.slot, (size_t)3 * ndims * ((d.B + 63) / 64))) || (rc = alloc(h, &b.s_posw, K)) ||
+      (rc = alloc(h, &b.slot, (size_t)3 * ndims * ((d.B + 63) / 64))) ||
+      (rc = alloc(h, &b.code, (size_t)d.B)) || (rc = alloc(h, &b.s_posw, K)) ||
       (rc = alloc(h, &b.s_stw, K)) || (rc = alloc(h, &b.s_curw, K)) || (rc = alloc(h, &b.s_last, K)) ||
       (rc = alloc(h, &b.s_algo, K)))
     return rc;
@@ -680,6 +682,7 @@ int mz_bank_use(mz_handle* h, int32_t bank) {
   d.bk_meta1 = b.meta1 + blk;
   d.bk_head = b.heads + 3 * bank * b.nD;
   d.bk_slot = b.slot;
+  d.bk_code = b.code;
   d.bk_G = (d.B + 63) / 64;
   return MZ_OK;
 }

@@ -81,6 +81,11 @@ struct MzDev {
   // of the group's winners, bk_slot[class * bk_G + g]
   int* bk_slot;             // [3 * bk_nd][bk_G]
   int bk_G;                 // 64-instance groups, ceil(B / 64)
+  // per instance, what k_bank_count saw before the reset launch: -2 not a winner, -1 a winner
+  // without a bank class, else its class. k_reset_done ranks a group's winners from these: with
+  // several waves per group, live state (done flag, last_term) read by one wave may already be
+  // reset by a sibling wave, which shifted the ranks (two winners on one slot, run to run)
+  int8_t* bk_code;          // [B]
   // per-instance size of a winner's next maze (the variable-size envs' update_maze growth,
   // simple_variable_maze_env.py:93-112 / toroidal_variable_maze_env.py:113-131): 0 = the winner
   // keeps its maze (the reference's `shape > max_shape` branch), null = its current size

@@ -651,7 +651,9 @@ __device__ bool bank_take(const MzDev& d, int e, int cls, int slot, uint2& meta)
 // group -> bk_slot[class * G + g] (the array is zeroed before the launch).
 __global__ __launch_bounds__(WAVE) void k_bank_count(MzDev d) {
   const int lane = threadIdx.x, g = blockIdx.x, e = g * WAVE + lane;
-  const int cls = regen_winner(d, e) ? bank_class(d, e) : -1;
+  const bool w = regen_winner(d, e);
+  const int cls = w ? bank_class(d, e) : -1;
+  if (e < d.B) d.bk_code[e] = (int8_t)(w ? cls : -2);
   unsigned long long pend = __ballot(cls >= 0);
   while (pend) {  // one pass per distinct class in the wave (wave-uniform loop)
     const int cj = __shfl(cls, __ffsll((long long)pend) - 1);
@@ -801,12 +803,17 @@ __global__ __launch_bounds__(WAVE) void k_reset_done(MzDev d, int regen, uint64_
   const int lane = threadIdx.x, e = grp * WAVE + lane;
   const bool done = e < d.B && ((d.posw[e] >> 20) & 1u);
   // gets a new maze (loaded once, coalesced); a winner whose next size is 0 keeps its maze
-  const bool win = regen && done && d.last_term[e] && mz_regen_dim(d, e) != 0;
+  bool win = regen && done && d.last_term[e] && mz_regen_dim(d, e) != 0;
   // this lane's bank slot if it is a winner with a bank class: the group's first slot of the
-  // class (k_bank_scan) + its rank among the group's winners of the class
+  // class (k_bank_scan) + its rank among the group's winners of the class — ranked from the
+  // codes k_bank_count stored before this launch (split > 1: a sibling wave may have reset some
+  // of the group's instances already, so their live flags no longer say "winner")
   int cls = -1, slot = 0;
   if (regen && d.bk_K) {
-    cls = win ? bank_class(d, e) : -1;
+    const int code = e < d.B ? (int)d.bk_code[e] : -2;
+    win = code != -2;
+    cls = code;  // -1 or the class for winners, -2 otherwise: only cls >= 0 takes a slot
+    if (cls < 0) cls = -1;
     unsigned long long pend = __ballot(cls >= 0);
     while (pend) {
       const int cj = __shfl(cls, __ffsll((long long)pend) - 1);
