@@ -928,14 +928,23 @@ __host__ __device__ inline size_t mz_torus_lds_bytes(int P) {
 
 // Generation + tables of a Philox maze in cell space (lds >= mz_cell_lds_bytes(P), toroidal:
 // mz_torus_lds_bytes(P)).
-__device__ void mz_build_cells(const MzDev& d, int e, int algo, uint64_t seed, int N, bool tor,
-                               uint8_t* lds) {
+// cell-space LDS state of a new build: no passages, empty bit sets (wave-wide)
+__device__ inline void mz_cells_clear(const MzCellLds& L) {
+  const int lane = threadIdx.x;
+  for (int q = lane; q < L.Q; q += 64) L.pas[q] = 0;
+  for (int i = lane; i < (L.Q + 31) / 32; i += 64) { L.b0[i] = 0u; L.b1[i] = 0u; }
+}
+
+__device__ __forceinline__ void mz_cells_finish(const MzDev& d, int e, const MzCellLds& L, int N,
+                                                bool tor);
+
+__device__ __forceinline__ void mz_build_cells(const MzDev& d, int e, int algo, uint64_t seed, int N,
+                                               bool tor, uint8_t* lds) {
   const int lane = threadIdx.x;
   const int G = tor ? N + 2 : N;
   const MzCellLds L = mz_cell_lds(lds, tor ? d.P + 2 : d.P, G);
-  const int W = L.W, Q = L.Q;
-  for (int q = lane; q < Q; q += 64) L.pas[q] = 0;
-  for (int i = lane; i < (Q + 31) / 32; i += 64) { L.b0[i] = 0u; L.b1[i] = 0u; }
+  const int W = L.W;
+  mz_cells_clear(L);
   __syncthreads();
   MzRng rng{seed, 0ull, {0u, 0u, 0u, 0u}};
   if (lane == 0) {
@@ -946,9 +955,53 @@ __device__ void mz_build_cells(const MzDev& d, int e, int algo, uint64_t seed, i
     else if (algo == MZ_ALGO_DFS_DEV) mz_cs_dfs(L, a * W + b, rng);
   }
   __syncthreads();
-  const int s = L.sh[2];
-  if (algo != MZ_ALGO_RPRIM_DEV && algo != MZ_ALGO_DFS_DEV) mz_cs_primkill(L, s, rng);
+  if (algo != MZ_ALGO_RPRIM_DEV && algo != MZ_ALGO_DFS_DEV) mz_cs_primkill(L, L.sh[2], rng);
   __syncthreads();
+  mz_cells_finish(d, e, L, N, tor);
+}
+
+// Philox r-prim / dfs builds of up to MZ_PACK mazes of one size and algorithm per wave
+// (euclidean): maze m's carve runs on lane 16 m over its own LDS region (`stride` bytes apart),
+// the MZ_PACK carves in lockstep — an r-prim carve is exactly Q - 1 iterations of the same
+// instructions (every cell but the start enters the frontier once; two draws per iteration, one
+// Philox word each), a dfs carve exactly 2 Q - 1 (each cell pushed and popped once; a push or a
+// backtrack per iteration) — so the wave issues each instruction once for all of them, where one
+// carve per wave left the SIMDs issuing one-lane instructions for ~18 waves per CU. Goal,
+// distance field and tables then run wave-wide, maze after maze. The same Philox draws in the
+// same order: the same mazes as mz_build_cells.
+#ifndef MZ_PACK
+#define MZ_PACK 4
+#endif
+// e / seed: lane l holds those of maze l >> 4 (lanes of mazes >= nm: unused)
+__device__ __forceinline__ void mz_build_cells_packed(const MzDev& d, int e, uint64_t seed, int nm,
+                                                      int N, int algo, uint8_t* lds, size_t stride) {
+  const int lane = threadIdx.x, m = lane >> 4;
+  for (int k = 0; k < nm; ++k) mz_cells_clear(mz_cell_lds(lds + k * stride, d.P, N));
+  __syncthreads();
+  if ((lane & 15) == 0 && m < nm) {
+    const MzCellLds L = mz_cell_lds(lds + m * stride, d.P, N);
+    const int W = L.W;
+    MzRng rng{seed, 0ull, {0u, 0u, 0u, 0u}};
+    const int a = (int)rng.below((uint32_t)W), b = (int)rng.below((uint32_t)W);
+    L.sh[2] = a * W + b;
+    if (algo == MZ_ALGO_RPRIM_DEV) mz_cs_rprim(L, a * W + b, rng);
+    else mz_cs_dfs(L, a * W + b, rng);
+  }
+  __syncthreads();
+  for (int k = 0; k < nm; ++k) {
+    mz_cells_finish(d, __shfl(e, 16 * k), mz_cell_lds(lds + k * stride, d.P, N), N, false);
+    __syncthreads();
+  }
+}
+
+// goal, distance field and tables of a carved cell-space maze (wave-wide): the rest of
+// mz_build_cells
+__device__ __forceinline__ void mz_cells_finish(const MzDev& d, int e, const MzCellLds& L, int N,
+                                                bool tor) {
+  const int lane = threadIdx.x;
+  const int G = tor ? N + 2 : N;
+  const int W = L.W;
+  const int s = L.sh[2];
   int goal = (MZ_GPROBE & 4) ? s : mz_cs_goal(L, G, s);
   if (goal < 0) goal = s;  // unreachable for W >= 2 (a spanning tree has >= 2 leaves)
   // open squares of the G x G generation grid

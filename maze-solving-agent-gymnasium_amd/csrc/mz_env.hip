@@ -703,6 +703,28 @@ __global__ __launch_bounds__(BS_T) void k_bank_scan(MzDev d) {
 // C > 1 over the instances of a handle draws the candidates best_of_mazes draws for those
 // instances (VectorMazeEnv.generate of n * C instances from `seed`: candidate c of maze k is
 // instance k * C + c, seed + k * C + c). The algorithm: algo_list[j] or algo_all.
+// Euclidean Philox r-prim / dfs candidates of one algorithm (the headline's bank classes),
+// MZ_PACK per wave (mz_build_cells_packed): candidates t0 .. t0 + MZ_PACK - 1 on lanes
+// 16 (t - t0) ..
+__global__ __launch_bounds__(WAVE) void k_cand_build_packed(MzDev cd, const int32_t* ids, int base,
+                                                            const int* count, int n, int C,
+                                                            int algo, int dim, uint64_t seed,
+                                                            uint32_t epoch, int stride) {
+  extern __shared__ __align__(16) uint8_t lds[];
+  const int used = count ? min(*count, n) : n;
+  const int total = used * C, m = threadIdx.x >> 4;
+  for (int t0 = blockIdx.x * MZ_PACK; t0 < total; t0 += gridDim.x * MZ_PACK) {
+    const int nm = min(MZ_PACK, total - t0);
+    const int t = t0 + min(m, nm - 1);
+    const int j = t / C, c = t - j * C;
+    const uint64_t id = (uint64_t)(ids ? ids[j] : base + j);
+    if ((threadIdx.x & 15) == 0 && m < nm) cd.algo[t] = (uint8_t)algo;
+    mz_build_cells_packed(cd, t, seed + id * (uint64_t)C + (uint64_t)c + ((uint64_t)epoch << 32), nm,
+                          dim, algo, lds, (size_t)stride);
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(WAVE) void k_cand_build(MzDev cd, const int32_t* ids, int base,
                                                      const int* count, int n, int C,
                                                      const uint8_t* algo_list, int algo_all,
@@ -990,6 +1012,9 @@ hipError_t mz_lds_attr(const void* fn, size_t bytes) {
   return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
+#ifndef MZ_PACK_DFS  // dfs candidate lists packed too (A/B builds: 0)
+#define MZ_PACK_DFS 1
+#endif
 #ifndef MZ_BANK_WGS
 #define MZ_BANK_WGS 0
 #endif
@@ -1125,15 +1150,25 @@ hipError_t mz_launch_cand_build(const MzDev& cd, const int32_t* ids, int base, c
                                 int C, const uint8_t* algo_list, int algo_all, int dim,
                                 uint64_t seed, uint32_t epoch, hipStream_t s) {
   if (n <= 0 || C <= 0) return hipSuccess;
-  const size_t lds = mz_build_lds_launch(cd.P, cd.toroidal, true, MZ_PY_PHILOX);
-  hipError_t ae = mz_lds_attr(reinterpret_cast<const void*>(k_cand_build), lds);
+  // euclidean Philox r-prim / dfs lists (the headline's bank classes) build MZ_PACK per wave
+  const bool packed = MZ_PACK > 1 && MZ_CELL_BUILD && !cd.toroidal && !algo_list &&
+                      (algo_all == MZ_ALGO_RPRIM_DEV || (MZ_PACK_DFS && algo_all == MZ_ALGO_DFS_DEV));
+  const size_t stride = packed ? mz_align16(mz_cell_lds_bytes(cd.P)) : 0;
+  const size_t lds = packed ? MZ_PACK * stride : mz_build_lds_launch(cd.P, cd.toroidal, true, MZ_PY_PHILOX);
+  const void* kfn = packed ? reinterpret_cast<const void*>(k_cand_build_packed)
+                           : reinterpret_cast<const void*>(k_cand_build);
+  hipError_t ae = mz_lds_attr(kfn, lds);
   if (ae != hipSuccess) return ae;
   // a bank refill runs beside the trainer's acting and update kernels: MZ_BANK_WGS caps its
   // resident builds (0 = as many as fit) so that it leaves CUs / LDS to them
-  const int total = n * C;
-  const int grid = MZ_BANK_WGS > 0 ? std::min(total, MZ_BANK_WGS) : mz_build_grid(total, lds);
-  hipLaunchKernelGGL(k_cand_build, dim3(std::max(grid, 1)), dim3(WAVE), lds, s, cd, ids, base, count, n,
-                     C, algo_list, algo_all, dim, seed, epoch);
+  const int total = packed ? (n * C + MZ_PACK - 1) / MZ_PACK : n * C;
+  const int grid = std::max(1, MZ_BANK_WGS > 0 ? std::min(total, MZ_BANK_WGS) : mz_build_grid(total, lds));
+  if (packed)
+    hipLaunchKernelGGL(k_cand_build_packed, dim3(grid), dim3(WAVE), lds, s, cd, ids, base, count, n, C,
+                       algo_all, dim, seed, epoch, (int)stride);
+  else
+    hipLaunchKernelGGL(k_cand_build, dim3(grid), dim3(WAVE), lds, s, cd, ids, base, count, n, C,
+                       algo_list, algo_all, dim, seed, epoch);
   return hipGetLastError();
 }
 
