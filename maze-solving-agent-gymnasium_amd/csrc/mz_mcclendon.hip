@@ -517,9 +517,10 @@ typedef unsigned __int128 u128;
 #endif
 constexpr int MC_LANE_WAVES = MZ_MC_LANE_WAVES;
 
-__global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, int n, int MM, int MK,
-                                                 double* out, int32_t* status, const int* limit,
-                                                 int mult) {
+// one candidate (index i of the list) per call: the body of a one-candidate-per-workgroup kernel,
+// every early return is workgroup-uniform
+__device__ __forceinline__ void mc_score(int i, MzDev d, const int32_t* ids, int n, int MM, int MK,
+                                         double* out, int32_t* status) {
   extern __shared__ __align__(16) unsigned char lds[];
   __shared__ int wsum[T / WAVE];
   __shared__ int s_bad, s_nsol, s_noff, s_open, s_edges, s_Hn, s_Bn, s_nl, s_nw, s_wq;
@@ -528,10 +529,6 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
   __shared__ unsigned long long s_pt[8];
   __shared__ unsigned int s_tmax[2];
 #endif
-  const int i = blockIdx.x;
-  if (i >= n) return;
-  // a bank refill scores the candidates of its consumed slots only: min(*limit, n / mult) groups
-  if (limit && i >= min(*limit, n / mult) * mult) return;
   const int e = ids ? ids[i] : i;
   auto fail = [&](int code) {
     if (threadIdx.x == 0) { out[2 * i] = out[2 * i + 1] = 0.0; status[i] = code; }
@@ -1681,6 +1678,29 @@ __global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, in
   }
 }
 
+// Workgroups score candidates blockIdx.x, + gridDim.x, ... (one workgroup per candidate when the
+// grid is the list; MZ_MC_WGS > 0 caps the resident workgroups of a launch, each then scoring
+// several in turn). A bank refill scores the candidates of its consumed slots only:
+// min(*limit, n / mult) groups of mult.
+#ifndef MZ_MC_WGS
+#define MZ_MC_WGS 0
+#endif
+__global__ __launch_bounds__(T) void k_mcclendon(MzDev d, const int32_t* ids, int n, int MM, int MK,
+                                                 double* out, int32_t* status, const int* limit,
+                                                 int mult) {
+  const int m = limit ? min(*limit, n / mult) * mult : n;
+#if MZ_MC_WGS > 0
+  // (the loop costs the body 208 B of scratch per lane at 128 VGPRs: built only when capped)
+  for (int i = blockIdx.x; i < m; i += gridDim.x) {
+    mc_score(i, d, ids, n, MM, MK, out, status);
+    __syncthreads();  // the next candidate reuses this workgroup's LDS
+  }
+#else
+  if ((int)blockIdx.x < m) mc_score(blockIdx.x, d, ids, n, MM, MK, out, status);
+#endif
+}
+
+
 }  // namespace
 
 size_t mz_mcclendon_lds(int P, bool toroidal, int* mm) {
@@ -1714,7 +1734,8 @@ hipError_t mz_launch_mcclendon(const MzDev& d, const int32_t* ids, int n, double
   }
   int MK = 16;
   while (MK < MM) MK <<= 1;
-  hipLaunchKernelGGL(k_mcclendon, dim3(n), dim3(T), bytes, s, d, ids, n, MM, MK, out, status, limit,
+  const int grid = MZ_MC_WGS > 0 && n > MZ_MC_WGS ? MZ_MC_WGS : n;
+  hipLaunchKernelGGL(k_mcclendon, dim3(grid), dim3(T), bytes, s, d, ids, n, MM, MK, out, status, limit,
                      mult < 1 ? 1 : mult);
   return hipGetLastError();
 }
