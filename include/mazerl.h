@@ -367,10 +367,9 @@ int mz_pair_surrogate(const float* lp_new_dev, const float* lp_old_dev, const fl
  * per parameter, then torch.optim.AdamW) as one launch over a flat f32 parameter buffer whose
  * segment k (length seg_len[k], a multiple of 4) has its gradient at grads_dev[k] (host array of
  * nseg <= 16 device pointers). lr_dev: device f32 learning rate. step_dev: device f32 [1], the
- * step count, advanced by one by the launch itself (so a captured graph advances it per replay;
- * the workgroup ticket that finds the last workgroup is library-owned device memory, one slot
- * per step_dev address, at most 4,096 distinct counters per process). write_grad: store the
- * clamped, grad_scale-scaled gradient back (clamp_ in place). */
+ * step count, advanced by one by the call itself on `stream` (a one-thread launch behind the
+ * update: a captured graph advances it per replay). write_grad: store the clamped,
+ * grad_scale-scaled gradient back (clamp_ in place). */
 int mz_adamw_flat(float* param_dev, float* exp_avg_dev, float* exp_avg_sq_dev,
                   const float* const* grads_dev, const int64_t* seg_len, int32_t nseg,
                   const float* lr_dev, float* step_dev, double beta1, double beta2, double eps,

@@ -18,27 +18,23 @@
 //   m = lerp(m, g, 1 - b1)                               (m + w * (g - m), w < 0.5)
 //   v = v * b2 + (1 - b2) * g * g
 //   p = p - (lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)
-// with t the step count after this step (read as step[0] + 1 by every workgroup; the last
-// workgroup to finish — found with a ticket the library owns — stores it back, so a captured HIP
-// graph advances it on every replay without a second launch) and lr read from the device (the cosine schedule writes it between replays).
+// with t the step count after this step (read as step[0] + 1 by every workgroup; a one-thread
+// launch behind it stores it back, so a captured HIP graph advances it on every replay) and lr
+// read from the device (the cosine schedule writes it between replays).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
 
-#include <map>
-#include <mutex>
-#include <unordered_map>
 
 #include "mz_learner.h"
 
-// k_adamw's grid: every workgroup takes one same-address ticket (publish_step), ~20 ns each at
-// the end of the launch — 2,048 workgroups of 256 made the launch 78 us alone (106 us per vector
-// step inside training) for ~60 MB of traffic; 256 workgroups of 512 (grid-stride beyond):
-// 20.4 us alone, DDQN training 60.8 -> 63-64 M env steps/s (profiles/r02z_adamw/,
-// profiles/exp_adamw_ticket.sh). The cost is each workgroup's fence + atomic round trip, not the
-// shared address: two-level tickets (16 group counters 128 B apart, then a root counter) measured
-// 8.8 vs 7.9 us at 256 workgroups, 12.9 vs 13.7 at 512 (profiles/ubench_ticket.hip,
-// profiles/r05u/ticket.jsonl), and k_adamw / k_head_loss unchanged with them.
+// k_adamw's grid: 256 workgroups of 512 (grid-stride beyond). Round 2 published the step count
+// from the workgroup that took the last of one same-address ticket per workgroup — each
+// workgroup's fence + atomic round trip at the end of the launch (2,048 workgroups of 256: 78 us
+// alone; 256: 20.4 us, ~5 us of it the ticket tail, profiles/ubench_ticket.hip,
+// profiles/r05u/ticket.jsonl; two-level tickets no better). Now a one-thread launch behind
+// k_adamw on the same stream advances it: the kernel boundary orders it after every
+// workgroup's read.
 #ifndef MZ_ADAMW_MAXWG
 #define MZ_ADAMW_MAXWG 256
 #endif
@@ -54,30 +50,12 @@ struct Segs {
   int n;
 };
 
-// The workgroup tickets live in library-owned device memory, one slot per step counter (the
-// caller's step_dev stays a plain f32 [1], mz_adamw_flat's contract): zero at module load, and the
-// last workgroup of every launch puts its slot back to zero. Slots are assigned per step_dev
-// address on the host (mz_launch_adamw) — two optimizers never share one.
-constexpr int ADAMW_TICKETS = 4096;
-__device__ unsigned g_adamw_ticket[ADAMW_TICKETS];
-
-// The last workgroup to take a ticket has seen every other workgroup read step[0] already, and
-// stores the new count.
-__device__ inline void publish_step(float* step, unsigned* ticket, float t) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    if (atomicAdd(ticket, 1u) == gridDim.x - 1) {
-      step[0] = t;
-      *ticket = 0u;
-    }
-  }
-}
+__global__ void k_step_publish(float* step) { step[0] = step[0] + 1.0f; }
 
 __global__ __launch_bounds__(MZ_ADAMW_TPB) void k_adamw(float* __restrict__ p, float* __restrict__ m,
                                                float* __restrict__ v, Segs segs,
                                                const float* __restrict__ lr_dev,
-                                               float* step_dev, unsigned* ticket, double b1,
+                                               const float* step_dev, double b1,
                                                double b2, double eps_d, double wd, float clamp,
                                                float gscale, int write_grad) {
   // the per-step scalars as torch's eager AdamW forms them (Python doubles, then f32 operands)
@@ -123,7 +101,6 @@ __global__ __launch_bounds__(MZ_ADAMW_TPB) void k_adamw(float* __restrict__ p, f
     reinterpret_cast<float4*>(v)[q] = v4;
     if (write_grad) *gp = g4;  // the clamped gradient stays visible, as with clamp_ in place
   }
-  publish_step(step_dev, ticket, t_next);
 }
 
 // ---- PPO's optimizer step (ppo_agent.py:232-236): clip_grad_norm_(params, 0.5), then AdamW
@@ -263,41 +240,13 @@ hipError_t mz_launch_adamw(float* p, float* m, float* v, const float* const* gra
     sg.g[k] = grads[k];
     sg.off[k + 1] = sg.off[k] + seg_len[k];
   }
-  // the ticket slot of this step counter on the current device (assigned on first use; neither
-  // hipGetDevice nor hipGetSymbolAddress is a stream operation, so this also works while a graph
-  // is being captured). The symbol has one instance per device: base and slots are per device.
-  static std::mutex mu;
-  static std::map<std::pair<int, const float*>, int> slots;
-  static std::map<int, int> used;
-  static std::map<int, unsigned*> bases;
-  unsigned* ticket;
-  {
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
-    std::lock_guard<std::mutex> lk(mu);
-    auto b = bases.find(dev);
-    if (b == bases.end()) {
-      void* p = nullptr;
-      e = hipGetSymbolAddress(&p, HIP_SYMBOL(g_adamw_ticket));
-      if (e != hipSuccess) return e;
-      b = bases.emplace(dev, static_cast<unsigned*>(p)).first;
-    }
-    const auto key = std::make_pair(dev, static_cast<const float*>(step));
-    auto it = slots.find(key);
-    if (it == slots.end()) {
-      int& n = used[dev];
-      if (n >= ADAMW_TICKETS) return hipErrorOutOfMemory;
-      it = slots.emplace(key, n++).first;
-    }
-    ticket = b->second + it->second;
-  }
   const int64_t n4 = sg.off[nseg] >> 2;
   int blocks = (int)((n4 + MZ_ADAMW_TPB - 1) / MZ_ADAMW_TPB);
   if (blocks > MZ_ADAMW_MAXWG) blocks = MZ_ADAMW_MAXWG;  // grid-stride beyond
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(k_adamw, dim3(blocks), dim3(MZ_ADAMW_TPB), 0, s, p, m, v, sg, lr, step, ticket, b1, b2, eps, wd,
+  hipLaunchKernelGGL(k_adamw, dim3(blocks), dim3(MZ_ADAMW_TPB), 0, s, p, m, v, sg, lr, step, b1, b2, eps, wd,
                      clamp, gscale, write_grad);
+  hipLaunchKernelGGL(k_step_publish, dim3(1), dim3(1), 0, s, step);
   return hipGetLastError();
 }
 

@@ -73,8 +73,8 @@ def test_flat_params_survive_state_dict_and_copy():
 
 
 def test_flat_adamw_step_counts_are_independent_and_graph_safe():
-    """The step count is a plain f32 [1] (include/mazerl.h mz_adamw_flat); the launch's
-    last-workgroup ticket is library-owned, one slot per counter. Two optimizers interleaved on
+    """The step count is a plain f32 [1] (include/mazerl.h mz_adamw_flat), advanced by a
+    one-thread launch behind the update on the caller's stream. Two optimizers interleaved on
     two streams, eagerly and as captured-graph replays, each advance their own count by exactly
     one per step."""
     from mazerl.agents.flat import FlatAdamW
