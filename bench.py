@@ -450,9 +450,10 @@ def config_legs(a, dev, rank=0, world=1):
                 broadcast_params(tr.net)
             tr.train(20)
             secs = timed_train(tr, a.cfg5_steps, f"config 5 leg ({mode})")
+            ran = tr.stopped_at or a.cfg5_steps  # (the growth leg's max-shape stop may come first)
             rec = {"mode": mode, "envs_per_gpu": B, "dims": [dims[0], dims[-1]], "toroidal": True,
-                   "vector_steps": a.cfg5_steps, "seconds": round(secs, 3),
-                   "env_steps_per_s": B * a.cfg5_steps * world / secs, "updates": tr.updates,
+                   "vector_steps": ran, "seconds": round(secs, 3),
+                   "env_steps_per_s": B * ran * world / secs, "updates": tr.updates,
                    "training_mazes_candidates": C,
                    "grad_allreduce": (dist.get_backend() if world > 1 else None)}
             if growth:

@@ -112,7 +112,13 @@ int mz_generate(mz_handle* h, const int32_t* env_ids_dev, int32_t n, const uint8
  * (candidate c of instance e: seed + e * candidates + c, the mazes mz_generate of
  * n * candidates instances from `seed` builds for instances e * candidates + c), scored by the
  * difficulty kernel, the first minimum copied into the instance (which is then reset like after
- * mz_generate). candidates == 1 is mz_generate_ex(MZ_RNG_PHILOX). Selection statistics:
+ * mz_generate). Euclidean handles score every candidate first with the order-free screen
+ * (mz_screen_batch) and decide a group from it when its minimum is separated from every other
+ * candidate by more than the screen's rigorous error bounds (+ 2^-40); the other groups are
+ * rebuilt and scored by the order-exact kernel (mz_difficulty_batch), and a candidate that kernel
+ * declines is scored by the host restatement (mz_difficulty) inside the stream
+ * (hipLaunchHostFunc), so every candidate of a group is compared. candidates == 1 is
+ * mz_generate_ex(MZ_RNG_PHILOX). Selection statistics:
  * mz_select_stats. Replaces update_new_maze (simple_maze_env.py:118-127) / the env constructors'
  * first maze (simple_maze_env.py:19-36). */
 int mz_generate_best(mz_handle* h, const int32_t* env_ids_dev, int32_t n, const uint8_t* algo_dev,
@@ -125,6 +131,17 @@ int mz_generate_best(mz_handle* h, const int32_t* env_ids_dev, int32_t n, const 
  * tie the chosen one's: the reference would keep the earlier), groups selected. reset != 0 zeroes
  * them after the copy. */
 int mz_select_stats(mz_handle* h, int32_t* out3_dev, int32_t reset, void* stream);
+/* The same counters, the first n (<= MZ_SELECT_STATS) of: [0] unresolved groups (a candidate
+ * with no score from the GPU kernels or the host — or a group past the exact path's per-run cap
+ * of 256, which keeps the screen's pick), [1] near ties (as above), [2] groups selected, [3]
+ * groups the screen left to the order-exact kernel, [4] candidates scored by the host
+ * restatement. */
+#define MZ_SELECT_STATS 5
+int mz_select_stats_ex(mz_handle* h, int32_t* out_dev, int32_t n, int32_t reset, void* stream);
+/* Test hooks of the best-of-C pipeline (flags, 0 = off): 1 every group to the order-exact
+ * kernel, 2 even-numbered candidates treated as declined by it (host-scored), 4 all candidates of
+ * a group from one seed (exact ties). */
+int mz_set_debug(mz_handle* h, int32_t flags);
 /* Per-instance size of a winner's next maze for mz_reset_done / mz_reset_list with regen_won:
  * dims_dev [B] uint8 (device, owned by the caller, read by every later reset launch; NULL = each
  * instance's current size, the default). 0 = the winner keeps its maze and is only reset — the
@@ -422,6 +439,14 @@ int mz_maze_complexity(const uint8_t* grid_host, int32_t h, int32_t w, int32_t s
  * is P + 2; tests/test_abi.py derives both limits from the plan). */
 int mz_difficulty_batch(mz_handle* h, const int32_t* env_ids_dev, int32_t n, double* out_dev,
                         int32_t* status_dev, void* stream);
+/* The order-free McClendon screen (csrc/mz_screen.hip; the best-of-C selection's first stage) of
+ * the listed euclidean instances (NULL = all B): out_dev [n][2] float64 = {prod, e} — the product
+ * prod_b (C_b + 1) * C_0 of maze_complexity_evaluation.py:319-329 summed in an order of its own,
+ * and a rigorous bound e on |prod_ref - prod| / prod for the reference's evaluation order (which
+ * mz_difficulty_batch reproduces); status_dev [n] int32: 0 ok, 2 declined (not a perfect maze on
+ * the odd lattice with a dead-end goal, or beyond the LDS plan). One wave per maze. */
+int mz_screen_batch(mz_handle* h, const int32_t* env_ids_dev, int32_t n, double* out_dev,
+                    int32_t* status_dev, void* stream);
 
 /* The reference's maze-metric suite (MetricsCalculator, metrics_calculator.py:11-133, as used by
  * generation_algos_metrics_evaluations.py:33-45) for the listed euclidean instances (NULL = all B),

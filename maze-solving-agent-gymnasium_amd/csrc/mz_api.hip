@@ -22,11 +22,33 @@
 // Candidate mazes of a best-of-C selection (maze bank refills with C > 1, mz_generate_best): an
 // MzDev view over `cap` scratch instances (cells, plane strips, per-instance words) plus the
 // McClendon output per candidate.
+// Candidates the order-exact kernel declines, scored by the host restatement (mz_difficulty.hip)
+// inside the stream: k_cand_gather writes their grids to mapped host memory, the stream runs
+// host_fallback_fn (hipLaunchHostFunc), k_cand_select reads the products back.
+struct MzHostFallback {
+  int cap = 0, gstride = 0;
+  uint8_t *grid_h = nullptr, *grid_d = nullptr;  // [cap][gstride]
+  int32_t *info_h = nullptr, *info_d = nullptr;  // [cap][5]: N, sr, sc, gr, gc
+  double *prod_h = nullptr, *prod_d = nullptr;   // [cap]
+  int32_t *ok_h = nullptr, *ok_d = nullptr;      // [cap]
+  int32_t* count_h = nullptr;                    // mapped: the gathered count, copied in-stream
+  int* count_d = nullptr;                        // device: k_cand_gather's slot counter
+  int32_t* map = nullptr;                        // device [candidates]: host slot or -1
+};
+
 struct MzCandStore {
   int cap = 0;
   MzDev v{};
   double* score = nullptr;    // [cap][2]: prod_b (C_b + 1) * C_0, sum (k_mcclendon)
   int32_t* status = nullptr;  // [cap]
+  // euclidean handles: the compact candidates, their screen and the per-target pick
+  MzCompact cc{};
+  double* sscore = nullptr;    // [cap][2]: screened product, relative bound (mz_screen.hip)
+  int32_t* sstatus = nullptr;  // [cap]
+  int32_t* pick = nullptr;     // [cap] per target: the candidate, -1 = the exact path
+  int32_t* xlist = nullptr;    // [kXCap] targets for the order-exact kernel
+  int* xcount = nullptr;
+  MzHostFallback hf;
 };
 
 struct MzBankStore {  // two banks x the enabled algorithms x sizes x K slots (mz_bank_*)
@@ -56,7 +78,12 @@ struct mz_handle {
   size_t staging_bytes = 0;
   MzBankStore bank;
   MzCandStore gen;             // mz_generate_best's candidates (chunks of the instance list)
-  int* sel_stats = nullptr;    // [4] best-of-C selections: unresolved groups, near ties, groups
+  int* sel_stats = nullptr;    // [8] best-of-C selections: unresolved groups, near ties, groups,
+                               // groups the screen left to the exact kernel, host-scored candidates
+  int dbg = 0;                 // MZ_DBG_* test hooks of the best-of-C pipeline (mz_set_debug)
+  std::vector<void*> host_allocs;  // mapped page-locked host memory (hipHostFree)
+  MzCompact scr{};             // mz_screen_batch's compact scratch
+  int scr_cap = 0;
 };
 
 namespace {
@@ -148,6 +175,50 @@ int alloc(mz_handle* h, T** p, size_t count) {
   return MZ_OK;
 }
 
+template <typename T>
+int host_alloc(mz_handle* h, T** hp, T** dp, size_t count) {
+  void* q = nullptr;
+  hipError_t e = hipHostMalloc(&q, count * sizeof(T) + 64, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e != hipSuccess) return fail(MZ_ENOMEM, "hipHostMalloc(%zu): %s", count * sizeof(T), hipGetErrorString(e));
+  h->host_allocs.push_back(q);
+  std::memset(q, 0, count * sizeof(T) + 64);
+  void* d = nullptr;
+  e = hipHostGetDevicePointer(&d, q, 0);
+  if (e != hipSuccess) return fail(MZ_EHIP, "hipHostGetDevicePointer: %s", hipGetErrorString(e));
+  *hp = static_cast<T*>(q);
+  *dp = static_cast<T*>(d);
+  return MZ_OK;
+}
+
+constexpr int kXCap = 256;  // targets per best-of-C run the order-exact kernel can take
+constexpr int kHCap = 256;  // declined candidates per run the host restatement can take
+
+int compact_alloc(mz_handle* h, MzCompact& cc, int cap) {
+  const int Qp = (mz_compact_qp(h->d.P) + 15) & ~15;
+  cc.Qp = Qp;
+  cc.QWp = (Qp + 31) / 32;
+  int rc;
+  if ((rc = alloc(h, &cc.pas, (size_t)cap * Qp)) || (rc = alloc(h, &cc.dist, (size_t)cap * Qp)) ||
+      (rc = alloc(h, &cc.sol, (size_t)cap * cc.QWp)) || (rc = alloc(h, &cc.meta, (size_t)cap)))
+    return rc;
+  return MZ_OK;
+}
+
+// the host restatement of the candidates k_cand_gather listed (runs on a HIP runtime thread in
+// stream order: no HIP calls here)
+void host_fallback_fn(void* arg) {
+  MzHostFallback* f = static_cast<MzHostFallback*>(arg);
+  const int n = std::min(*f->count_h, f->cap);
+  for (int i = 0; i < n; ++i) {
+    const int32_t* in = f->info_h + 5 * (size_t)i;
+    double p = 0.0;
+    const int rc = mz_mcclendon_host_prod(f->grid_h + (size_t)i * f->gstride, in[0], in[0], in[1],
+                                          in[2], in[3], in[4], &p);
+    f->prod_h[i] = p;
+    f->ok_h[i] = rc == MZ_OK && p > 0.0;
+  }
+}
+
 // scratch for `cap` candidate mazes: a view of the handle's layout over its own arrays
 int cand_alloc(mz_handle* h, MzCandStore& cs, int cap) {
   const MzDev& d = h->d;
@@ -165,7 +236,72 @@ int cand_alloc(mz_handle* h, MzCandStore& cs, int cap) {
   v.regen_dim = nullptr;
   cs.v = v;
   cs.cap = cap;
+  MzHostFallback& hf = cs.hf;
+  int32_t* count_dview = nullptr;  // (the count's device view: unused, the copy lands on the host)
+  hf.cap = kHCap;
+  hf.gstride = (d.P + 2) * (d.P + 2);
+  if ((rc = host_alloc(h, &hf.grid_h, &hf.grid_d, (size_t)hf.cap * hf.gstride)) ||
+      (rc = host_alloc(h, &hf.info_h, &hf.info_d, (size_t)hf.cap * 5)) ||
+      (rc = host_alloc(h, &hf.prod_h, &hf.prod_d, (size_t)hf.cap)) ||
+      (rc = host_alloc(h, &hf.ok_h, &hf.ok_d, (size_t)hf.cap)) ||
+      (rc = host_alloc(h, &hf.count_h, &count_dview, 1)) || (rc = alloc(h, &hf.count_d, 1)) ||
+      (rc = alloc(h, &hf.map, n)))
+    return rc;
+  if (!d.toroidal) {
+    if ((rc = compact_alloc(h, cs.cc, cap)) || (rc = alloc(h, &cs.sscore, 2 * n)) ||
+        (rc = alloc(h, &cs.sstatus, n)) || (rc = alloc(h, &cs.pick, n)) ||
+        (rc = alloc(h, &cs.xlist, (size_t)kXCap)) || (rc = alloc(h, &cs.xcount, 1)))
+      return rc;
+  }
   return MZ_OK;
+}
+
+// The order-exact selection of the first min(*count, n) listed groups (count null: n):
+// k_mcclendon's scores (already in cs.score / cs.status for candidates j * C + c), the declined
+// candidates scored on the host, the first minimum into dst (k_cand_select).
+int exact_select(mz_handle* h, MzCandStore& cs, const MzDev& dst, const int32_t* ids, int base,
+                 const int* count, int n, int C, const int32_t* xlist, int count_groups,
+                 hipStream_t s) {
+  MzHostFallback& hf = cs.hf;
+  MZ_HIP(hipMemsetAsync(hf.count_d, 0, sizeof(int), s));
+  MZ_HIP(mz_launch_cand_gather(cs.v, count, n, C, cs.status, hf.map, hf.grid_d, hf.info_d,
+                               hf.count_d, hf.cap, hf.gstride, s, h->dbg));
+  MZ_HIP(hipMemcpyAsync(hf.count_h, hf.count_d, sizeof(int), hipMemcpyDeviceToHost, s));
+  MZ_HIP(hipLaunchHostFunc(s, host_fallback_fn, &hf));
+  MZ_HIP(mz_launch_cand_select(cs.v, dst, ids, base, count, n, C, cs.score, cs.status,
+                               h->sel_stats, s, xlist, hf.map, hf.prod_d, hf.ok_d, hf.cap,
+                               count_groups, h->dbg));
+  return MZ_OK;
+}
+
+// Best-of-C over the first min(*count, n) targets (count null: n): target j's C Philox
+// candidates (mz_cand_seed of id(j) = ids ? ids[j] : base + j), the first minimum of McClendon
+// difficulty into dst instance id(j) (BaseMazeEnv.generate_maze, base_maze_env.py:78-97).
+// Euclidean: compact candidates, the order-free screen, a pick where the screen's bounds decide
+// and tables for it (k_cand_expand); the groups it cannot decide (none in practice) through the
+// order-exact kernel on rebuilt candidates. Toroidal: the order-exact kernel on every candidate.
+int bestof_run(mz_handle* h, MzCandStore& cs, const MzDev& dst, const int32_t* ids, int base,
+               const int* count, int n, int C, const uint8_t* algo_list, int algo_all, int dim,
+               uint64_t seed, uint32_t epoch, hipStream_t s) {
+  const MzDev& cv = cs.v;
+  const int dbg = h->dbg;
+  if (cs.cc.Qp > 0) {
+    MZ_HIP(mz_launch_cand_compact(cs.cc, h->d.P, ids, base, count, n, C, algo_list, algo_all, dim,
+                                  seed, epoch, s, dbg));
+    MZ_HIP(mz_launch_screen(cs.cc, h->d.P, n * C, cs.sscore, cs.sstatus, s, count, C));
+    MZ_HIP(hipMemsetAsync(cs.xcount, 0, sizeof(int), s));
+    MZ_HIP(mz_launch_cand_pick(count, n, C, cs.sscore, cs.sstatus, cs.pick, cs.xlist, cs.xcount,
+                               kXCap, h->sel_stats, s, dbg));
+    MZ_HIP(mz_launch_cand_expand(cs.cc, dst, ids, base, count, n, C, cs.pick, algo_list, algo_all, s));
+    const int xc = std::min(kXCap, std::min(n, cs.cap / C));
+    MZ_HIP(mz_launch_cand_rebuild(cv, cs.xlist, cs.xcount, xc, ids, base, C, algo_list, algo_all,
+                                  dim, seed, epoch, s, dbg));
+    MZ_HIP(mz_launch_mcclendon(cv, nullptr, xc * C, cs.score, cs.status, s, cs.xcount, C));
+    return exact_select(h, cs, dst, ids, base, cs.xcount, xc, C, cs.xlist, 0, s);
+  }
+  MZ_HIP(mz_launch_cand_build(cv, ids, base, count, n, C, algo_list, algo_all, dim, seed, epoch, s, dbg));
+  MZ_HIP(mz_launch_mcclendon(cv, nullptr, n * C, cs.score, cs.status, s, count, C));
+  return exact_select(h, cs, dst, ids, base, count, n, C, nullptr, 1, s);
 }
 
 }  // namespace
@@ -205,7 +341,7 @@ int mz_create(const mz_config* cfg, mz_handle** out) {
       (rc = alloc(h, &d.meta0, B)) ||
       (rc = alloc(h, &d.meta1, B)) || (rc = alloc(h, &d.posw, B)) || (rc = alloc(h, &d.stw, B)) ||
       (rc = alloc(h, &d.curw, B)) || (rc = alloc(h, &d.algo, B)) || (rc = alloc(h, &d.last_term, B)) ||
-      (rc = alloc(h, &d.ticket, 16)) || (rc = alloc(h, &h->sel_stats, 4))) {
+      (rc = alloc(h, &d.ticket, 16)) || (rc = alloc(h, &h->sel_stats, 8))) {
     mz_destroy(h);
     return rc;
   }
@@ -232,6 +368,7 @@ int mz_destroy(mz_handle* h) {
   DeviceGuard g(h->cfg.device);
   (void)hipDeviceSynchronize();
   for (void* p : h->allocs) (void)hipFree(p);
+  for (void* p : h->host_allocs) (void)hipHostFree(p);
   if (h->staging) (void)hipFree(h->staging);
   delete h;
   return MZ_OK;
@@ -643,12 +780,9 @@ int mz_bank_fill(mz_handle* h, int32_t bank, uint64_t seed, void* stream) {
     // (size index di = 0 keeps the single-size bank's keys)
     const uint64_t key = seed ^ ((uint64_t)(3 * bank + a + 1) << 56) ^ ((uint64_t)di << 48);
     if (b.C > 1) {  // best-of-C: candidates, their difficulty, the first minimum into the slot
-      const MzDev& cv = b.cand.v;
-      MZ_HIP(mz_launch_cand_build(cv, nullptr, 0, head, b.K, b.C, nullptr, a, b.dims[di], key,
-                                  b.epoch[bank], s));
-      MZ_HIP(mz_launch_mcclendon(cv, nullptr, b.K * b.C, b.cand.score, b.cand.status, s, head, b.C));
-      MZ_HIP(mz_launch_cand_select(cv, bd, nullptr, 0, head, b.K, b.C, b.cand.score, b.cand.status,
-                                   h->sel_stats, s));
+      int rc = bestof_run(h, b.cand, bd, nullptr, 0, head, b.K, b.C, nullptr, a, b.dims[di], key,
+                          b.epoch[bank], s);
+      if (rc) return rc;
     } else {
       MZ_HIP(mz_launch_cand_build(bd, nullptr, 0, head, b.K, 1, nullptr, a, b.dims[di], key,
                                   b.epoch[bank], s));
@@ -749,25 +883,54 @@ int mz_generate_best(mz_handle* h, const int32_t* env_ids_dev, int32_t n, const 
     if (h->gen.cap) MZ_HIP(hipStreamSynchronize(s));  // (the old scratch stays owned by the handle)
     if ((rc = cand_alloc(h, h->gen, chunk * candidates))) return rc;
   }
-  const MzDev& cv = h->gen.v;
   for (int j0 = 0; j0 < n; j0 += chunk) {
     const int m = std::min(chunk, n - j0);
     const int32_t* ids = env_ids_dev ? env_ids_dev + j0 : nullptr;
     const uint8_t* al = algo_dev ? algo_dev + j0 : nullptr;
-    MZ_HIP(mz_launch_cand_build(cv, ids, j0, nullptr, m, candidates, al, algo_all, dim, seed, 0u, s));
-    MZ_HIP(mz_launch_mcclendon(cv, nullptr, m * candidates, h->gen.score, h->gen.status, s));
-    MZ_HIP(mz_launch_cand_select(cv, h->d, ids, j0, nullptr, m, candidates, h->gen.score,
-                                 h->gen.status, h->sel_stats, s));
+    if ((rc = bestof_run(h, h->gen, h->d, ids, j0, nullptr, m, candidates, al, algo_all, dim, seed,
+                         0u, s)))
+      return rc;
   }
   return MZ_OK;
 }
 
 int mz_select_stats(mz_handle* h, int32_t* out3_dev, int32_t reset, void* stream) {
-  if (!h) return fail(MZ_EINVAL, "null handle");
+  return mz_select_stats_ex(h, out3_dev, 3, reset, stream);
+}
+
+int mz_select_stats_ex(mz_handle* h, int32_t* out_dev, int32_t n, int32_t reset, void* stream) {
+  if (!h || n < 0 || n > MZ_SELECT_STATS) return fail(MZ_EINVAL, "bad arguments");
   DeviceGuard g(h->cfg.device);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (out3_dev) MZ_HIP(hipMemcpyAsync(out3_dev, h->sel_stats, 3 * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
-  if (reset) MZ_HIP(hipMemsetAsync(h->sel_stats, 0, 4 * sizeof(int32_t), s));
+  if (out_dev && n) MZ_HIP(hipMemcpyAsync(out_dev, h->sel_stats, n * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+  if (reset) MZ_HIP(hipMemsetAsync(h->sel_stats, 0, 8 * sizeof(int32_t), s));
+  return MZ_OK;
+}
+
+int mz_set_debug(mz_handle* h, int32_t flags) {
+  if (!h) return fail(MZ_EINVAL, "null handle");
+  if (flags & ~7) return fail(MZ_EINVAL, "debug flags %d", flags);
+  h->dbg = flags;
+  return MZ_OK;
+}
+
+int mz_screen_batch(mz_handle* h, const int32_t* env_ids_dev, int32_t n, double* out_dev,
+                    int32_t* status_dev, void* stream) {
+  if (!h || !out_dev || !status_dev) return fail(MZ_EINVAL, "bad arguments");
+  if (h->d.toroidal) return fail(MZ_EINVAL, "the screen scores euclidean mazes");
+  if (!env_ids_dev) n = h->d.B;
+  if (n < 0 || (!env_ids_dev && n > h->d.B)) return fail(MZ_EINVAL, "n out of range");
+  if (n == 0) return MZ_OK;
+  DeviceGuard g(h->cfg.device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (h->scr_cap < n) {
+    if (h->scr_cap) MZ_HIP(hipStreamSynchronize(s));  // (the old scratch stays owned by the handle)
+    int rc = compact_alloc(h, h->scr, n);
+    if (rc) return rc;
+    h->scr_cap = n;
+  }
+  MZ_HIP(mz_launch_compact_from_handle(h->d, env_ids_dev, n, h->scr, s));
+  MZ_HIP(mz_launch_screen(h->scr, h->d.P, n, out_dev, status_dev, s));
   return MZ_OK;
 }
 

@@ -13,6 +13,7 @@
 //               max_steps (set_max_steps simple_maze_env.py:52-58), reset state.
 #pragma once
 #include "mz_common.h"
+#include "mz_screen.h"
 
 // Distance fields of Philox-generated mazes from the carved tree (mz_tree_dist) instead of
 // level-synchronous BFS; 0 = the BFS everywhere (A/B builds)
@@ -807,8 +808,10 @@ __device__ int mz_cs_goal(const MzCellLds& L, int N, int s) {
 
 // Distance to the goal cell of every cell, in squares, into L.A: mz_tree_dist in cell space
 // (parents are the neighbours across an open passage at depth - 2); a cell-space BFS when the
-// tree walk fails (never for these generators) or MZ_TREE_DIST is 0.
-__device__ void mz_cs_dist(const MzCellLds& L, int s, int goal) {
+// tree walk fails (never for these generators) or MZ_TREE_DIST is 0. Returns true when the tree
+// walk ran: L.b1 then holds the goal's root path in the start-rooted carve tree, i.e. the
+// solution path's cells (the BFS leaves its visited bits there instead).
+__device__ bool mz_cs_dist(const MzCellLds& L, int s, int goal) {
   const int lane = threadIdx.x, Q = L.Q, W = L.W;
   bool ok = MZ_TREE_DIST;
   if (ok) {
@@ -866,7 +869,7 @@ __device__ void mz_cs_dist(const MzCellLds& L, int s, int goal) {
       L.A[q] = (uint16_t)((int)L.dep[q] + dg - 2 * (int)L.dep[a]);
     }
     __syncthreads();
-    return;
+    return true;
   }
   // level-synchronous BFS over the cells from the goal (distances in squares; the carve depths
   // are not needed any more: their array is the queue)
@@ -902,6 +905,7 @@ __device__ void mz_cs_dist(const MzCellLds& L, int s, int goal) {
     tail = L.sh[0];
     __syncthreads();
   }
+  return false;
 }
 
 // Toroidal mazes (gen_maze_no_border, maze_generation.py:37-56): generated in cell space on the
@@ -938,11 +942,55 @@ __device__ inline void mz_cells_clear(const MzCellLds& L) {
 __device__ __forceinline__ void mz_cells_finish(const MzDev& d, int e, const MzCellLds& L, int N,
                                                 bool tor);
 
-__device__ __forceinline__ void mz_build_cells(const MzDev& d, int e, int algo, uint64_t seed, int N,
-                                               bool tor, uint8_t* lds) {
+// Tables of instance e (cell words, plane strips, meta / reset state) from a euclidean cell-space
+// maze in LDS: passages L.pas, distances to the goal L.A (squares), start / goal cells s / goal.
+__device__ __forceinline__ void mz_cells_tables(const MzDev& d, int e, const MzCellLds& L, int N,
+                                                int s, int goal) {
+  const int W = L.W;
+  auto open_g = [&](int r, int c) -> bool {
+    const bool ro = r & 1, co = c & 1;
+    if (ro && co) return true;  // every cell is in the tree
+    if (!ro && !co) return false;
+    if (ro) return c > 0 && c < N - 1 && (L.pas[(r >> 1) * W + ((c - 1) >> 1)] & 1);
+    return r > 0 && r < N - 1 && (L.pas[((r - 1) >> 1) * W + (c >> 1)] & 2);
+  };
+  auto dist = [&](int r, int c) -> int {  // open squares: a passage is one step from its nearer cell
+    if ((r & 1) && (c & 1)) return L.A[(r >> 1) * W + (c >> 1)];
+    const int q = (r & 1) ? (r >> 1) * W + ((c - 1) >> 1) : ((r - 1) >> 1) * W + (c >> 1);
+    const int q2 = (r & 1) ? q + 1 : q + W;
+    return min((int)L.A[q], (int)L.A[q2]) + 1;
+  };
+  const int sr = 2 * (s / W) + 1, sc = 2 * (s % W) + 1;
+  const int gr = 2 * (goal / W) + 1, gc = 2 * (goal % W) + 1;
+  mz_build_write(d, e, N, false, sr, sc, gr, gc, open_g, dist);
+}
+
+// A carved euclidean cell-space maze as a best-of-C candidate (mz_screen.h): goal and distance
+// field as mz_cells_finish, then only the compact form leaves LDS — no cell words or planes; the
+// selected candidate's tables are written from it afterwards (k_cand_expand).
+__device__ __forceinline__ void mz_cells_compact(const MzCompact& cc, int t, const MzCellLds& L,
+                                                 int N) {
   const int lane = threadIdx.x;
-  const int G = tor ? N + 2 : N;
-  const MzCellLds L = mz_cell_lds(lds, tor ? d.P + 2 : d.P, G);
+  const int s = L.sh[2];
+  int goal = mz_cs_goal(L, N, s);
+  if (goal < 0) goal = s;  // unreachable for W >= 2 (a spanning tree has >= 2 leaves)
+  const bool sol = mz_cs_dist(L, s, goal);
+  const int Q = L.Q;
+  uint32_t* gp = reinterpret_cast<uint32_t*>(cc.pas + (size_t)t * cc.Qp);
+  uint32_t* ga = reinterpret_cast<uint32_t*>(cc.dist + (size_t)t * cc.Qp);
+  const uint32_t* lp = reinterpret_cast<const uint32_t*>(L.pas);
+  const uint32_t* la = reinterpret_cast<const uint32_t*>(L.A);
+  for (int i = lane; i < (Q + 3) / 4; i += 64) gp[i] = lp[i];
+  for (int i = lane; i < (Q + 1) / 2; i += 64) ga[i] = la[i];
+  for (int i = lane; i < (Q + 31) / 32; i += 64) cc.sol[(size_t)t * cc.QWp + i] = L.b1[i];
+  if (lane == 0)
+    cc.meta[t] = (uint32_t)N | (sol ? 0u : MZ_CMETA_NOSOL) | ((uint32_t)s << 8) | ((uint32_t)goal << 20);
+  __syncthreads();
+}
+
+// the carve of mz_build_cells (wave-wide): passages, carve depths and the start cell (L.sh[2])
+__device__ __forceinline__ void mz_carve_cells(const MzCellLds& L, int algo, uint64_t seed) {
+  const int lane = threadIdx.x;
   const int W = L.W;
   mz_cells_clear(L);
   __syncthreads();
@@ -957,6 +1005,13 @@ __device__ __forceinline__ void mz_build_cells(const MzDev& d, int e, int algo, 
   __syncthreads();
   if (algo != MZ_ALGO_RPRIM_DEV && algo != MZ_ALGO_DFS_DEV) mz_cs_primkill(L, L.sh[2], rng);
   __syncthreads();
+}
+
+__device__ __forceinline__ void mz_build_cells(const MzDev& d, int e, int algo, uint64_t seed, int N,
+                                               bool tor, uint8_t* lds) {
+  const int G = tor ? N + 2 : N;
+  const MzCellLds L = mz_cell_lds(lds, tor ? d.P + 2 : d.P, G);
+  mz_carve_cells(L, algo, seed);
   mz_cells_finish(d, e, L, N, tor);
 }
 
@@ -973,13 +1028,14 @@ __device__ __forceinline__ void mz_build_cells(const MzDev& d, int e, int algo, 
 #define MZ_PACK 4
 #endif
 // e / seed: lane l holds those of maze l >> 4 (lanes of mazes >= nm: unused)
-__device__ __forceinline__ void mz_build_cells_packed(const MzDev& d, int e, uint64_t seed, int nm,
-                                                      int N, int algo, uint8_t* lds, size_t stride) {
+// the carves of mz_build_cells_packed (P: the pitch the LDS regions are laid out for)
+__device__ __forceinline__ void mz_carve_packed(int P, uint64_t seed, int nm, int N, int algo,
+                                                uint8_t* lds, size_t stride) {
   const int lane = threadIdx.x, m = lane >> 4;
-  for (int k = 0; k < nm; ++k) mz_cells_clear(mz_cell_lds(lds + k * stride, d.P, N));
+  for (int k = 0; k < nm; ++k) mz_cells_clear(mz_cell_lds(lds + k * stride, P, N));
   __syncthreads();
   if ((lane & 15) == 0 && m < nm) {
-    const MzCellLds L = mz_cell_lds(lds + m * stride, d.P, N);
+    const MzCellLds L = mz_cell_lds(lds + m * stride, P, N);
     const int W = L.W;
     MzRng rng{seed, 0ull, {0u, 0u, 0u, 0u}};
     const int a = (int)rng.below((uint32_t)W), b = (int)rng.below((uint32_t)W);
@@ -988,6 +1044,11 @@ __device__ __forceinline__ void mz_build_cells_packed(const MzDev& d, int e, uin
     else mz_cs_dfs(L, a * W + b, rng);
   }
   __syncthreads();
+}
+
+__device__ __forceinline__ void mz_build_cells_packed(const MzDev& d, int e, uint64_t seed, int nm,
+                                                      int N, int algo, uint8_t* lds, size_t stride) {
+  mz_carve_packed(d.P, seed, nm, N, algo, lds, stride);
   for (int k = 0; k < nm; ++k) {
     mz_cells_finish(d, __shfl(e, 16 * k), mz_cell_lds(lds + k * stride, d.P, N), N, false);
     __syncthreads();
@@ -1017,17 +1078,11 @@ __device__ __forceinline__ void mz_cells_finish(const MzDev& d, int e, const MzC
   const int gr = 2 * (goal / W) + 1 - off, gc = 2 * (goal % W) + 1 - off;
   if (!tor) {
     if (!(MZ_GPROBE & 2)) mz_cs_dist(L, s, goal);
-    auto dist = [&](int r, int c) -> int {  // open squares: a passage is one step from its nearer cell
-      if ((r & 1) && (c & 1)) return L.A[(r >> 1) * W + (c >> 1)];
-      const int q = (r & 1) ? (r >> 1) * W + ((c - 1) >> 1) : ((r - 1) >> 1) * W + (c >> 1);
-      const int q2 = (r & 1) ? q + 1 : q + W;
-      return min((int)L.A[q], (int)L.A[q2]) + 1;
-    };
     if (MZ_GPROBE & 1) {  // probe: only the meta words (no cell words / planes)
       if (lane == 0) { d.meta0[e] = (uint32_t)N | ((uint32_t)N << 8) | ((uint32_t)sr << 16) | ((uint32_t)sc << 24); d.meta1[e] = (uint32_t)gr | ((uint32_t)gc << 8); }
       return;
     }
-    mz_build_write(d, e, N, false, sr, sc, gr, gc, open_g, dist);
+    mz_cells_tables(d, e, L, N, s, goal);
     return;
   }
   // torus: BFS from the goal over row masks, in the region after the passages

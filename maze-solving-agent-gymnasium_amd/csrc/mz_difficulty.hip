@@ -236,7 +236,7 @@ std::vector<std::vector<int>> components(const Graph& G, const std::unordered_se
 
 // difficulty_of_maze (:319-329) and complexity_of_maze (:311-317) of one euclidean grid
 int mcclendon(const uint8_t* g, int32_t H, int32_t W, int32_t sr, int32_t sc, int32_t gr,
-              int32_t gc, double* difficulty, double* complexity) {
+              int32_t gc, double* difficulty, double* complexity, double* prod_out = nullptr) {
   if (!g || H < 3 || W < 3) return MZ_EINVAL;
   auto open = [&](int r, int c) { return g[r * W + c] != 0; };
   auto nbrs = [&](int v) {
@@ -413,6 +413,7 @@ int mcclendon(const uint8_t* g, int32_t H, int32_t W, int32_t sr, int32_t sc, in
   const double c0 = hallway_complexity(H0, d_sol, h0_nodes, h0_order);  // branch 0 = [0], last
   prod *= c0;
   sum += c0;
+  if (prod_out) *prod_out = prod;
   if (difficulty) {
     if (!(prod > 0.0)) return MZ_EINVAL;  // math.log domain error in the reference
     *difficulty = std::log(prod);
@@ -436,4 +437,12 @@ extern "C" int mz_maze_complexity(const uint8_t* g, int32_t H, int32_t W, int32_
                                   int32_t gr, int32_t gc, double* difficulty, double* complexity) {
   if (!difficulty && !complexity) return MZ_EINVAL;
   return mcclendon(g, H, W, sr, sc, gr, gc, difficulty, complexity);
+}
+
+// The product difficulty_of_maze takes the log of (the quantity k_mcclendon outputs): the
+// best-of-C selection's host fallback for candidates the GPU kernel declines (mz_api.hip).
+int mz_mcclendon_host_prod(const uint8_t* g, int32_t H, int32_t W, int32_t sr, int32_t sc,
+                           int32_t gr, int32_t gc, double* prod) {
+  if (!prod) return MZ_EINVAL;
+  return mcclendon(g, H, W, sr, sc, gr, gc, nullptr, nullptr, prod);
 }

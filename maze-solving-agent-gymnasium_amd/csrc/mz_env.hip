@@ -698,7 +698,8 @@ __global__ __launch_bounds__(BS_T) void k_bank_scan(MzDev d) {
 // Candidate builds (one wave per maze, persistent): target j of a list of n targets (n = the
 // static count, or min(*count, n) — a bank block's slots consumed since its last fill) gets C
 // candidate mazes at indices j * C + c of the view `cd`, Philox seed
-//   seed + (id(j) * C + c) + (epoch << 32),   id(j) = ids ? ids[j] : base + j,
+//   mz_cand_seed(seed, id(j), C, c, epoch) = seed + (id(j) * C + c) + (epoch << 32),
+//   id(j) = ids ? ids[j] : base + j,
 // so C = 1 with cd = the bank block is the bank's own fill (seed + slot + epoch << 32), and
 // C > 1 over the instances of a handle draws the candidates best_of_mazes draws for those
 // instances (VectorMazeEnv.generate of n * C instances from `seed`: candidate c of maze k is
@@ -709,7 +710,7 @@ __global__ __launch_bounds__(BS_T) void k_bank_scan(MzDev d) {
 __global__ __launch_bounds__(WAVE) void k_cand_build_packed(MzDev cd, const int32_t* ids, int base,
                                                             const int* count, int n, int C,
                                                             int algo, int dim, uint64_t seed,
-                                                            uint32_t epoch, int stride) {
+                                                            uint32_t epoch, int stride, int dbg) {
   extern __shared__ __align__(16) uint8_t lds[];
   const int used = count ? min(*count, n) : n;
   const int total = used * C, m = threadIdx.x >> 4;
@@ -719,8 +720,8 @@ __global__ __launch_bounds__(WAVE) void k_cand_build_packed(MzDev cd, const int3
     const int j = t / C, c = t - j * C;
     const uint64_t id = (uint64_t)(ids ? ids[j] : base + j);
     if ((threadIdx.x & 15) == 0 && m < nm) cd.algo[t] = (uint8_t)algo;
-    mz_build_cells_packed(cd, t, seed + id * (uint64_t)C + (uint64_t)c + ((uint64_t)epoch << 32), nm,
-                          dim, algo, lds, (size_t)stride);
+    mz_build_cells_packed(cd, t, mz_cand_seed(seed, id, C, c, epoch, dbg), nm, dim, algo, lds,
+                          (size_t)stride);
     __syncthreads();
   }
 }
@@ -728,7 +729,8 @@ __global__ __launch_bounds__(WAVE) void k_cand_build_packed(MzDev cd, const int3
 __global__ __launch_bounds__(WAVE) void k_cand_build(MzDev cd, const int32_t* ids, int base,
                                                      const int* count, int n, int C,
                                                      const uint8_t* algo_list, int algo_all,
-                                                     int dim, uint64_t seed, uint32_t epoch) {
+                                                     int dim, uint64_t seed, uint32_t epoch,
+                                                     int dbg) {
   extern __shared__ __align__(16) uint8_t lds[];
   const int used = count ? min(*count, n) : n;
   for (int t = blockIdx.x; t < used * C; t += gridDim.x) {
@@ -736,35 +738,299 @@ __global__ __launch_bounds__(WAVE) void k_cand_build(MzDev cd, const int32_t* id
     const int algo = algo_list ? algo_list[j] : algo_all;
     const uint64_t id = (uint64_t)(ids ? ids[j] : base + j);
     if (threadIdx.x == 0) cd.algo[t] = (uint8_t)algo;
-    mz_build_one(cd, t, cd.toroidal, true, algo, seed + id * (uint64_t)C + (uint64_t)c +
-                 ((uint64_t)epoch << 32), dim, nullptr, 0, 0, 0, 0, lds);
+    mz_build_one(cd, t, cd.toroidal, true, algo, mz_cand_seed(seed, id, C, c, epoch, dbg), dim,
+                 nullptr, 0, 0, 0, 0, lds);
     __syncthreads();
   }
 }
 
-// Best-of-C selection (BaseMazeEnv.generate_maze, base_maze_env.py:78-97; toroidal
-// toroidal_maze_env.py:40-54): target j keeps the candidate with the smallest McClendon
-// difficulty, the FIRST one on ties (the reference replaces only on a strict `<`). The kernel
-// compares prod_b (C_b + 1) * C_0 (k_mcclendon's output, whose math.log the reference compares):
-// log is monotone, so the first minimum of the products is the first minimum of the logs except
-// when two different products round to the same log — counted in stats[1] (a candidate within a
-// relative 2^-40 of the minimum, listed before it), never seen on the fixtures. A group with a
-// candidate the kernel left to the host (status != 0: not a tree, a hallway beyond the wave's set
-// table, ...) picks among the others and is counted in stats[0]; stats[2] counts the groups.
-// One wave per target: the chosen candidate's cells, plane strips and per-instance words are
-// copied into dst instance dst_ids[j] (or base + j).
-__global__ __launch_bounds__(WAVE) void k_cand_select(MzDev cd, MzDev dst, const int32_t* dst_ids,
-                                                      int base, const int* count, int n, int C,
-                                                      const double* score, const int32_t* status,
-                                                      int* stats) {
+// Euclidean Philox candidates in compact form (mz_screen.h): the carve, goal and distance field
+// of k_cand_build_packed / k_cand_build, but no cell words or plane strips — 4.8 KB per 81 x 81
+// candidate leave the CU instead of 29 KB, and only the selected one gets tables
+// (k_cand_expand). The same seeds, so the same mazes.
+__global__ __launch_bounds__(WAVE) void k_cand_compact_packed(MzCompact cc, int P, const int32_t* ids,
+                                                              int base, const int* count, int n,
+                                                              int C, int algo, int dim,
+                                                              uint64_t seed, uint32_t epoch,
+                                                              int stride, int dbg) {
+  extern __shared__ __align__(16) uint8_t lds[];
+  const int used = count ? min(*count, n) : n;
+  const int total = used * C, m = threadIdx.x >> 4;
+  for (int t0 = blockIdx.x * MZ_PACK; t0 < total; t0 += gridDim.x * MZ_PACK) {
+    const int nm = min(MZ_PACK, total - t0);
+    const int t = t0 + min(m, nm - 1);
+    const int j = t / C, c = t - j * C;
+    const uint64_t id = (uint64_t)(ids ? ids[j] : base + j);
+    mz_carve_packed(P, mz_cand_seed(seed, id, C, c, epoch, dbg), nm, dim, algo, lds, (size_t)stride);
+    for (int k = 0; k < nm; ++k) mz_cells_compact(cc, t0 + k, mz_cell_lds(lds + k * stride, P, dim), dim);
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(WAVE) void k_cand_compact(MzCompact cc, int P, const int32_t* ids,
+                                                       int base, const int* count, int n, int C,
+                                                       const uint8_t* algo_list, int algo_all,
+                                                       int dim, uint64_t seed, uint32_t epoch,
+                                                       int dbg) {
+  extern __shared__ __align__(16) uint8_t lds[];
+  const int used = count ? min(*count, n) : n;
+  for (int t = blockIdx.x; t < used * C; t += gridDim.x) {
+    const int j = t / C, c = t - j * C;
+    const int algo = algo_list ? algo_list[j] : algo_all;
+    const uint64_t id = (uint64_t)(ids ? ids[j] : base + j);
+    const MzCellLds L = mz_cell_lds(lds, P, dim);
+    mz_carve_cells(L, algo, mz_cand_seed(seed, id, C, c, epoch, dbg));
+    mz_cells_compact(cc, t, L, dim);
+    __syncthreads();
+  }
+}
+
+// Best-of-C decision from the screen (mz_screen.hip): target j keeps candidate a, the first
+// minimum of the screened products, when every other candidate c is provably larger in the
+// reference's own float evaluation as well: p_c (1 - e_c) > p_a (1 + e_a) (1 + 2^-40) — the e's
+// bound each screened product's distance from the reference's product, and the 2^-40 keeps the
+// two logs the reference compares apart (base_maze_env.py:78-97 keeps the first strict minimum of
+// math.log). Any other group (a candidate the screen declined, or two candidates within the
+// bounds) is listed for the order-exact kernel (k_mcclendon), at most xcap of them per launch;
+// a group past that cap keeps the screen's pick and is counted unresolved. stats: [0] unresolved
+// groups, [2] groups, [3] groups sent to the exact kernel.
+__global__ __launch_bounds__(WAVE) void k_cand_pick(const int* count, int n, int C,
+                                                    const double* score, const int32_t* status,
+                                                    int32_t* pick, int32_t* xlist, int* xcount,
+                                                    int xcap, int* stats, int dbg) {
   const int used = count ? min(*count, n) : n;
   const int lane = threadIdx.x;
   for (int j = blockIdx.x; j < used; j += gridDim.x) {
     const int t0 = j * C;
     const bool ok = lane < C && status[t0 + lane] == 0;
     const double p = lane < C ? score[2 * (t0 + lane)] : 0.0;
+    const double e = lane < C ? score[2 * (t0 + lane) + 1] : 0.0;
     const unsigned long long okm = __ballot(ok);
-    // first minimum over the resolvable candidates (wave-uniform loop over C <= 64)
+    int a = 0;
+    double best = 0.0;
+    bool have = false;
+    for (int c = 0; c < C; ++c) {  // wave-uniform
+      if (!((okm >> c) & 1ull)) continue;
+      const double pc = __shfl(p, c);
+      if (!have || pc < best) { best = pc; a = c; have = true; }
+    }
+    const double ea = __shfl(e, a);
+    const double hi = __dmul_rn(__dmul_rn(best, __dadd_rn(1.0, ea)), 1.0 + 0x1p-40);
+    const bool sep = lane >= C || lane == a || __dmul_rn(p, __dsub_rn(1.0, e)) > hi;
+    const bool all_ok = okm == ((C >= 64) ? ~0ull : ((1ull << C) - 1ull));
+    const bool decided = all_ok && __all(sep) && !(dbg & MZ_DBG_SCREEN_OFF);
+    if (lane == 0) {
+      int pk = a;
+      if (!decided) {
+        const int k = atomicAdd(xcount, 1);
+        if (k < xcap) {
+          xlist[k] = j;
+          pk = -1;
+          atomicAdd(stats + 3, 1);
+        } else {
+          atomicAdd(stats + 0, 1);
+        }
+      }
+      pick[j] = pk;
+      atomicAdd(stats + 2, 1);
+    }
+  }
+}
+
+// Tables of each decided target's chosen candidate, from its compact form, into dst instance
+// dst_ids[j] (or base + j): cell words, plane strips, meta and reset state (mz_cells_tables).
+__global__ __launch_bounds__(WAVE) void k_cand_expand(MzCompact cc, MzDev dst, const int32_t* dst_ids,
+                                                      int base, const int* count, int n, int C,
+                                                      const int32_t* pick, const uint8_t* algo_list,
+                                                      int algo_all) {
+  extern __shared__ __align__(16) uint8_t lds[];
+  const int used = count ? min(*count, n) : n;
+  const int lane = threadIdx.x;
+  for (int j = blockIdx.x; j < used; j += gridDim.x) {
+    const int pk = pick[j];
+    if (pk < 0) continue;  // wave-uniform
+    const size_t t = (size_t)j * C + pk;
+    const uint32_t meta = cc.meta[t];
+    const int N = meta & 0x7F, s = (int)((meta >> 8) & 0xFFFu), g = (int)(meta >> 20);
+    const MzCellLds L = mz_cell_lds(lds, dst.P, N);
+    const uint32_t* gp = reinterpret_cast<const uint32_t*>(cc.pas + t * cc.Qp);
+    const uint32_t* ga = reinterpret_cast<const uint32_t*>(cc.dist + t * cc.Qp);
+    uint32_t* lp = reinterpret_cast<uint32_t*>(L.pas);
+    uint32_t* la = reinterpret_cast<uint32_t*>(L.A);
+    for (int i = lane; i < (L.Q + 3) / 4; i += WAVE) lp[i] = gp[i];
+    for (int i = lane; i < (L.Q + 1) / 2; i += WAVE) la[i] = ga[i];
+    __syncthreads();
+    const int de = dst_ids ? dst_ids[j] : base + j;
+    if (lane == 0) dst.algo[de] = (uint8_t)(algo_list ? algo_list[j] : algo_all);
+    mz_cells_tables(dst, de, L, N, s, g);
+    __syncthreads();
+  }
+}
+
+// The exact path's candidates: listed target k (= xlist[k], k < *xcount) gets its C candidates
+// built with tables at indices k * C + c of `cd` — the same seeds, so the same mazes as its
+// compact builds.
+__global__ __launch_bounds__(WAVE) void k_cand_rebuild(MzDev cd, const int32_t* xlist, const int* xcount,
+                                                       int xcap, const int32_t* ids, int base, int C,
+                                                       const uint8_t* algo_list, int algo_all, int dim,
+                                                       uint64_t seed, uint32_t epoch, int dbg) {
+  extern __shared__ __align__(16) uint8_t lds[];
+  const int used = min(*xcount, xcap);
+  for (int t = blockIdx.x; t < used * C; t += gridDim.x) {
+    const int k = t / C, c = t - k * C;
+    const int j = xlist[k];
+    const int algo = algo_list ? algo_list[j] : algo_all;
+    const uint64_t id = (uint64_t)(ids ? ids[j] : base + j);
+    if (threadIdx.x == 0) cd.algo[t] = (uint8_t)algo;
+    mz_build_one(cd, t, cd.toroidal, true, algo, mz_cand_seed(seed, id, C, c, epoch, dbg), dim,
+                 nullptr, 0, 0, 0, 0, lds);
+    __syncthreads();
+  }
+}
+
+// Candidates of the first min(*count, n) targets that k_mcclendon declined (status != 0; with
+// MZ_DBG_DECLINE_EVEN also every even-numbered one): their evaluated grid (toroidal: the bordered
+// crop the kernel scores, 0 wall / 1 open / 2 goal) and start / goal go to host memory, slot
+// hmap[t] (< hcap; -1: none), for the host restatement (mz_difficulty.hip) that the stream runs
+// next (hipLaunchHostFunc, mz_api.hip).
+__global__ __launch_bounds__(WAVE) void k_cand_gather(MzDev cd, const int* count, int n, int C,
+                                                      const int32_t* status, int32_t* hmap,
+                                                      uint8_t* hgrid, int32_t* hinfo, int* hcount,
+                                                      int hcap, int gstride, int dbg) {
+  const int used = count ? min(*count, n) : n;
+  const int lane = threadIdx.x;
+  for (int t = blockIdx.x; t < used * C; t += gridDim.x) {
+    const bool decl = status[t] != 0 || ((dbg & MZ_DBG_DECLINE_EVEN) && ((t % C) & 1) == 0);
+    if (!decl) {
+      if (lane == 0) hmap[t] = -1;
+      continue;
+    }
+    int slot = 0;
+    if (lane == 0) slot = atomicAdd(hcount, 1);
+    slot = __shfl(slot, 0);
+    if (lane == 0) hmap[t] = slot < hcap ? slot : -1;
+    if (slot >= hcap) continue;
+    const bool tor = cd.toroidal;
+    const int P = cd.P, o = tor ? 1 : 0;
+    const uint32_t m0 = cd.meta0[t], m1 = cd.meta1[t];
+    const int Nm = m0 & 0xFF, N = tor ? Nm + 2 : Nm;
+    const int gr = (m1 & 0xFF) + o, gc = ((m1 >> 8) & 0xFF) + o;
+    const uint32_t* cw = cd.cells + (size_t)t * P * P;
+    uint8_t* g = hgrid + (size_t)slot * gstride;
+    for (int q = lane; q < N * N; q += WAVE) {
+      const int r = q / N, c = q - r * N;
+      const bool in = r >= o && r < o + Nm && c >= o && c < o + Nm;
+      const bool op = in && (cw[(r - o) * P + (c - o)] & MZ_CELL_OPEN);
+      g[q] = !op ? 0 : ((r == gr && c == gc) ? 2 : 1);
+    }
+    if (lane == 0) {
+      int32_t* in = hinfo + 5 * (size_t)slot;
+      in[0] = N;
+      in[1] = (int)((m0 >> 16) & 0xFF) + o;
+      in[2] = (int)(m0 >> 24) + o;
+      in[3] = gr;
+      in[4] = gc;
+    }
+  }
+}
+
+// Compact form of resident euclidean mazes (the screen's input, mz_screen.h) from their tables:
+// passages from the open passage squares, distances from the cell words' D field, the solution's
+// cells by walking from the start down the distance field (lane 0). Instances ids[i] (or i) ->
+// compact slot i. Used by mz_screen_batch (the screen checked against the exact kernel on any
+// resident maze); a maze off the odd lattice is flagged MZ_CMETA_NOSOL (the screen declines it).
+__global__ __launch_bounds__(WAVE) void k_compact_from_handle(MzDev d, const int32_t* ids, int n,
+                                                              MzCompact cc) {
+  const int lane = threadIdx.x;
+  for (int i = blockIdx.x; i < n; i += gridDim.x) {
+    const int e = ids ? ids[i] : i;
+    const uint32_t m0 = d.meta0[e], m1 = d.meta1[e];
+    const int N = m0 & 0xFF, sr = (m0 >> 16) & 0xFF, sc = m0 >> 24, gr = m1 & 0xFF, gc = (m1 >> 8) & 0xFF;
+    const int W = (N - 1) / 2, Q = W * W, P = d.P;
+    const uint32_t* cw = d.cells + (size_t)e * P * P;
+    auto open = [&](int r, int c) { return r >= 0 && c >= 0 && r < N && c < N && (cw[r * P + c] & MZ_CELL_OPEN); };
+    bool lattice = !d.toroidal && (N & 1) && N < 128 && (sr & 1) && (sc & 1) && (gr & 1) && (gc & 1);
+    uint8_t* gp = cc.pas + (size_t)i * cc.Qp;
+    uint16_t* ga = cc.dist + (size_t)i * cc.Qp;
+    uint32_t* gs = cc.sol + (size_t)i * cc.QWp;
+    for (int q = lane; q < Q && lattice; q += WAVE) {
+      const int r = 2 * (q / W) + 1, c = 2 * (q % W) + 1;
+      gp[q] = (uint8_t)((open(r, c + 1) && c + 2 < N ? 1 : 0) | (open(r + 1, c) && r + 2 < N ? 2 : 0));
+      ga[q] = (uint16_t)(cw[r * P + c] & MZ_CELL_D_MASK);
+    }
+    for (int k = lane; k < cc.QWp; k += WAVE) gs[k] = 0u;
+    __syncthreads();
+    if (lane == 0 && lattice) {  // start -> goal down the distance field
+      int r = sr, c = sc;
+      for (int it = 0; it <= N * N; ++it) {
+        if ((r & 1) && (c & 1)) {
+          const int q = (r >> 1) * W + (c >> 1);
+          gs[q >> 5] |= 1u << (q & 31);
+        }
+        if (r == gr && c == gc) break;
+        const int D = (int)(cw[r * P + c] & MZ_CELL_D_MASK);
+        int nr = -1, nc = -1;
+        for (int k = 0; k < 4; ++k) {
+          const int rr = r + mz_dr(k), cc2 = c + mz_dc(k);
+          if (open(rr, cc2) && (int)(cw[rr * P + cc2] & MZ_CELL_D_MASK) == D - 1) { nr = rr; nc = cc2; }
+        }
+        if (nr < 0) { lattice = false; break; }
+        r = nr;
+        c = nc;
+      }
+    }
+    lattice = __shfl((int)lattice, 0) != 0;
+    if (lane == 0)
+      cc.meta[i] = (uint32_t)(N & 0x7F) | (lattice ? 0u : MZ_CMETA_NOSOL) |
+                   ((uint32_t)((sr >> 1) * W + (sc >> 1)) << 8) | ((uint32_t)((gr >> 1) * W + (gc >> 1)) << 20);
+    __syncthreads();
+  }
+}
+
+// Best-of-C selection (BaseMazeEnv.generate_maze, base_maze_env.py:78-97; toroidal
+// toroidal_maze_env.py:40-54) from the order-exact scores: target j keeps the candidate with the
+// smallest McClendon difficulty, the FIRST one on ties (the reference replaces only on a strict
+// `<`). The kernel compares prod_b (C_b + 1) * C_0 (k_mcclendon's output, whose math.log the
+// reference compares): log is monotone, so the first minimum of the products is the first minimum
+// of the logs except when two different products round to the same log — counted in stats[1] (a
+// candidate within a relative 2^-40 of the minimum, listed before it), never seen on the
+// fixtures. A candidate the kernel left to the host (status != 0: not a tree, a hallway beyond
+// the wave's set table, ...) takes the host restatement's product (hmap / hprod / hok, gathered
+// by k_cand_gather); a group with a candidate that has neither is counted in stats[0] and picks
+// among the others; stats[2] counts the groups (count_groups), stats[4] the host scores used.
+// One wave per target j < min(*count, n): the chosen candidate's cells, plane strips and
+// per-instance words are copied into dst instance dst_ids[j'] (or base + j'), j' = xlist ?
+// xlist[j] : j.
+__global__ __launch_bounds__(WAVE) void k_cand_select(MzDev cd, MzDev dst, const int32_t* dst_ids,
+                                                      int base, const int* count, int n, int C,
+                                                      const double* score, const int32_t* status,
+                                                      int* stats, const int32_t* xlist,
+                                                      const int32_t* hmap, const double* hprod,
+                                                      const int32_t* hok, int hcap,
+                                                      int count_groups, int dbg) {
+  const int used = count ? min(*count, n) : n;
+  const int lane = threadIdx.x;
+  for (int j = blockIdx.x; j < used; j += gridDim.x) {
+    const int t0 = j * C;
+    bool ok = false, host = false;
+    double p = 0.0;
+    if (lane < C) {
+      const int t = t0 + lane;
+      const bool decl = status[t] != 0 || ((dbg & MZ_DBG_DECLINE_EVEN) && (lane & 1) == 0);
+      if (!decl) {
+        ok = true;
+        p = score[2 * t];
+      } else if (hmap) {
+        const int h = hmap[t];
+        if (h >= 0 && h < hcap && hok[h]) {
+          ok = host = true;
+          p = hprod[h];
+        }
+      }
+    }
+    const unsigned long long okm = __ballot(ok);
+    const unsigned long long hostm = __ballot(host);
+    // first minimum over the scored candidates (wave-uniform loop over C <= 64)
     int pick = 0;
     double best = 0.0;
     bool have = false;
@@ -778,10 +1044,12 @@ __global__ __launch_bounds__(WAVE) void k_cand_select(MzDev cd, MzDev dst, const
     if (lane == 0) {
       if (okm != ((C >= 64) ? ~0ull : ((1ull << C) - 1ull))) atomicAdd(stats + 0, 1);
       if (nearm) atomicAdd(stats + 1, 1);
-      atomicAdd(stats + 2, 1);
+      if (hostm) atomicAdd(stats + 4, __popcll(hostm));
+      if (count_groups) atomicAdd(stats + 2, 1);
     }
     const size_t src = (size_t)(t0 + pick);
-    const size_t de = (size_t)(dst_ids ? dst_ids[j] : base + j);
+    const int jd = xlist ? xlist[j] : j;
+    const size_t de = (size_t)(dst_ids ? dst_ids[jd] : base + jd);
     const size_t pp = (size_t)cd.P * cd.P, pw = (size_t)cd.PW;
     wave_copy(dst.cells + de * pp, cd.cells + src * pp, pp);
     wave_copy(dst.planes + de * pw, cd.planes + src * pw, pw);
@@ -1148,7 +1416,7 @@ hipError_t mz_launch_reset_done(const MzDev& d, int regen, uint64_t seed, uint32
 
 hipError_t mz_launch_cand_build(const MzDev& cd, const int32_t* ids, int base, const int* count, int n,
                                 int C, const uint8_t* algo_list, int algo_all, int dim,
-                                uint64_t seed, uint32_t epoch, hipStream_t s) {
+                                uint64_t seed, uint32_t epoch, hipStream_t s, int dbg) {
   if (n <= 0 || C <= 0) return hipSuccess;
   // euclidean Philox r-prim / dfs lists (the headline's bank classes) build MZ_PACK per wave
   const bool packed = MZ_PACK > 1 && MZ_CELL_BUILD && !cd.toroidal && !algo_list &&
@@ -1165,20 +1433,103 @@ hipError_t mz_launch_cand_build(const MzDev& cd, const int32_t* ids, int base, c
   const int grid = std::max(1, MZ_BANK_WGS > 0 ? std::min(total, MZ_BANK_WGS) : mz_build_grid(total, lds));
   if (packed)
     hipLaunchKernelGGL(k_cand_build_packed, dim3(grid), dim3(WAVE), lds, s, cd, ids, base, count, n, C,
-                       algo_all, dim, seed, epoch, (int)stride);
+                       algo_all, dim, seed, epoch, (int)stride, dbg);
   else
     hipLaunchKernelGGL(k_cand_build, dim3(grid), dim3(WAVE), lds, s, cd, ids, base, count, n, C,
-                       algo_list, algo_all, dim, seed, epoch);
+                       algo_list, algo_all, dim, seed, epoch, dbg);
+  return hipGetLastError();
+}
+
+hipError_t mz_launch_cand_compact(const MzCompact& cc, int P, const int32_t* ids, int base,
+                                  const int* count, int n, int C, const uint8_t* algo_list,
+                                  int algo_all, int dim, uint64_t seed, uint32_t epoch, hipStream_t s,
+                                  int dbg) {
+  if (n <= 0 || C <= 0) return hipSuccess;
+  if (dim > P || cc.Qp < mz_compact_qp(P)) return hipErrorInvalidValue;
+  const bool packed = MZ_PACK > 1 && !algo_list &&
+                      (algo_all == MZ_ALGO_RPRIM_DEV || (MZ_PACK_DFS && algo_all == MZ_ALGO_DFS_DEV));
+  const size_t stride = mz_align16(mz_cell_lds_bytes(P));
+  const size_t lds = packed ? MZ_PACK * stride : stride;
+  const void* kfn = packed ? reinterpret_cast<const void*>(k_cand_compact_packed)
+                           : reinterpret_cast<const void*>(k_cand_compact);
+  hipError_t ae = mz_lds_attr(kfn, lds);
+  if (ae != hipSuccess) return ae;
+  const int total = packed ? (n * C + MZ_PACK - 1) / MZ_PACK : n * C;
+  const int grid = std::max(1, MZ_BANK_WGS > 0 ? std::min(total, MZ_BANK_WGS) : mz_build_grid(total, lds));
+  if (packed)
+    hipLaunchKernelGGL(k_cand_compact_packed, dim3(grid), dim3(WAVE), lds, s, cc, P, ids, base, count,
+                       n, C, algo_all, dim, seed, epoch, (int)stride, dbg);
+  else
+    hipLaunchKernelGGL(k_cand_compact, dim3(grid), dim3(WAVE), lds, s, cc, P, ids, base, count, n, C,
+                       algo_list, algo_all, dim, seed, epoch, dbg);
+  return hipGetLastError();
+}
+
+hipError_t mz_launch_cand_pick(const int* count, int n, int C, const double* score,
+                               const int32_t* status, int32_t* pick, int32_t* xlist, int* xcount,
+                               int xcap, int* stats, hipStream_t s, int dbg) {
+  if (n <= 0) return hipSuccess;
+  if (C < 1 || C > WAVE) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_cand_pick, dim3(std::min(n, 4096)), dim3(WAVE), 0, s, count, n, C, score,
+                     status, pick, xlist, xcount, xcap, stats, dbg);
+  return hipGetLastError();
+}
+
+hipError_t mz_launch_cand_expand(const MzCompact& cc, const MzDev& dst, const int32_t* dst_ids,
+                                 int base, const int* count, int n, int C, const int32_t* pick,
+                                 const uint8_t* algo_list, int algo_all, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const size_t lds = mz_align16(mz_cell_lds_bytes(dst.P));
+  hipError_t ae = mz_lds_attr(reinterpret_cast<const void*>(k_cand_expand), lds);
+  if (ae != hipSuccess) return ae;
+  hipLaunchKernelGGL(k_cand_expand, dim3(std::max(1, mz_build_grid(n, lds))), dim3(WAVE), lds, s, cc,
+                     dst, dst_ids, base, count, n, C, pick, algo_list, algo_all);
+  return hipGetLastError();
+}
+
+hipError_t mz_launch_cand_rebuild(const MzDev& cd, const int32_t* xlist, const int* xcount, int xcap,
+                                  const int32_t* ids, int base, int C, const uint8_t* algo_list,
+                                  int algo_all, int dim, uint64_t seed, uint32_t epoch, hipStream_t s,
+                                  int dbg) {
+  if (xcap <= 0 || C <= 0) return hipSuccess;
+  const size_t lds = mz_build_lds_launch(cd.P, cd.toroidal, true, MZ_PY_PHILOX);
+  hipError_t ae = mz_lds_attr(reinterpret_cast<const void*>(k_cand_rebuild), lds);
+  if (ae != hipSuccess) return ae;
+  // the list is nearly always empty: a small persistent grid
+  const int grid = std::max(1, std::min(xcap * C, 1024));
+  hipLaunchKernelGGL(k_cand_rebuild, dim3(grid), dim3(WAVE), lds, s, cd, xlist, xcount, xcap, ids, base,
+                     C, algo_list, algo_all, dim, seed, epoch, dbg);
+  return hipGetLastError();
+}
+
+hipError_t mz_launch_cand_gather(const MzDev& cd, const int* count, int n, int C,
+                                 const int32_t* status, int32_t* hmap, uint8_t* hgrid,
+                                 int32_t* hinfo, int* hcount, int hcap, int gstride, hipStream_t s,
+                                 int dbg) {
+  if (n <= 0 || C <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_cand_gather, dim3(std::max(1, std::min(n * C, 1024))), dim3(WAVE), 0, s, cd,
+                     count, n, C, status, hmap, hgrid, hinfo, hcount, hcap, gstride, dbg);
+  return hipGetLastError();
+}
+
+hipError_t mz_launch_compact_from_handle(const MzDev& d, const int32_t* ids, int n, const MzCompact& cc,
+                                        hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (cc.Qp < mz_compact_qp(d.P)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_compact_from_handle, dim3(std::min(n, 4096)), dim3(WAVE), 0, s, d, ids, n, cc);
   return hipGetLastError();
 }
 
 hipError_t mz_launch_cand_select(const MzDev& cd, const MzDev& dst, const int32_t* dst_ids,
                                  int base, const int* count, int n, int C, const double* score,
-                                 const int32_t* status, int* stats, hipStream_t s) {
+                                 const int32_t* status, int* stats, hipStream_t s,
+                                 const int32_t* xlist, const int32_t* hmap, const double* hprod,
+                                 const int32_t* hok, int hcap, int count_groups, int dbg) {
   if (n <= 0) return hipSuccess;
   if (C < 1 || C > WAVE) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_cand_select, dim3(std::min(n, 4096)), dim3(WAVE), 0, s, cd, dst, dst_ids,
-                     base, count, n, C, score, status, stats);
+                     base, count, n, C, score, status, stats, xlist, hmap, hprod, hok, hcap,
+                     count_groups, dbg);
   return hipGetLastError();
 }
 

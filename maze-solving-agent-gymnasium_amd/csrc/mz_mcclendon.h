@@ -15,3 +15,7 @@ size_t mz_mcclendon_lds(int P, bool toroidal, int* mm);
 hipError_t mz_launch_mcclendon(const MzDev& d, const int32_t* ids, int n, double* out,
                                int32_t* status, hipStream_t s, const int* limit = nullptr,
                                int mult = 1);
+// Host restatement (mz_difficulty.hip): *prod = prod_b (C_b + 1) * C_0 of a grid (0 wall, 1 open,
+// 2 goal), the quantity k_mcclendon outputs; MZ_OK or an error code.
+int mz_mcclendon_host_prod(const uint8_t* g, int32_t H, int32_t W, int32_t sr, int32_t sc,
+                           int32_t gr, int32_t gc, double* prod);

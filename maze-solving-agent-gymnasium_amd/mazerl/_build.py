@@ -20,12 +20,12 @@ LIBDIR = os.path.join(PKG, "_lib")
 LIB = os.path.join(LIBDIR, "libmazerl.so")
 SOURCES = ["mz_env.hip", "mz_api.hip", "mz_difficulty.hip", "mz_qnet.hip", "mz_metrics.hip",
            "mz_stem.hip", "mz_optim.hip", "mz_trainer.hip", "mz_ppo.hip",
-           "mz_qact.hip", "mz_mcclendon.hip"]
+           "mz_qact.hip", "mz_mcclendon.hip", "mz_screen.hip"]
 EXTRA_FLAGS = {"mz_qnet.hip": ["-ffinite-math-only"],
                "mz_qact.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 BASE_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall"]
 DEPS = SOURCES + ["mz_common.h", "mz_kernels.h", "mz_build.inc.h", "mz_pygen.inc.h",
-                  "mz_mcclendon.h", "mz_learner.h"]
+                  "mz_mcclendon.h", "mz_learner.h", "mz_screen.h"]
 HEADER = os.path.join(os.path.dirname(ROOT), "include", "mazerl.h")
 
 

@@ -39,7 +39,8 @@ EXPORTS = ["mz_last_error", "mz_device_count", "mz_create", "mz_destroy", "mz_lo
            "mz_act", "mz_step_act", "mz_expand_window", "mz_set_algorithm", "mz_query", "mz_get_grid",
            "mz_difficulty", "mz_maze_complexity", "mz_maze_metrics", "mz_difficulty_batch", "mz_get_meta", "mz_discounted_returns", "mz_q_front",
            "mz_bank_create", "mz_bank_create_dims", "mz_bank_create_ex", "mz_bank_fill", "mz_bank_use",
-           "mz_bank_slot_grid", "mz_generate_best", "mz_select_stats", "mz_set_regen_dims",
+           "mz_bank_slot_grid", "mz_generate_best", "mz_select_stats", "mz_select_stats_ex",
+           "mz_set_debug", "mz_screen_batch", "mz_set_regen_dims",
            "mz_bank_consumed", "mz_state_bytes", "mz_state_save", "mz_state_load",
            "mz_stem_forward", "mz_stem_backward", "mz_stem_workspace_floats", "mz_adamw_flat",
            "mz_pair_surrogate", "mz_leaky_relu_bf16", "mz_colsum_f32",
@@ -108,6 +109,11 @@ def load(build_if_missing=True):
     L.mz_generate_best.argtypes = [vp, vp, C.c_int32, vp, C.c_int32, C.c_int32, C.c_uint64,
                                    C.c_int32, vp]
     L.mz_select_stats.argtypes = [vp, vp, C.c_int32, vp]
+    if hasattr(L, "mz_select_stats_ex") or not os.environ.get("MZ_LIB_OVERRIDE"):
+        # (an MZ_LIB_OVERRIDE build of an earlier round lacks these: A/B timing runs)
+        L.mz_select_stats_ex.argtypes = [vp, vp, C.c_int32, C.c_int32, vp]
+        L.mz_set_debug.argtypes = [vp, C.c_int32]
+        L.mz_screen_batch.argtypes = [vp, vp, C.c_int32, vp, vp, vp]
     L.mz_set_regen_dims.argtypes = [vp, vp]
     L.mz_bank_use.argtypes = [vp, C.c_int32]
     L.mz_bank_consumed.argtypes = [vp, C.c_int32, vp, vp]

@@ -693,8 +693,11 @@ class VectorDQNLearner:
         rp, n = self.replay, self.replay.size
         opt = self.opt
         if hasattr(opt, "exp_avg"):  # FlatAdamW (device-side lr and step count)
+            # (a sharded step, distributed.GradAllReduce.attach: the moments are valid only on
+            # this rank's (offset, length) of the flat buffer — recorded, checked on load)
             ost = {"exp_avg": opt.exp_avg.clone(), "exp_avg_sq": opt.exp_avg_sq.clone(),
-                   "step": opt._step_buf.clone(), "lr": float(opt.param_groups[0]["lr"])}
+                   "step": opt._step_buf.clone(), "lr": float(opt.param_groups[0]["lr"]),
+                   "shard": None if opt.shard is None else [int(x) for x in opt.shard]}
         else:
             ost = {"torch": opt.state_dict()}
         heads = [self.fused] + list(getattr(self, "actor_fused", []))
@@ -746,6 +749,12 @@ class VectorDQNLearner:
         if "torch" in o:
             self.opt.load_state_dict(o["torch"])
         else:
+            saved, now = o.get("shard"), getattr(self.opt, "shard", None)
+            if saved is not None and (now is None or tuple(saved) != tuple(now)):
+                raise ValueError(f"the saved optimizer moments hold only the flat-buffer shard "
+                                 f"{tuple(saved)} of a sharded data-parallel step; this learner "
+                                 f"updates {'all of it' if now is None else tuple(now)} — resume "
+                                 f"with the same world size and rank")
             self.opt.exp_avg.copy_(o["exp_avg"])
             self.opt.exp_avg_sq.copy_(o["exp_avg_sq"])
             self.opt._step_buf.copy_(o["step"])

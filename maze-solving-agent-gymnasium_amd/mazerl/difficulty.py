@@ -66,6 +66,23 @@ def difficulty_batch(env, env_ids=None, complexity=False):
     return (d, c) if complexity else d
 
 
+def screen_batch(env, env_ids=None):
+    """The order-free McClendon screen of resident euclidean mazes (mz_screen_batch,
+    csrc/mz_screen.hip: one wave per maze): (prod [n], bound [n], status [n]) numpy — the product
+    whose log is the difficulty, summed in an order of its own, a rigorous bound on its relative
+    distance from the reference's float64 evaluation, status 0 ok / 2 declined."""
+    import torch
+    dev = env.device
+    ids = None if env_ids is None else torch.as_tensor(env_ids, dtype=torch.int32, device=dev)
+    n = env.num_envs if ids is None else int(ids.numel())
+    out = torch.zeros(max(n, 1), 2, dtype=torch.float64, device=dev)
+    st = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
+    N.check(N.load().mz_screen_batch(env._h, None if ids is None else ids.data_ptr(), n,
+                                     out.data_ptr(), st.data_ptr(), env._stream()))
+    o = out[:n].cpu().numpy()
+    return o[:, 0].copy(), o[:, 1].copy(), st[:n].cpu().numpy()
+
+
 def maze_complexity(grid, start, goal):
     """(difficulty_of_maze(), complexity_of_maze()) of a euclidean grid (host, mz_maze_complexity)."""
     g = np.ascontiguousarray(grid, dtype=np.uint8)

@@ -121,8 +121,9 @@ def main(argv=None):
                          eps=a.eps_final, device=dev, mazes=mz6)
         res = {
             "variant": a.variant, "envs_per_gpu": B, "n_gpus": world, "dim": a.dim, "algo": a.algo,
-            "vector_steps": a.steps, "train_seconds": secs,
-            "train_env_steps_per_s": B * a.steps * world / secs,
+            "vector_steps": trainer.stopped_at or a.steps, "train_seconds": secs,
+            # (the max-shape stop can end training before a.steps)
+            "train_env_steps_per_s": B * (trainer.stopped_at or a.steps) * world / secs,
             "updates": learner.n_updates, "updates_per_s": learner.n_updates / secs,
             "batch": a.batch, "train_wins": int(stats[0]), "train_episodes": int(stats[1]),
             "win_rate_greedy": greedy, "win_rate_eps": epsr, "eval_eps": a.eps_final,

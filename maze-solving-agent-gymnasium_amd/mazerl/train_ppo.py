@@ -84,8 +84,8 @@ def main(argv=None):
         rate6, _ = evaluate(tr, a.eval_mazes, dims, a.algo, seed=0x7E580000, eps=0.0,
                             toroidal=True, device=dev, mazes=mz6)
         print(json.dumps({"config": "ppo toroidal variable", "envs_per_gpu": a.envs, "n_gpus": world,
-                          "dims": [dims[0], dims[-1]], "vector_steps": a.steps, "train_seconds": secs,
-                          "train_env_steps_per_s": a.envs * a.steps * world / secs,
+                          "dims": [dims[0], dims[-1]], "vector_steps": tr.stopped_at or a.steps, "train_seconds": secs,
+                          "train_env_steps_per_s": a.envs * (tr.stopped_at or a.steps) * world / secs,
                           "episodes": int(st[0]), "wins": int(st[1]), "updates": tr.updates,
                           "seed": a.seed, "acting": "f32 (ActorCriticNet.act as the reference)",
                           "win_rate_greedy": rate, "win_rate_greedy_best_of_6": rate6,

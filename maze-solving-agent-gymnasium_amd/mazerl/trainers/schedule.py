@@ -26,6 +26,15 @@ vectorised readings of change_algorithm:
   "per-instance"       every instance is a trainer of its own: its own win count drives its
                        algorithm and its own epsilon_decay (a per-instance tensor).
 
+With N data-parallel ranks (rank r owns global instances [r B, (r + 1) B)) the learner's wins are
+counted over every rank's instances in global instance order: each vector step the ranks exchange
+their winner counts (one all-gather of N int64s), and a winner's global win number is the wins of
+all earlier vector steps + the wins of the lower ranks in this step + its rank within its own
+shard — the same numbers one process holding all N B instances would assign, so every rank
+switches algorithms and multiplies epsilon_decay at the same vector step. The max-shape stop
+likewise waits for every rank's instances (a MIN all-reduce of the retired flag every 32 vector
+steps): a rank that stopped alone would leave the others' learner collectives unmatched.
+
 Growth is per instance (the size belongs to the env, and every instance is an env): an instance's
 k-th new maze on a win is start + 4 k while that is <= max_dim; a win at a size whose + 4 would pass
 max_dim keeps the maze; an instance whose size reaches max_dim on a win is `retired` (the
@@ -33,8 +42,16 @@ reference's trainer returns there). The vectorised trainers stop once every inst
 (retired instances keep stepping their last maze until then — a batch cannot drop rows).
 """
 import torch
+import torch.distributed as dist
 
 from ..vector_env import ALGOS
+
+
+def _world():
+    """(rank, world size) of the default process group, (0, 1) without one."""
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
 
 RULES = ("global", "per-instance")
 
@@ -59,6 +76,7 @@ class WinSchedule:
     def __init__(self, env, curriculum=None, growth=None, learner=None, algorithm="r-prim"):
         self.env, self.learner = env, learner
         self.rule = curriculum_rule(curriculum)
+        self.rank, self.world = _world()
         dev, B = env.device, env.num_envs
         if isinstance(algorithm, str):
             a = torch.full((B,), ALGOS[algorithm], dtype=torch.uint8, device=dev)
@@ -104,12 +122,22 @@ class WinSchedule:
             return
         dfs, pk = ALGOS["dfs"], ALGOS["prim&kill"]
         if self.rule == "global":
-            # global win numbers of this step's winners, in instance order
-            rank = self.total_wins + torch.cumsum(w, 0)
+            # global win numbers of this step's winners, in global instance order: the wins of
+            # the lower ranks' shards first (data-parallel), then this shard's in instance order
+            mine = w.sum().to(torch.int64)
+            if self.world > 1:
+                parts = [torch.zeros(1, dtype=torch.int64, device=mine.device)
+                         for _ in range(self.world)]
+                dist.all_gather(parts, mine.view(1))
+                cnt = torch.cat(parts)
+                off, step_wins = cnt[:self.rank].sum(), cnt.sum()
+            else:
+                off, step_wins = 0, mine
+            rank = self.total_wins + off + torch.cumsum(w, 0)
             na = torch.where(rank >= 10, dfs, torch.where(rank >= 5, pk, self.algo.long()))
             self.algo = torch.where(t, na.to(torch.uint8), self.algo)
             before = self.total_wins.clone()
-            self.total_wins += w.sum()
+            self.total_wins += step_wins
             self.inst_wins += w
             L = self.learner
             if L is not None and hasattr(L, "eps_decay"):
@@ -150,12 +178,19 @@ class WinSchedule:
         self._set_next()
 
     def all_retired(self):
-        return self.growth is not None and bool(self.retired.all())
+        """The max-shape stop: every instance of every rank retired (one MIN all-reduce with N
+        ranks — every rank calls this at the same vector steps)."""
+        if self.growth is None:
+            return False
+        done = self.retired.all().to(torch.int32).view(1)
+        if self.world > 1:
+            dist.all_reduce(done, op=dist.ReduceOp.MIN)
+        return bool(done.item())
 
     def summary(self):
         """Host-side counts (one synchronisation)."""
         names = ["r-prim", "dfs", "prim&kill"]  # ids: vector_env.ALGOS
-        out = {"rule": self.rule, "total_wins": int(self.total_wins),
+        out = {"rule": self.rule, "total_wins": int(self.total_wins),  # (global: all ranks')
                "instances_per_algorithm": dict(zip(
                    names, torch.bincount(self.maze_algo.long(), minlength=3).tolist())),
                "new_mazes_per_algorithm": dict(zip(names, self.new_mazes.tolist()))}

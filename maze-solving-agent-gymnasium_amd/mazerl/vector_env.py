@@ -182,13 +182,25 @@ class VectorMazeEnv:
 
     def select_stats(self, reset=False):
         """Best-of-C selection counters of this handle (bank refills + generate(candidates > 1)):
-        {"unresolved": groups with a candidate the GPU difficulty kernel could not score (picked
-        among the others), "near_ties": groups whose choice a 1-ulp log tie could change,
-        "groups": selections made}."""
-        out = torch.zeros(3, dtype=torch.int32, device=self.device)
-        N.check(self.lib.mz_select_stats(self._h, out.data_ptr(), int(bool(reset)), self._stream()))
-        u, t, g = (int(x) for x in out.cpu())
-        return {"unresolved": u, "near_ties": t, "groups": g}
+        {"unresolved": groups with a candidate neither the GPU kernels nor the host restatement
+        scored (picked among the others), "near_ties": groups whose choice a 1-ulp log tie could
+        change, "groups": selections made, "exact": groups the order-free screen could not decide
+        (scored by the order-exact kernel), "host_scored": candidates that kernel declined, scored
+        by the host restatement}."""
+        out = torch.zeros(5, dtype=torch.int32, device=self.device)
+        if hasattr(self.lib, "mz_select_stats_ex"):
+            N.check(self.lib.mz_select_stats_ex(self._h, out.data_ptr(), 5, int(bool(reset)),
+                                                self._stream()))
+        else:  # an earlier round's library (MZ_LIB_OVERRIDE A/B runs): the first three
+            N.check(self.lib.mz_select_stats(self._h, out.data_ptr(), int(bool(reset)),
+                                             self._stream()))
+        u, t, g, x, hs = (int(x) for x in out.cpu())
+        return {"unresolved": u, "near_ties": t, "groups": g, "exact": x, "host_scored": hs}
+
+    def set_debug(self, flags):
+        """Test hooks of the best-of-C pipeline (mz_set_debug): 1 every group through the
+        order-exact kernel, 2 even-numbered candidates host-scored, 4 identical candidates."""
+        N.check(self.lib.mz_set_debug(self._h, int(flags)))
 
     def set_regen_dims(self, dims):
         """Per-instance size of a winner's next maze (uint8 device tensor [B], kept referenced

@@ -152,3 +152,87 @@ def test_best_of_bank_rejects_bad_candidates():
     assert big.lib.mz_bank_create_ex(big._h, 4, arr, 1, 1, 6) == -2  # beyond the LDS plan
     assert big.lib.mz_bank_create_ex(big._h, 4, arr, 1, 1, 1) == 0   # one candidate: no scoring
     big.close()
+
+
+# ---- the screen -> exact -> host pipeline (mz_screen.hip, k_cand_pick, k_cand_select) ---------
+def _gen(n, dim, algo, seed, dbg):
+    from mazerl import VectorMazeEnv
+    env = VectorMazeEnv(n, dim, enrich=True, device="cuda:0", seed=seed, generate=False,
+                        done_list=False)
+    env.set_debug(dbg)
+    env.select_stats(reset=True)
+    env.generate(algorithm=algo, dim=dim, seed=seed, candidates=6)
+    torch.cuda.synchronize()
+    return env
+
+
+def test_screen_decides_and_matches_exact_path():
+    """The screen's picks == every group through the order-exact kernel (debug flag 1) == the
+    host-log argmin of best_of_mazes; without the flag no group needs the exact kernel."""
+    from mazerl.trainers.vector_trainer import best_of_mazes
+    for n, dim, algo in ((40, 81, "r-prim"), (40, 81, "dfs"), (40, 41, "prim&kill")):
+        seed = 0x5C2EE0 + dim
+        a = _gen(n, dim, algo, seed, 0)
+        b = _gen(n, dim, algo, seed, 1)
+        grids, sg, _ = best_of_mazes(n, dim, algo, seed=seed, device="cuda:0", candidates=6)
+        for e in range(n):
+            assert np.array_equal(a.grid(e), grids[e]) and np.array_equal(b.grid(e), grids[e]), e
+            qa, qb = a.query(e), b.query(e)
+            assert qa == qb and (qa["start_r"], qa["start_c"], qa["goal_r"], qa["goal_c"]) == tuple(sg[e])
+        sa, sb = a.select_stats(), b.select_stats()
+        assert sa["groups"] == n and sa["exact"] == 0 and sa["unresolved"] == 0, sa
+        assert sb["groups"] == n and sb["exact"] == n and sb["unresolved"] == 0, sb
+        a.close()
+        b.close()
+
+
+def test_screen_cannot_decide_identical_candidates_exact_path_keeps_the_first():
+    """All six candidates of a group from one seed (debug flag 4): equal difficulties, which no
+    bound can separate — the group goes to the exact kernel, whose first-minimum rule keeps
+    candidate 0 (the reference replaces only on a strict `<`): the maze of seed + 6 e."""
+    from mazerl import VectorMazeEnv
+    n, dim, seed = 24, 41, 0x71A5
+    env = _gen(n, dim, "r-prim", seed, 4)
+    ref = VectorMazeEnv(6 * n, dim, enrich=True, device="cuda:0", seed=seed, algorithm="r-prim",
+                        done_list=False)
+    for e in range(n):
+        assert np.array_equal(env.grid(e), ref.grid(6 * e)), e
+    st = env.select_stats()
+    assert st["exact"] == n and st["unresolved"] == 0 and st["near_ties"] == 0, st
+    env.close()
+    ref.close()
+
+
+def test_declined_candidates_are_scored_on_the_host():
+    """Candidates the exact kernel declines (forced for every even-numbered one, debug flags
+    1 | 2) are scored by the host restatement inside the stream: the selection is still the
+    first minimum over all six (best_of_mazes), none unresolved."""
+    from mazerl.trainers.vector_trainer import best_of_mazes
+    n, dim, seed = 30, 33, 0xDEC1
+    env = _gen(n, dim, "dfs", seed, 3)
+    grids, sg, _ = best_of_mazes(n, dim, "dfs", seed=seed, device="cuda:0", candidates=6)
+    for e in range(n):
+        assert np.array_equal(env.grid(e), grids[e]), e
+    st = env.select_stats()
+    assert st["exact"] == n and st["host_scored"] == 3 * n and st["unresolved"] == 0, st
+    env.close()
+
+
+def test_bank_slots_with_host_scored_candidates():
+    """A best-of-6 bank whose refill has its even candidates declined (host-scored): every slot
+    equals the reference's first minimum over the six candidates (best_of_mazes)."""
+    from mazerl import VectorMazeEnv
+    B, K, dim, seed = 32, 12, 21, 0xBA4C0044
+    env = VectorMazeEnv(B, dim, enrich=True, device="cuda:0", seed=3, algorithm="r-prim",
+                        done_list=False)
+    env.set_debug(3)
+    env.select_stats(reset=True)
+    env.enable_bank(slots=K, swap_every=10 ** 9, algorithms=["r-prim", "prim&kill"], seed=seed,
+                    candidates=6)
+    torch.cuda.synchronize()
+    for algo in ("r-prim", "prim&kill"):
+        assert_bank_block(env, 0, algo, dim, 0, range(K), seed, 0)
+        assert_bank_block(env, 1, algo, dim, 0, range(K), seed, 0)
+    st = env.select_stats()
+    assert st["groups"] == 4 * K and st["host_scored"] == 4 * K * 3 and st["unresolved"] == 0, st
+    env.close()

@@ -167,3 +167,84 @@ def test_sharded_step_equals_allreduce_step(world):
         assert torch.equal(r["shard_sum"], r["full_sum"])
         assert torch.equal(r["sharded"], r["allreduce"])
         assert torch.equal(r["sharded"], rs[0]["sharded"])
+
+
+class _FakeEnv:
+    """What WinSchedule needs of a VectorMazeEnv (CPU tensors)."""
+
+    def __init__(self, B, max_dim=81):
+        self.device, self.num_envs, self.max_dim = torch.device("cpu"), B, max_dim
+        self.algo_set, self.regen = None, None
+
+    def set_algorithm(self, a):
+        self.algo_set = a.clone()
+
+    def set_regen_dims(self, d):
+        self.regen = d
+
+
+def _schedule_steps():
+    g = torch.Generator().manual_seed(11)
+    return [(torch.rand(16, generator=g) < 0.3) for _ in range(6)]
+
+
+def _schedule_worker(rank, world, port, outdir):
+    """Each rank holds 8 of 16 instances: the global rule's algorithms and epsilon_decay match a
+    single process holding all 16; with growth, a rank whose instances all retired keeps
+    training until every rank's have (a rank stopping alone left the others'
+    collectives unmatched)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from mazerl.distributed import init_from_env
+    from mazerl.trainers.schedule import WinSchedule
+    init_from_env("gloo")
+
+    class L:
+        eps_decay = 100.0
+    lr = L()
+    s = WinSchedule(_FakeEnv(8), "global", learner=lr)
+    algos = []
+    for t in _schedule_steps():
+        t = t[8 * rank:8 * rank + 8]
+        s.before_reset(t)
+        s.after_reset(t)
+        algos.append(s.algo.clone())
+    # growth 15 -> 19 (max 19): an instance retires on its first win
+    g = WinSchedule(_FakeEnv(8, max_dim=19), None, growth=(15, 19))
+    seen = []
+    for k in range(3):
+        t = torch.zeros(8, dtype=torch.bool)
+        if rank == 0 and k == 0:
+            t[:] = True       # rank 0's whole shard retires at once
+        if rank == 1 and k == 2:
+            t[:] = True       # rank 1's two steps later
+        g.before_reset(t)
+        g.after_reset(t)
+        seen.append(g.all_retired())
+    torch.save({"algos": torch.stack(algos), "eps_decay": float(lr.eps_decay),
+                "total_wins": int(s.total_wins), "retired_seen": seen},
+               os.path.join(outdir, f"s{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_global_schedule_and_growth_stop_over_two_ranks():
+    from mazerl.trainers.schedule import WinSchedule
+
+    class L:
+        eps_decay = 100.0
+    lr = L()
+    ref = WinSchedule(_FakeEnv(16), "global", learner=lr)
+    ref_algos = []
+    for t in _schedule_steps():
+        ref.before_reset(t)
+        ref.after_reset(t)
+        ref_algos.append(ref.algo.clone())
+    ref_algos = torch.stack(ref_algos)
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_schedule_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        out = [torch.load(os.path.join(d, f"s{r}.pt"), weights_only=True) for r in range(2)]
+    assert torch.equal(torch.cat([out[0]["algos"], out[1]["algos"]], 1), ref_algos)
+    for o in out:
+        assert o["eps_decay"] == float(lr.eps_decay) and o["total_wins"] == int(ref.total_wins)
+        assert o["retired_seen"] == [False, False, True]
