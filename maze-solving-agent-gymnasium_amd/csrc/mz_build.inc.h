@@ -503,6 +503,8 @@ struct MzCellLds {
                    //     the distance to the goal
   int* sh;
   int W, Q;
+  uint32_t mW;     // ceil(2^18 / W): q / W == (q * mW) >> 18 for every cell q (q < 2^12, W <= 64)
+  int cap;         // list capacity (Q; the lite r-prim regions: mz_lite_cap)
 };
 
 // MZ_CELL_ALIAS 0: the distance array separate from the list (A/B builds)
@@ -527,6 +529,8 @@ __device__ inline MzCellLds mz_cell_lds(uint8_t* base, int P, int N) {
   L.A = MZ_CELL_ALIAS ? L.list : reinterpret_cast<uint16_t*>(base + off);
   L.W = (N - 1) / 2;
   L.Q = L.W * L.W;
+  L.mW = ((1u << 18) + (uint32_t)L.W - 1u) / (uint32_t)(L.W > 0 ? L.W : 1);
+  L.cap = L.Q;
   return L;
 }
 
@@ -539,8 +543,11 @@ __device__ inline void cs_clr(uint32_t* b, int q) { atomicAnd(&b[q >> 5], ~(1u <
 
 // neighbour cell of q in direction k — 0 up, 1 down, 2 left, 3 right (the generators' order
 // (-2,0),(2,0),(0,-2),(0,2), maze_generation.py:72) — or -1 outside the grid
-__device__ inline int cs_nb(int q, int k, int W) {
-  const int r = q / W, c = q - r * W;
+// (the carves call this every step: the row by a multiply-shift, not a division by the
+// runtime W — ~25 dependent instructions per call on the carve's serial chain)
+__device__ inline int cs_row(int q, uint32_t mW) { return (int)(((uint32_t)q * mW) >> 18); }
+__device__ inline int cs_nb(int q, int k, int W, uint32_t mW) {
+  const int r = cs_row(q, mW), c = q - r * W;
   if (k == 0) return r > 0 ? q - W : -1;
   if (k == 1) return r + 1 < W ? q + W : -1;
   if (k == 2) return c > 0 ? q - 1 : -1;
@@ -555,7 +562,7 @@ __device__ inline void cs_link(const MzCellLds& L, int q, int k) {
 }
 // whether the passage from q in direction k is open (the neighbour exists)
 __device__ inline bool cs_open_dir(const MzCellLds& L, int q, int k) {
-  const int r = q / L.W, c = q - r * L.W;
+  const int r = cs_row(q, L.mW), c = q - r * L.W;
   if (k == 0) return r > 0 && (L.pas[q - L.W] & 2);
   if (k == 1) return (L.pas[q] & 2) != 0;
   if (k == 2) return c > 0 && (L.pas[q - 1] & 1);
@@ -569,7 +576,7 @@ __device__ void mz_cs_rprim(const MzCellLds& L, int s, MzRng& rng) {
   cs_set(L.b0, s);
   L.dep[s] = 0;
   for (int k = 0; k < 4; ++k) {
-    const int j = cs_nb(s, k, W);
+    const int j = cs_nb(s, k, W, L.mW);
     if (j >= 0) { L.list[nf++] = (uint16_t)j; cs_set(L.b1, j); }
   }
   while (nf > 0) {
@@ -582,7 +589,7 @@ __device__ void mz_cs_rprim(const MzCellLds& L, int s, MzRng& rng) {
     uint32_t w0[4], w1[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      j[k] = cs_nb(f, k, W);
+      j[k] = cs_nb(f, k, W, L.mW);
       const int jj = j[k] >= 0 ? j[k] : f;
       w0[k] = L.b0[jj >> 5] >> (jj & 31);
       w1[k] = L.b1[jj >> 5] >> (jj & 31);
@@ -626,7 +633,7 @@ __device__ void mz_cs_dfs(const MzCellLds& L, int s, MzRng& rng) {
     uint32_t w0[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {  // left, right, up, down
-      j[k] = cs_nb(top, k == 0 ? 2 : (k == 1 ? 3 : k - 2), W);
+      j[k] = cs_nb(top, k == 0 ? 2 : (k == 1 ? 3 : k - 2), W, L.mW);
       const int jj = j[k] >= 0 ? j[k] : top;
       w0[k] = L.b0[jj >> 5] >> (jj & 31);
     }
@@ -660,7 +667,7 @@ __device__ inline int mz_cs_pk_nbrs(const MzCellLds& L, int p, uint64_t& out) {
   int cnt = 0;
   out = 0;
   for (int k = 0; k < 4; ++k) {
-    const int j = cs_nb(p, k, L.W);
+    const int j = cs_nb(p, k, L.W, L.mW);
     if (j >= 0 && !cs_bit(L.b0, j)) mz_k4_push(out, cnt, j | (k << 12));
   }
   return cnt;
@@ -670,7 +677,7 @@ __device__ inline void mz_cs_pk_mark(const MzCellLds& L, int p) {
   cs_set(L.b0, p);
   if (mz_cs_pk_nbrs(L, p, tmp) > 0) cs_set(L.b1, p); else cs_clr(L.b1, p);
   for (int k = 0; k < 4; ++k) {
-    const int n = cs_nb(p, k, L.W);
+    const int n = cs_nb(p, k, L.W, L.mW);
     if (n >= 0 && cs_bit(L.b0, n) && mz_cs_pk_nbrs(L, n, tmp) == 0) cs_clr(L.b1, n);
   }
 }
@@ -679,7 +686,7 @@ __device__ inline void mz_cs_pk_mark(const MzCellLds& L, int p) {
 // the mark's neighbour-of-neighbour scans made several dependent ones. Returns p's unmarked
 // neighbours (what the walk's next mz_cs_pk_nbrs(p) would read: the mark changes p's bit only).
 __device__ inline int mz_cs_pk_mark_w(const MzCellLds& L, int p, uint64_t& out) {
-  const int W = L.W, r = p / W, c = p - r * W;
+  const int W = L.W, r = cs_row(p, L.mW), c = p - r * W;
   uint32_t rows[5];
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
@@ -703,13 +710,13 @@ __device__ inline int mz_cs_pk_mark_w(const MzCellLds& L, int p, uint64_t& out) 
 #pragma unroll
   for (int k = 0; k < 4; ++k) {  // up, down, left, right
     const int i = 2 + (k == 0 ? -1 : (k == 1 ? 1 : 0)), j = 2 + (k == 2 ? -1 : (k == 3 ? 1 : 0));
-    if (!mk(i, j)) mz_k4_push(out, cnt, cs_nb(p, k, W) | (k << 12));
+    if (!mk(i, j)) mz_k4_push(out, cnt, cs_nb(p, k, W, L.mW) | (k << 12));
   }
   if (cnt > 0) cs_set(L.b1, p); else cs_clr(L.b1, p);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int i = 2 + (k == 0 ? -1 : (k == 1 ? 1 : 0)), j = 2 + (k == 2 ? -1 : (k == 3 ? 1 : 0));
-    const int n = cs_nb(p, k, W);
+    const int n = cs_nb(p, k, W, L.mW);
     if (n >= 0 && mk(i, j) && free_nbrs(i, j) == 0) cs_clr(L.b1, n);
   }
   return cnt;
@@ -793,7 +800,7 @@ __device__ int mz_cs_goal(const MzCellLds& L, int N, int s) {
     int nb = 0;
     for (int k = 0; k < 4; ++k) nb += cs_open_dir(L, q, k);
     if (nb != 1) continue;
-    const int r = q / W, c = q - r * W, p = (2 * r + 1) * N + 2 * c + 1;
+    const int r = cs_row(q, L.mW), c = q - r * W, p = (2 * r + 1) * N + 2 * c + 1;
     const uint32_t key = ((uint32_t)(L.dep[q] + 1) << 16) | (uint32_t)(0xFFFF - p);
     best = key > best ? key : best;
   }
@@ -823,7 +830,7 @@ __device__ bool mz_cs_dist(const MzCellLds& L, int s, int goal) {
         a = 0xFFFF;
         for (int k = 0; k < 4; ++k)
           if (cs_open_dir(L, q, k)) {
-            const int n = cs_nb(q, k, W);
+            const int n = cs_nb(q, k, W, L.mW);
             if ((int)L.dep[n] == want) a = n;
           }
         bad |= a == 0xFFFF;
@@ -892,7 +899,7 @@ __device__ bool mz_cs_dist(const MzCellLds& L, int s, int goal) {
         const int v = queue[i], dv = L.A[v];
         for (int k = 0; k < 4; ++k) {
           if (!cs_open_dir(L, v, k)) continue;
-          const int n = cs_nb(v, k, W);
+          const int n = cs_nb(v, k, W, L.mW);
           const uint32_t bit = 1u << (n & 31);
           if (atomicOr(&L.b1[n >> 5], bit) & bit) continue;
           L.A[n] = (uint16_t)(dv + 2);
@@ -1043,6 +1050,199 @@ __device__ __forceinline__ void mz_carve_packed(int P, uint64_t seed, int nm, in
     if (algo == MZ_ALGO_RPRIM_DEV) mz_cs_rprim(L, a * W + b, rng);
     else mz_cs_dfs(L, a * W + b, rng);
   }
+  __syncthreads();
+}
+
+// ---- Lite r-prim candidates (k_cand_compact_lite): more carves in flight per CU ------------
+// A carve is one serial chain of LDS round trips per maze, so a CU's build throughput is the
+// number of carves its LDS holds. The lite region keeps only what the carve itself needs: the
+// passages with each cell's parent direction (pas bits 2-3: toward the neighbour it joined), the
+// two bit sets, and a frontier list capped at mz_lite_cap cells (random Prim's frontier stays far
+// below: max 199 over 300 simulated 40 x 40 carves, 319 at 63 x 63) — ~2.9 KB at 81 x 81 instead of
+// 8.5 KB: no carve depths (the depths come afterwards from the parent directions by pointer
+// jumping, in a per-wave scratch the finish uses maze after maze). The same Philox draws over the
+// same frontier order: the same mazes as mz_cs_rprim. A frontier that would pass the cap ends the
+// carve and flags the candidate (cmeta MZ_CMETA_NOSOL): the screen declines it and the group is
+// rebuilt in full for the order-exact kernel (k_cand_rebuild).
+__host__ __device__ inline int mz_lite_cap(int P) {
+  const int Qp = (P / 2) * (P / 2);
+  int cap = Qp / 4 > 128 ? Qp / 4 : 128;
+  cap = cap < Qp ? cap : Qp;
+  return (cap + 15) & ~15;
+}
+__host__ __device__ inline size_t mz_lite_lds_bytes(int P) {
+  const size_t Qp = (size_t)(P / 2) * (P / 2), QW = (Qp + 31) / 32;
+  return 64 + mz_align16(Qp) + 2 * mz_align16(4 * QW) + mz_align16(2 * (size_t)mz_lite_cap(P));
+}
+// the per-wave finish scratch: depth words [Qp] (u32) + distances [Qp] (u16)
+__host__ __device__ inline size_t mz_lite_scratch_bytes(int P) {
+  const size_t Qp = (size_t)(P / 2) * (P / 2);
+  return mz_align16(4 * Qp) + mz_align16(2 * Qp);
+}
+__device__ inline MzCellLds mz_lite_lds(uint8_t* base, int P, int N) {
+  const size_t Wp = (size_t)P / 2, Qp = Wp * Wp, QW = (Qp + 31) / 32;
+  MzCellLds L;
+  L.sh = reinterpret_cast<int*>(base);
+  size_t off = 64;
+  L.pas = base + off; off += mz_align16(Qp);
+  L.b0 = reinterpret_cast<uint32_t*>(base + off); off += mz_align16(4 * QW);
+  L.b1 = reinterpret_cast<uint32_t*>(base + off); off += mz_align16(4 * QW);
+  L.list = reinterpret_cast<uint16_t*>(base + off);
+  L.dep = nullptr;
+  L.A = nullptr;
+  L.W = (N - 1) / 2;
+  L.Q = L.W * L.W;
+  L.mW = ((1u << 18) + (uint32_t)L.W - 1u) / (uint32_t)(L.W > 0 ? L.W : 1);
+  L.cap = mz_lite_cap(P);
+  return L;
+}
+
+// random_prim_visit (maze_generation.py:59-99) as mz_cs_rprim, one lane, without carve depths:
+// cell f records the direction of the neighbour it joins (pas bits 2-3)
+__device__ void mz_lite_rprim(const MzCellLds& L, int s, MzRng& rng) {
+  const int W = L.W;
+  int nf = 0;
+  cs_set(L.b0, s);
+  for (int k = 0; k < 4; ++k) {
+    const int j = cs_nb(s, k, W, L.mW);
+    if (j >= 0) { L.list[nf++] = (uint16_t)j; cs_set(L.b1, j); }
+  }
+  uint32_t* pw = reinterpret_cast<uint32_t*>(L.pas);
+  while (nf > 0) {
+    const int i = (int)rng.below((uint32_t)nf);
+    const int f = L.list[i];
+    L.list[i] = L.list[--nf];
+    int j[4];
+    uint32_t w0[4], w1[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      j[k] = cs_nb(f, k, W, L.mW);
+      const int jj = j[k] >= 0 ? j[k] : f;
+      w0[k] = L.b0[jj >> 5] >> (jj & 31);
+      w1[k] = L.b1[jj >> 5] >> (jj & 31);
+    }
+    uint64_t nb = 0;
+    int cnt = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (j[k] >= 0 && (w0[k] & 1u)) mz_k4_push(nb, cnt, j[k] | (k << 12));
+    if (cnt) {
+      const int v = mz_k4(nb, (int)rng.below((uint32_t)cnt)), kk = v >> 12;
+      cs_set(L.b0, f);
+      cs_link(L, f, kk);
+      atomicOr(pw + (f >> 2), (uint32_t)(kk << 2) << (8 * (f & 3)));
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (j[k] >= 0 && !(w0[k] & 1u) && !(w1[k] & 1u)) {
+          if (nf == L.cap) { L.sh[4] = 1; nf = 0; break; }  // past the cap: flagged, abandoned
+          L.list[nf++] = (uint16_t)j[k];
+          cs_set(L.b1, j[k]);
+        }
+      }
+    }
+  }
+}
+
+// The finish of a lite candidate (wave-wide; J / A: the per-wave scratch): carve depths by pointer
+// jumping over the parent directions (J = ancestor | distance << 16), the goal as mz_cs_goal, the
+// distance field as mz_cs_dist's tree path (the goal's root path marked in b1: the solution's
+// cells), then the compact form leaves LDS as mz_cells_compact writes it.
+__device__ __forceinline__ void mz_lite_finish(const MzCompact& cc, int t, const MzCellLds& L, int N,
+                                               uint32_t* J, uint16_t* A) {
+  const int lane = threadIdx.x, Q = L.Q, W = L.W;
+  const int s = L.sh[2];
+  const bool over = L.sh[4] != 0;
+  auto parent = [&](int q) { return cs_nb(q, (L.pas[q] >> 2) & 3, W, L.mW); };
+  bool ok = !over;
+  int goal = s;
+  if (ok) {
+    for (int q = lane; q < Q; q += 64) J[q] = q == s ? (uint32_t)s : ((uint32_t)parent(q) | (2u << 16));
+    __syncthreads();
+    bool conv = false;
+    for (int it = 0; it < 16 && !conv; ++it) {
+      bool ch = false;
+      for (int q = lane; q < Q; q += 64) {
+        const uint32_t j = J[q];
+        const int a = (int)(j & 0xFFFFu);
+        if (a == s) continue;
+        const uint32_t ja = J[a];
+        J[q] = (ja & 0xFFFFu) | ((j & 0xFFFF0000u) + (ja & 0xFFFF0000u));
+        ch = true;
+      }
+      conv = !__any(ch);
+      __syncthreads();
+    }
+    ok = conv;
+    auto dep = [&](int q) { return (int)(J[q] >> 16); };
+    // find_random_position (maze_generation.py:187-218): the deepest dead end, then the smallest
+    // square index (mz_cs_goal's key)
+    uint32_t best = 0;
+    for (int q = lane; q < Q && ok; q += 64) {
+      if (q == s) continue;
+      int nb = 0;
+      for (int k = 0; k < 4; ++k) nb += cs_open_dir(L, q, k);
+      if (nb != 1) continue;
+      const int r = cs_row(q, L.mW), c = q - r * W, p = (2 * r + 1) * N + 2 * c + 1;
+      const uint32_t key = ((uint32_t)(dep(q) + 1) << 16) | (uint32_t)(0xFFFF - p);
+      best = key > best ? key : best;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint32_t x = __shfl_xor(best, o);
+      best = x > best ? x : best;
+    }
+    if (best) {
+      const int p = 0xFFFF - (int)(best & 0xFFFF), r = p / N, c = p - r * N;
+      goal = (r >> 1) * W + (c >> 1);
+    }
+    // distances to the goal: parents into A, the goal's root path into b1, every cell's first
+    // ancestor on that path by pointer jumping, D = dep + dep(goal) - 2 dep(ancestor)
+    for (int q = lane; q < Q; q += 64) A[q] = (uint16_t)(q == s ? s : parent(q));
+    for (int i = lane; i < (Q + 31) / 32; i += 64) L.b1[i] = 0u;
+    __syncthreads();
+    if (lane == 0) {
+      int x = goal, n = 0;
+      for (; n <= Q; ++n) {
+        cs_set(L.b1, x);
+        if (x == s) break;
+        x = A[x];
+      }
+      L.sh[3] = n > Q;
+    }
+    __syncthreads();
+    ok = ok && !L.sh[3];
+    conv = false;
+    for (int it = 0; it < 32 && !conv && ok; ++it) {
+      bool ch = false;
+      for (int q = lane; q < Q; q += 64) {
+        const int a = A[q];
+        if (cs_bit(L.b1, a)) continue;
+        A[q] = A[a];
+        ch = true;
+      }
+      conv = !__any(ch);
+      __syncthreads();
+    }
+    ok = ok && conv;
+    if (ok) {
+      const int dg = dep(goal);
+      for (int q = lane; q < Q; q += 64) {
+        const int a = cs_bit(L.b1, q) ? q : A[q];
+        A[q] = (uint16_t)(dep(q) + dg - 2 * dep(a));
+      }
+    }
+    __syncthreads();
+  }
+  uint32_t* gp = reinterpret_cast<uint32_t*>(cc.pas + (size_t)t * cc.Qp);
+  uint32_t* ga = reinterpret_cast<uint32_t*>(cc.dist + (size_t)t * cc.Qp);
+  const uint32_t* lp = reinterpret_cast<const uint32_t*>(L.pas);
+  const uint32_t* la = reinterpret_cast<const uint32_t*>(A);
+  if (ok) {
+    for (int i = lane; i < (Q + 3) / 4; i += 64) gp[i] = lp[i] & 0x03030303u;  // (passages only)
+    for (int i = lane; i < (Q + 1) / 2; i += 64) ga[i] = la[i];
+    for (int i = lane; i < (Q + 31) / 32; i += 64) cc.sol[(size_t)t * cc.QWp + i] = L.b1[i];
+  }
+  if (lane == 0)
+    cc.meta[t] = (uint32_t)N | (ok ? 0u : MZ_CMETA_NOSOL) | ((uint32_t)s << 8) | ((uint32_t)goal << 20);
   __syncthreads();
 }
 

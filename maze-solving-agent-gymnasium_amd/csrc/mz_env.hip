@@ -767,6 +767,48 @@ __global__ __launch_bounds__(WAVE) void k_cand_compact_packed(MzCompact cc, int 
   }
 }
 
+// Lite r-prim candidates (mz_lite_rprim): MZ_LPACK carves per wave in lockstep on lanes
+// (64 / MZ_LPACK) m, each in a ~2.9 KB region, then the finish maze after maze in the wave's
+// scratch (depth words + distances) after the regions. The same seeds and draws: the same mazes.
+#ifndef MZ_LPACK
+#define MZ_LPACK 4
+#endif
+__global__ __launch_bounds__(WAVE) void k_cand_compact_lite(MzCompact cc, int P, const int32_t* ids,
+                                                            int base, const int* count, int n, int C,
+                                                            int dim, uint64_t seed, uint32_t epoch,
+                                                            int stride, int dbg) {
+  extern __shared__ __align__(16) uint8_t lds[];
+  constexpr int SP = WAVE / MZ_LPACK;
+  const int used = count ? min(*count, n) : n;
+  const int total = used * C, lane = threadIdx.x, m = lane / SP;
+  uint8_t* scr = lds + (size_t)MZ_LPACK * stride;
+  uint32_t* J = reinterpret_cast<uint32_t*>(scr);
+  uint16_t* A = reinterpret_cast<uint16_t*>(scr + mz_align16(4 * (size_t)mz_compact_qp(P)));
+  for (int t0 = blockIdx.x * MZ_LPACK; t0 < total; t0 += gridDim.x * MZ_LPACK) {
+    const int nm = min(MZ_LPACK, total - t0);
+    const int t = t0 + min(m, nm - 1);
+    const int j = t / C, c = t - j * C;
+    const uint64_t id = (uint64_t)(ids ? ids[j] : base + j);
+    for (int k = 0; k < nm; ++k) {
+      const MzCellLds L = mz_lite_lds(lds + k * stride, P, dim);
+      mz_cells_clear(L);
+      if (lane == 0) { L.sh[3] = 0; L.sh[4] = 0; }
+    }
+    __syncthreads();
+    if ((lane % SP) == 0 && m < nm) {
+      const MzCellLds L = mz_lite_lds(lds + m * stride, P, dim);
+      const int W = L.W;
+      MzRng rng{mz_cand_seed(seed, id, C, c, epoch, dbg), 0ull, {0u, 0u, 0u, 0u}};
+      const int a = (int)rng.below((uint32_t)W), b = (int)rng.below((uint32_t)W);
+      L.sh[2] = a * W + b;
+      mz_lite_rprim(L, a * W + b, rng);
+    }
+    __syncthreads();
+    for (int k = 0; k < nm; ++k) mz_lite_finish(cc, t0 + k, mz_lite_lds(lds + k * stride, P, dim), dim, J, A);
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(WAVE) void k_cand_compact(MzCompact cc, int P, const int32_t* ids,
                                                        int base, const int* count, int n, int C,
                                                        const uint8_t* algo_list, int algo_all,
@@ -1280,6 +1322,9 @@ hipError_t mz_lds_attr(const void* fn, size_t bytes) {
   return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
+#ifndef MZ_LITE  // r-prim candidates in the lite regions (A/B builds: 0)
+#define MZ_LITE 1
+#endif
 #ifndef MZ_PACK_DFS  // dfs candidate lists packed too (A/B builds: 0)
 #define MZ_PACK_DFS 1
 #endif
@@ -1446,6 +1491,17 @@ hipError_t mz_launch_cand_compact(const MzCompact& cc, int P, const int32_t* ids
                                   int dbg) {
   if (n <= 0 || C <= 0) return hipSuccess;
   if (dim > P || cc.Qp < mz_compact_qp(P)) return hipErrorInvalidValue;
+  if (MZ_LITE && !algo_list && algo_all == MZ_ALGO_RPRIM_DEV) {  // r-prim: the lite regions
+    const size_t stride = mz_align16(mz_lite_lds_bytes(P));
+    const size_t lds = MZ_LPACK * stride + mz_lite_scratch_bytes(P);
+    hipError_t ae = mz_lds_attr(reinterpret_cast<const void*>(k_cand_compact_lite), lds);
+    if (ae != hipSuccess) return ae;
+    const int total = (n * C + MZ_LPACK - 1) / MZ_LPACK;
+    const int grid = std::max(1, MZ_BANK_WGS > 0 ? std::min(total, MZ_BANK_WGS) : mz_build_grid(total, lds));
+    hipLaunchKernelGGL(k_cand_compact_lite, dim3(grid), dim3(WAVE), lds, s, cc, P, ids, base, count,
+                       n, C, dim, seed, epoch, (int)stride, dbg);
+    return hipGetLastError();
+  }
   const bool packed = MZ_PACK > 1 && !algo_list &&
                       (algo_all == MZ_ALGO_RPRIM_DEV || (MZ_PACK_DFS && algo_all == MZ_ALGO_DFS_DEV));
   const size_t stride = mz_align16(mz_cell_lds_bytes(P));

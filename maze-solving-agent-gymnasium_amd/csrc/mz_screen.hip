@@ -210,9 +210,13 @@ __device__ void screen_one(const MzCompact& cc, int t, uint8_t* lds, double* out
     d0 += (long)__shfl_xor((int)d0, o);  // d0 < 2^31 (at most the maze's squares)
     n0 += ny;
   }
-  // ---- 4. the break's excluded junctions: a degree-4 hallway node whose parent is a solution
-  // junction adds only its first child's junction before the break; first(x) = the smallest
-  // dead end (row-major) below x, by walking the dead ends in order (each cell written once)
+  // ---- 4. the break's excluded junctions: a degree-4 hallway node p whose parent is a solution
+  // junction adds only its first child's junction before the break; its first child is the one
+  // whose subtree holds the smallest dead end (row-major) below p. Every off-solution point x gets
+  // T(x), its topmost off-solution ancestor point, and C(x), the point just below T(x) on the way
+  // up from x (pointer jumping over (T, C) pairs packed in one word, in the S region — free until
+  // step 7); each dead end e offers itself to M[T(e)] (atomicMin, in the X / Y region — both
+  // re-initialised in step 5); p's first child is then C(M[p]).
   bool need = false;
   auto child_pt = [&](int q, int k) {  // the first point down the corridor from q in direction k
     int y = nb(q, k);
@@ -226,34 +230,57 @@ __device__ void screen_one(const MzCompact& cc, int t, uint8_t* lds, double* out
     return fsol(fp) && fj(fp);
   };
   for (int q = lane; q < Q; q += WV)
-    if (brk(q))
+    if (brk(q)) {
+      int nj = 0;
       for (int k = 0; k < 4; ++k)
-        if (k != fpd(L.fl[q]) && fj(L.fl[child_pt(q, k)])) need = true;
+        if (k != fpd(L.fl[q]) && fj(L.fl[child_pt(q, k)])) ++nj;
+      if (nj) need = true;
+    }
   if (__any(need)) {
-    for (int q = lane; q < Q; q += WV) L.X[q] = NONE;
+    uint32_t* TC = reinterpret_cast<uint32_t*>(L.S);  // T | C << 16
+    uint32_t* M = reinterpret_cast<uint32_t*>(L.X);
+    for (int q = lane; q < Q; q += WV) {
+      const uint8_t f = L.fl[q];
+      uint32_t tc = 0xFFFFFFFFu;
+      if (fpt(f) && !fsol(f)) {
+        const int p = L.pp[q];
+        tc = fsol(L.fl[p]) ? ((uint32_t)q | ((uint32_t)q << 16)) : ((uint32_t)p | ((uint32_t)q << 16));
+      }
+      TC[q] = tc;
+      M[q] = 0xFFFFFFFFu;
+    }
     __syncthreads();
-    for (int b0 = 0; b0 < Q; b0 += WV) {
-      const int q = b0 + lane;
-      const uint8_t f = q < Q ? L.fl[q] : 0;
-      unsigned long long m = __ballot(q < Q && fdeg(f) == 1 && !fsol(f));
-      if (lane == 0)
-        while (m) {
-          const int e = b0 + __ffsll((long long)m) - 1;
-          m &= m - 1;
-          for (int y = e; !fsol(L.fl[y]) && L.X[y] == NONE; y = nb(y, fpd(L.fl[y]))) L.X[y] = (uint16_t)e;
+    bool tconv = false;
+    for (int it = 0; it < 20 && !tconv; ++it) {
+      bool ch = false;
+      for (int q = lane; q < Q; q += WV) {
+        const uint32_t tc = TC[q];
+        if (tc == 0xFFFFFFFFu) continue;
+        const int a = (int)(tc & 0xFFFFu);
+        const uint32_t ta = TC[a];
+        if ((int)(ta & 0xFFFFu) != a) {  // a is not a top: jump to its target, keep its C
+          TC[q] = ta;
+          ch = true;
         }
+      }
+      tconv = !__any(ch);
+      __syncthreads();
+    }
+    if (!tconv) { fail(); return; }
+    for (int q = lane; q < Q; q += WV) {
+      const uint8_t f = L.fl[q];
+      if (fdeg(f) == 1 && !fsol(f)) atomicMin(&M[TC[q] & 0xFFFFu], (uint32_t)q);
     }
     __syncthreads();
     for (int q = lane; q < Q; q += WV) {
       if (!brk(q)) continue;
+      const uint32_t m = M[q];
+      const int fc = m == 0xFFFFFFFFu ? -1 : (int)(TC[m] >> 16);
       const int pd = fpd(L.fl[q]);
-      int kf = -1, best = 0x7FFFFFFF;
-      for (int k = 0; k < 4; ++k)
-        if (k != pd && (int)L.X[nb(q, k)] < best) { best = L.X[nb(q, k)]; kf = k; }
       for (int k = 0; k < 4; ++k) {
-        if (k == pd || k == kf) continue;
+        if (k == pd) continue;
         const int cp = child_pt(q, k);
-        if (fj(L.fl[cp])) L.fl[cp] |= F_EXCL;
+        if (cp != fc && fj(L.fl[cp])) L.fl[cp] |= F_EXCL;
       }
     }
     __syncthreads();

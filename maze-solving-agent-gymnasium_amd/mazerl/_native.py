@@ -169,7 +169,7 @@ def load(build_if_missing=True):
     L.mz_host_alloc.argtypes = [C.c_uint64, C.c_int32, C.POINTER(vp), C.POINTER(vp)]
     L.mz_host_free.argtypes = [vp]
     for f in EXPORTS:
-        if f != "mz_last_error":
+        if f != "mz_last_error" and (hasattr(L, f) or not os.environ.get("MZ_LIB_OVERRIDE")):
             getattr(L, f).restype = C.c_int
     L.mz_qact_workspace_floats.restype = C.c_int64
     _lib = L

@@ -1,15 +1,21 @@
 #!/bin/bash
-# An experiment library: the current objects of libmazerl.so with ONE source replaced by another
-# version of it (a file path or a git revision's copy), into profiles/_bin/<name>.so (gitignored).
-#   profiles/build_variant.sh <name> <csrc file name> <alt source path | git rev> [extra hipcc flags]
+# Build libmazerl.so with extra compile flags into profiles/_bin/<name>.so (A/B variants).
+# usage: profiles/build_variant.sh <name> <flags...>
 set -e
-cd "$(dirname "$0")/.."
-name=$1; file=$2; alt=$3; shift 3
-C=maze-solving-agent-gymnasium_amd/csrc
-L=maze-solving-agent-gymnasium_amd/mazerl/_lib
-src=$alt
-if [ ! -f "$alt" ]; then src=/tmp/variant_$name.hip; git show "$alt:$C/$file" > $src; fi
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -I $C "$@" -c -o /tmp/variant_$name.o $src
-mkdir -p profiles/_bin
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o profiles/_bin/$name.so $(ls $L/obj/*.o | grep -v "/$file.o") /tmp/variant_$name.o
-echo profiles/_bin/$name.so
+name=$1; shift
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+C=$ROOT/maze-solving-agent-gymnasium_amd/csrc
+O=/tmp/variant_$name
+mkdir -p $O $ROOT/profiles/_bin
+objs=()
+for f in mz_env.hip mz_api.hip mz_difficulty.hip mz_qnet.hip mz_metrics.hip mz_stem.hip mz_optim.hip \
+         mz_trainer.hip mz_ppo.hip mz_qact.hip mz_mcclendon.hip mz_screen.hip; do
+  extra=""
+  [ $f = mz_qnet.hip ] && extra="-ffinite-math-only"
+  [ $f = mz_qact.hip ] && extra="-mllvm -amdgpu-mfma-vgpr-form"
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off $extra "$@" -c -o $O/$f.o $C/$f &
+  objs+=($O/$f.o)
+done
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $ROOT/profiles/_bin/$name.so "${objs[@]}"
+echo $ROOT/profiles/_bin/$name.so
