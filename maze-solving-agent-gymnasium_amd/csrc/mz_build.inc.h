@@ -1064,22 +1064,24 @@ __device__ __forceinline__ void mz_carve_packed(int P, uint64_t seed, int nm, in
 // same frontier order: the same mazes as mz_cs_rprim. A frontier that would pass the cap ends the
 // carve and flags the candidate (cmeta MZ_CMETA_NOSOL): the screen declines it and the group is
 // rebuilt in full for the order-exact kernel (k_cand_rebuild).
-__host__ __device__ inline int mz_lite_cap(int P) {
+// (dfs: the stack can hold every cell — a dfs region keeps the full list, ~5.3 KB at 81 x 81)
+__host__ __device__ inline int mz_lite_cap(int P, int algo = MZ_ALGO_RPRIM_DEV) {
   const int Qp = (P / 2) * (P / 2);
+  if (algo == MZ_ALGO_DFS_DEV) return (Qp + 15) & ~15;
   int cap = Qp / 4 > 128 ? Qp / 4 : 128;
   cap = cap < Qp ? cap : Qp;
   return (cap + 15) & ~15;
 }
-__host__ __device__ inline size_t mz_lite_lds_bytes(int P) {
+__host__ __device__ inline size_t mz_lite_lds_bytes(int P, int algo = MZ_ALGO_RPRIM_DEV) {
   const size_t Qp = (size_t)(P / 2) * (P / 2), QW = (Qp + 31) / 32;
-  return 64 + mz_align16(Qp) + 2 * mz_align16(4 * QW) + mz_align16(2 * (size_t)mz_lite_cap(P));
+  return 64 + mz_align16(Qp) + 2 * mz_align16(4 * QW) + mz_align16(2 * (size_t)mz_lite_cap(P, algo));
 }
 // the per-wave finish scratch: depth words [Qp] (u32) + distances [Qp] (u16)
 __host__ __device__ inline size_t mz_lite_scratch_bytes(int P) {
   const size_t Qp = (size_t)(P / 2) * (P / 2);
   return mz_align16(4 * Qp) + mz_align16(2 * Qp);
 }
-__device__ inline MzCellLds mz_lite_lds(uint8_t* base, int P, int N) {
+__device__ inline MzCellLds mz_lite_lds(uint8_t* base, int P, int N, int algo = MZ_ALGO_RPRIM_DEV) {
   const size_t Wp = (size_t)P / 2, Qp = Wp * Wp, QW = (Qp + 31) / 32;
   MzCellLds L;
   L.sh = reinterpret_cast<int*>(base);
@@ -1093,7 +1095,7 @@ __device__ inline MzCellLds mz_lite_lds(uint8_t* base, int P, int N) {
   L.W = (N - 1) / 2;
   L.Q = L.W * L.W;
   L.mW = ((1u << 18) + (uint32_t)L.W - 1u) / (uint32_t)(L.W > 0 ? L.W : 1);
-  L.cap = mz_lite_cap(P);
+  L.cap = mz_lite_cap(P, algo);
   return L;
 }
 
@@ -1140,6 +1142,44 @@ __device__ void mz_lite_rprim(const MzCellLds& L, int s, MzRng& rng) {
         }
       }
     }
+  }
+}
+
+// deept_first_visit (maze_generation.py:101-128) as mz_cs_dfs, one lane, without carve depths:
+// a pushed cell records the direction back to the cell it was carved from (pas bits 2-3)
+__device__ void mz_lite_dfs(const MzCellLds& L, int s, MzRng& rng) {
+  const int W = L.W;
+  int sp = 0;
+  L.list[sp++] = (uint16_t)s;
+  cs_set(L.b0, s);
+  uint32_t* pw = reinterpret_cast<uint32_t*>(L.pas);
+  int top = s;
+  while (sp > 0) {
+    int j[4];
+    uint32_t w0[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // left, right, up, down
+      j[k] = cs_nb(top, k == 0 ? 2 : (k == 1 ? 3 : k - 2), W, L.mW);
+      const int jj = j[k] >= 0 ? j[k] : top;
+      w0[k] = L.b0[jj >> 5] >> (jj & 31);
+    }
+    uint64_t cand = 0;
+    int cnt = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (j[k] >= 0 && !(w0[k] & 1u)) mz_k4_push(cand, cnt, k);
+    if (!cnt) {
+      if (--sp > 0) top = L.list[sp - 1];
+      continue;
+    }
+    const int k = mz_k4(cand, (int)rng.below((uint32_t)cnt));
+    const int dir = k == 0 ? 2 : (k == 1 ? 3 : k - 2);
+    const int jn = k == 0 ? j[0] : (k == 1 ? j[1] : (k == 2 ? j[2] : j[3]));
+    cs_link(L, top, dir);
+    cs_set(L.b0, jn);
+    atomicOr(pw + (jn >> 2), (uint32_t)((dir ^ 1) << 2) << (8 * (jn & 3)));
+    L.list[sp++] = (uint16_t)jn;
+    top = jn;
   }
 }
 

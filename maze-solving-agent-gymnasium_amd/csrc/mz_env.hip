@@ -775,8 +775,8 @@ __global__ __launch_bounds__(WAVE) void k_cand_compact_packed(MzCompact cc, int 
 #endif
 __global__ __launch_bounds__(WAVE) void k_cand_compact_lite(MzCompact cc, int P, const int32_t* ids,
                                                             int base, const int* count, int n, int C,
-                                                            int dim, uint64_t seed, uint32_t epoch,
-                                                            int stride, int dbg) {
+                                                            int algo, int dim, uint64_t seed,
+                                                            uint32_t epoch, int stride, int dbg) {
   extern __shared__ __align__(16) uint8_t lds[];
   constexpr int SP = WAVE / MZ_LPACK;
   const int used = count ? min(*count, n) : n;
@@ -790,21 +790,23 @@ __global__ __launch_bounds__(WAVE) void k_cand_compact_lite(MzCompact cc, int P,
     const int j = t / C, c = t - j * C;
     const uint64_t id = (uint64_t)(ids ? ids[j] : base + j);
     for (int k = 0; k < nm; ++k) {
-      const MzCellLds L = mz_lite_lds(lds + k * stride, P, dim);
+      const MzCellLds L = mz_lite_lds(lds + k * stride, P, dim, algo);
       mz_cells_clear(L);
       if (lane == 0) { L.sh[3] = 0; L.sh[4] = 0; }
     }
     __syncthreads();
     if ((lane % SP) == 0 && m < nm) {
-      const MzCellLds L = mz_lite_lds(lds + m * stride, P, dim);
+      const MzCellLds L = mz_lite_lds(lds + m * stride, P, dim, algo);
       const int W = L.W;
       MzRng rng{mz_cand_seed(seed, id, C, c, epoch, dbg), 0ull, {0u, 0u, 0u, 0u}};
       const int a = (int)rng.below((uint32_t)W), b = (int)rng.below((uint32_t)W);
       L.sh[2] = a * W + b;
-      mz_lite_rprim(L, a * W + b, rng);
+      if (algo == MZ_ALGO_DFS_DEV) mz_lite_dfs(L, a * W + b, rng);
+      else mz_lite_rprim(L, a * W + b, rng);
     }
     __syncthreads();
-    for (int k = 0; k < nm; ++k) mz_lite_finish(cc, t0 + k, mz_lite_lds(lds + k * stride, P, dim), dim, J, A);
+    for (int k = 0; k < nm; ++k)
+      mz_lite_finish(cc, t0 + k, mz_lite_lds(lds + k * stride, P, dim, algo), dim, J, A);
     __syncthreads();
   }
 }
@@ -1325,6 +1327,9 @@ hipError_t mz_lds_attr(const void* fn, size_t bytes) {
 #ifndef MZ_LITE  // r-prim candidates in the lite regions (A/B builds: 0)
 #define MZ_LITE 1
 #endif
+#ifndef MZ_LITE_DFS  // dfs candidates too
+#define MZ_LITE_DFS 1
+#endif
 #ifndef MZ_PACK_DFS  // dfs candidate lists packed too (A/B builds: 0)
 #define MZ_PACK_DFS 1
 #endif
@@ -1491,15 +1496,17 @@ hipError_t mz_launch_cand_compact(const MzCompact& cc, int P, const int32_t* ids
                                   int dbg) {
   if (n <= 0 || C <= 0) return hipSuccess;
   if (dim > P || cc.Qp < mz_compact_qp(P)) return hipErrorInvalidValue;
-  if (MZ_LITE && !algo_list && algo_all == MZ_ALGO_RPRIM_DEV) {  // r-prim: the lite regions
-    const size_t stride = mz_align16(mz_lite_lds_bytes(P));
+  if (MZ_LITE && !algo_list &&
+      (algo_all == MZ_ALGO_RPRIM_DEV || (MZ_LITE_DFS && algo_all == MZ_ALGO_DFS_DEV))) {
+    // r-prim / dfs: the lite regions
+    const size_t stride = mz_align16(mz_lite_lds_bytes(P, algo_all));
     const size_t lds = MZ_LPACK * stride + mz_lite_scratch_bytes(P);
     hipError_t ae = mz_lds_attr(reinterpret_cast<const void*>(k_cand_compact_lite), lds);
     if (ae != hipSuccess) return ae;
     const int total = (n * C + MZ_LPACK - 1) / MZ_LPACK;
     const int grid = std::max(1, MZ_BANK_WGS > 0 ? std::min(total, MZ_BANK_WGS) : mz_build_grid(total, lds));
     hipLaunchKernelGGL(k_cand_compact_lite, dim3(grid), dim3(WAVE), lds, s, cc, P, ids, base, count,
-                       n, C, dim, seed, epoch, (int)stride, dbg);
+                       n, C, algo_all, dim, seed, epoch, (int)stride, dbg);
     return hipGetLastError();
   }
   const bool packed = MZ_PACK > 1 && !algo_list &&

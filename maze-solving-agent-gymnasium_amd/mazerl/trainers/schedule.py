@@ -193,7 +193,8 @@ class WinSchedule:
         out = {"rule": self.rule, "total_wins": int(self.total_wins),  # (global: all ranks')
                "instances_per_algorithm": dict(zip(
                    names, torch.bincount(self.maze_algo.long(), minlength=3).tolist())),
-               "new_mazes_per_algorithm": dict(zip(names, self.new_mazes.tolist()))}
+               "new_mazes_per_algorithm": dict(zip(names, self.new_mazes.tolist())),
+               "wins_per_instance_median": float(self.inst_wins.float().median())}
         if self.growth is not None:
             sizes = growth_sizes(*self.growth)
             cnt = torch.bincount((self.dim - self.growth[0]) // 4, minlength=len(sizes)).tolist()

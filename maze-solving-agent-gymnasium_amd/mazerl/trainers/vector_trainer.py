@@ -297,7 +297,28 @@ def load_selected(env, mazes):
     env.reset()
 
 
-def steps_done_epsilon(learner, num_mazes):
+def snapshot_mazes(env, ids):
+    """The listed instances' current mazes as best_of_mazes returns them (grids uint8 [n, D, D],
+    start_goal int32 [n, 4], sizes [n]; D = the largest): the mazes the reference's env keeps in
+    `env.mazes` — the first one and each win's update_maze replacement (simple_maze_env.py:81-94)
+    — are, for a trained instance, the mazes it holds over training; evaluate(mazes=...) replays
+    them as test(n, new=False) does (update_visited_maze(remove=True), :96-116)."""
+    import numpy as np
+    ids = [int(i) for i in ids]
+    qs = [env.query(i) for i in ids]
+    D = max(q["n"] for q in qs)
+    grids = np.zeros((len(ids), D, D), np.uint8)
+    sg = np.zeros((len(ids), 4), np.int32)
+    sizes = np.zeros(len(ids), np.int32)
+    for k, (i, q) in enumerate(zip(ids, qs)):
+        g = env.grid(i)
+        grids[k, :g.shape[0], :g.shape[1]] = g
+        sg[k] = (q["start_r"], q["start_c"], q["goal_r"], q["goal_c"])
+        sizes[k] = q["n"]
+    return grids, sg, sizes
+
+
+def steps_done_epsilon(learner, num_mazes, instances=None):
     """The reference's test-time epsilon (test() acts through DQNAgent.get_action, dqn_agent.py:
     104-119: eps = eps_final + (eps_start - eps_final) * exp(-steps_done / decay), steps_done += 1
     per action, never reset during test): a callable k -> per-maze epsilon after k actions, each
@@ -306,7 +327,8 @@ def steps_done_epsilon(learner, num_mazes):
     after another on one counter."""
     sd0 = learner.steps_done.detach().float()
     B = sd0.numel()
-    idx = torch.arange(num_mazes, device=sd0.device) % B
+    idx = (torch.arange(num_mazes, device=sd0.device) % B if instances is None else
+           torch.as_tensor(instances, dtype=torch.long, device=sd0.device))  # (seen mazes: their own)
     sd0 = sd0[idx]
     dec = learner.eps_decay
     dec = dec[idx] if torch.is_tensor(dec) and dec.dim() > 0 else torch.full_like(sd0, float(dec))
