@@ -97,9 +97,10 @@ def parse(argv=None):
     # the per-instance rule's leg: each instance is a trainer of its own (its own wins,
     # epsilon_decay and steps_done), so it needs the reference's per-agent cadence — an instance
     # reaches its 10th win (dfs) only once its own epsilon has decayed: fewer instances, more
-    # vector steps (41 x 41: epsilon(16,000 steps) = 0.12 before the x3 / x4)
+    # vector steps (41 x 41: epsilon(16,000 steps) = 0.12 before the x3 / x4; at 16,000 steps every
+    # instance had passed its 5th win and none its 10th, profiles/r06/bench_full_r06e.json)
     ap.add_argument("--curriculum-pi-envs", type=int, default=512)
-    ap.add_argument("--curriculum-pi-steps", type=int, default=16000)
+    ap.add_argument("--curriculum-pi-steps", type=int, default=32000)
     ap.add_argument("--curriculum-pi-updates", type=int, default=2)
     ap.add_argument("--curriculum-rules", default="global,per-instance",
                     help="change_algorithm over the learner's wins (global: the reference's one "

@@ -57,7 +57,7 @@ struct ScrL {
   uint16_t *pp, *X, *Y, *Z;  // parent point; hallway root; branch root / rank; ranks, first()
   double* S;                 // [Hmax] hallway sums of 1 / (2 d)
   uint32_t* D;               // [Hmax] hallway sums of d
-  uint16_t *hroot, *hb;      // [Hmax] hallway root cell, branch rank
+  uint16_t* hb;              // [Hmax] hallway branch rank (over pas: dead after step 1)
   double* Cb;                // [Bmax] branch sums
   int* sh;
   int Hmax, Bmax;
@@ -68,7 +68,8 @@ __host__ __device__ inline size_t a16(size_t x) { return (x + 15) & ~(size_t)15;
 // LDS plan for candidates of stride Qp (cells, a multiple of 16); base null: bytes only
 __host__ __device__ inline size_t scr_layout(int Qp, ScrL* L, uint8_t* base) {
   const size_t Q = (size_t)Qp, QW = (Q + 31) / 32;
-  const int Hmax = Qp / 2 + 16, Bmax = Qp / 4 + 16;
+  // (32.4 KB at 81 x 81: five waves per CU; a maze past these caps is declined -> exact kernel)
+  const int Hmax = Qp / 2, Bmax = Qp / 4 + 16;
   size_t off = 0;
   auto take = [&](size_t bytes) { uint8_t* p = base ? base + off : nullptr; off += a16(bytes); return p; };
   uint8_t* sh = take(64);
@@ -83,8 +84,6 @@ __host__ __device__ inline size_t scr_layout(int Qp, ScrL* L, uint8_t* base) {
   uint8_t* S = take(8 * (size_t)Hmax);
   uint8_t* Cb = take(8 * (size_t)Bmax);
   uint8_t* D = take(4 * (size_t)Hmax);
-  uint8_t* hr = take(2 * (size_t)Hmax);
-  uint8_t* hb = take(2 * (size_t)Hmax);
   if (L) {
     L->sh = reinterpret_cast<int*>(sh);
     L->pas = pas;
@@ -98,8 +97,7 @@ __host__ __device__ inline size_t scr_layout(int Qp, ScrL* L, uint8_t* base) {
     L->S = reinterpret_cast<double*>(S);
     L->Cb = reinterpret_cast<double*>(Cb);
     L->D = reinterpret_cast<uint32_t*>(D);
-    L->hroot = reinterpret_cast<uint16_t*>(hr);
-    L->hb = reinterpret_cast<uint16_t*>(hb);
+    L->hb = reinterpret_cast<uint16_t*>(pas);  // 2 Hmax = Qp bytes
     L->Hmax = Hmax;
     L->Bmax = Bmax;
   }
@@ -253,14 +251,19 @@ __device__ void screen_one(const MzCompact& cc, int t, uint8_t* lds, double* out
     bool tconv = false;
     for (int it = 0; it < 20 && !tconv; ++it) {
       bool ch = false;
-      for (int q = lane; q < Q; q += WV) {
-        const uint32_t tc = TC[q];
-        if (tc == 0xFFFFFFFFu) continue;
-        const int a = (int)(tc & 0xFFFFu);
-        const uint32_t ta = TC[a];
-        if ((int)(ta & 0xFFFFu) != a) {  // a is not a top: jump to its target, keep its C
-          TC[q] = ta;
-          ch = true;
+      for (int q0 = lane; q0 < Q; q0 += 4 * WV) {
+        uint32_t tc[4], ta[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) tc[u] = q0 + u * WV < Q ? TC[q0 + u * WV] : 0xFFFFFFFFu;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) ta[u] = tc[u] != 0xFFFFFFFFu ? TC[tc[u] & 0xFFFFu] : 0u;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (tc[u] == 0xFFFFFFFFu) continue;
+          if ((ta[u] & 0xFFFFu) != (tc[u] & 0xFFFFu)) {  // not at a top: jump, keep the target's C
+            TC[q0 + u * WV] = ta[u];
+            ch = true;
+          }
         }
       }
       tconv = !__any(ch);
@@ -299,16 +302,24 @@ __device__ void screen_one(const MzCompact& cc, int t, uint8_t* lds, double* out
   bool conv = false;
   for (int it = 0; it < 20 && !conv; ++it) {
     bool ch = false;
-    for (int q = lane; q < Q; q += WV) {
-      const int a = L.X[q];
-      if (a != NONE) {
-        const int b = L.X[a];
-        if (b != a) { L.X[q] = (uint16_t)b; ch = true; }
+    for (int q0 = lane; q0 < Q; q0 += 4 * WV) {  // 4 cells' loads in flight per lane
+      int a[4], b[4], c[4], d[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int q = q0 + u * WV;
+        a[u] = q < Q ? L.X[q] : NONE;
+        c[u] = q < Q ? L.Y[q] : NONE;
       }
-      const int c = L.Y[q];
-      if (c != NONE) {
-        const int d = L.Y[c];
-        if (d != c) { L.Y[q] = (uint16_t)d; ch = true; }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        b[u] = a[u] != NONE ? L.X[a[u]] : NONE;
+        d[u] = c[u] != NONE ? L.Y[c[u]] : NONE;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int q = q0 + u * WV;
+        if (a[u] != NONE && b[u] != a[u]) { L.X[q] = (uint16_t)b[u]; ch = true; }
+        if (c[u] != NONE && d[u] != c[u]) { L.Y[q] = (uint16_t)d[u]; ch = true; }
       }
     }
     conv = !__any(ch);
@@ -339,7 +350,6 @@ __device__ void screen_one(const MzCompact& cc, int t, uint8_t* lds, double* out
       const int h = Hn + __popcll(m & ((1ull << lane) - 1ull));
       if (h < L.Hmax) {
         L.Z[q] = (uint16_t)h;
-        L.hroot[h] = (uint16_t)q;
         L.hb[h] = L.Y[q];
         L.S[h] = 0.0;
         L.D[h] = 0u;
