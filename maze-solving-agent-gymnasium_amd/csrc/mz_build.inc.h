@@ -1183,6 +1183,130 @@ __device__ void mz_lite_dfs(const MzCellLds& L, int s, MzRng& rng) {
   }
 }
 
+// The lite carves with their Philox words prefetched (MZ_RING): a draw read inline runs a
+// Philox4x32-10 block (40 quarter-rate multiplies) on the carve's serial chain every 4th draw —
+// about a third of an r-prim iteration's cycles. The stream is counter-based (word n =
+// philox(key, n >> 2)[n & 3]), so the words can come from anywhere: each maze keeps a ring of
+// 4 SP words in LDS (SP = the lanes per maze), refilled by its SP lanes at once (one block each)
+// whenever its next iteration could pass the ring's end. The loop runs on every lane (the refill
+// check is a wave vote; the carve body is the maze's first lane's), and a carve reads its draws
+// from the ring in the order MzRng would produce them: the same mazes.
+template <int SP>
+__device__ inline void mz_ring_fill(uint32_t* ring, uint64_t key, int rb, int lane) {
+  const int k = lane % SP;
+  uint32_t o[4];
+  mz_philox(key, MZ_GEN_STREAM, (uint64_t)(rb >> 2) + (uint64_t)k, o);
+  *reinterpret_cast<uint4*>(ring + 4 * k) = make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+template <int SP>
+__device__ void mz_lite_carve_ring(const MzCellLds& L, int algo, uint64_t key, bool carver,
+                                   uint32_t* ring) {
+  constexpr int RW = 4 * SP;
+  const int lane = threadIdx.x, W = L.W;
+  const bool dfs = algo == MZ_ALGO_DFS_DEV;
+  uint32_t* pw = reinterpret_cast<uint32_t*>(L.pas);
+  int n = 0, rb = 0;  // (carver lanes) the next draw's index, the ring's first
+  mz_ring_fill<SP>(ring, key, 0, lane);
+  __syncthreads();
+  auto below = [&](uint32_t mm) {
+    const uint32_t u = ring[n - rb];
+    ++n;
+    return (uint32_t)(((uint64_t)u * mm) >> 32);
+  };
+  int nf = 0, top = 0;  // r-prim: frontier size; dfs: stack size (nf) and top
+  bool active = carver;
+  if (carver) {
+    // start = (randrange(1, G-1, 2), randrange(1, G-1, 2)) (maze_generation.py:21)
+    const int a = (int)below((uint32_t)W), b = (int)below((uint32_t)W);
+    const int s = a * W + b;
+    L.sh[2] = s;
+    cs_set(L.b0, s);
+    if (dfs) {
+      L.list[nf++] = (uint16_t)s;
+      top = s;
+    } else {
+      for (int k = 0; k < 4; ++k) {
+        const int j = cs_nb(s, k, W, L.mW);
+        if (j >= 0) { L.list[nf++] = (uint16_t)j; cs_set(L.b1, j); }
+      }
+    }
+  }
+  for (;;) {
+    const bool need = active && n + 2 > rb + RW;
+    if (__any(need)) {  // the mazes that need it refill, all their lanes at once
+      const int src = (lane / SP) * SP;
+      const int nn = __shfl(n, src);
+      if (__shfl((int)need, src)) mz_ring_fill<SP>(ring, key, nn & ~3, lane);
+      if (need) rb = n & ~3;
+      __syncthreads();
+    }
+    if (!__any(active)) break;
+    if (!active) continue;
+    if (dfs) {  // one step of deept_first_visit (maze_generation.py:101-128), as mz_lite_dfs
+      int j[4];
+      uint32_t w0[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        j[k] = cs_nb(top, k == 0 ? 2 : (k == 1 ? 3 : k - 2), W, L.mW);
+        const int jj = j[k] >= 0 ? j[k] : top;
+        w0[k] = L.b0[jj >> 5] >> (jj & 31);
+      }
+      uint64_t cand = 0;
+      int cnt = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (j[k] >= 0 && !(w0[k] & 1u)) mz_k4_push(cand, cnt, k);
+      if (!cnt) {
+        if (--nf > 0) top = L.list[nf - 1];
+        else active = false;
+        continue;
+      }
+      const int k = mz_k4(cand, (int)below((uint32_t)cnt));
+      const int dir = k == 0 ? 2 : (k == 1 ? 3 : k - 2);
+      const int jn = k == 0 ? j[0] : (k == 1 ? j[1] : (k == 2 ? j[2] : j[3]));
+      cs_link(L, top, dir);
+      cs_set(L.b0, jn);
+      atomicOr(pw + (jn >> 2), (uint32_t)((dir ^ 1) << 2) << (8 * (jn & 3)));
+      L.list[nf++] = (uint16_t)jn;
+      top = jn;
+    } else {  // one step of random_prim_visit (maze_generation.py:59-99), as mz_lite_rprim
+      const int i = (int)below((uint32_t)nf);
+      const int f = L.list[i];
+      L.list[i] = L.list[--nf];
+      int j[4];
+      uint32_t w0[4], w1[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        j[k] = cs_nb(f, k, W, L.mW);
+        const int jj = j[k] >= 0 ? j[k] : f;
+        w0[k] = L.b0[jj >> 5] >> (jj & 31);
+        w1[k] = L.b1[jj >> 5] >> (jj & 31);
+      }
+      uint64_t nb = 0;
+      int cnt = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (j[k] >= 0 && (w0[k] & 1u)) mz_k4_push(nb, cnt, j[k] | (k << 12));
+      if (cnt) {
+        const int v = mz_k4(nb, (int)below((uint32_t)cnt)), kk = v >> 12;
+        cs_set(L.b0, f);
+        cs_link(L, f, kk);
+        atomicOr(pw + (f >> 2), (uint32_t)(kk << 2) << (8 * (f & 3)));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (j[k] >= 0 && !(w0[k] & 1u) && !(w1[k] & 1u)) {
+            if (nf == L.cap) { L.sh[4] = 1; nf = 0; break; }  // past the cap: flagged, abandoned
+            L.list[nf++] = (uint16_t)j[k];
+            cs_set(L.b1, j[k]);
+          }
+        }
+      }
+      if (nf == 0) active = false;
+    }
+  }
+}
+
 // The finish of a lite candidate (wave-wide; J / A: the per-wave scratch): carve depths by pointer
 // jumping over the parent directions (J = ancestor | distance << 16), the goal as mz_cs_goal, the
 // distance field as mz_cs_dist's tree path (the goal's root path marked in b1: the solution's

@@ -773,6 +773,9 @@ __global__ __launch_bounds__(WAVE) void k_cand_compact_packed(MzCompact cc, int 
 #ifndef MZ_LPACK
 #define MZ_LPACK 4
 #endif
+#ifndef MZ_RING  // the lite carves' Philox words prefetched into an LDS ring (A/B builds: 0)
+#define MZ_RING 1
+#endif
 __global__ __launch_bounds__(WAVE) void k_cand_compact_lite(MzCompact cc, int P, const int32_t* ids,
                                                             int base, const int* count, int n, int C,
                                                             int algo, int dim, uint64_t seed,
@@ -795,7 +798,12 @@ __global__ __launch_bounds__(WAVE) void k_cand_compact_lite(MzCompact cc, int P,
       if (lane == 0) { L.sh[3] = 0; L.sh[4] = 0; }
     }
     __syncthreads();
-    if ((lane % SP) == 0 && m < nm) {
+    if (MZ_RING) {  // every lane: the carve loop with the Philox ring (mz_lite_carve_ring)
+      const MzCellLds L = mz_lite_lds(lds + m * stride, P, dim, algo);
+      uint32_t* ring = reinterpret_cast<uint32_t*>(lds + m * stride + mz_lite_lds_bytes(P, algo));
+      mz_lite_carve_ring<SP>(L, algo, mz_cand_seed(seed, id, C, c, epoch, dbg),
+                             (lane % SP) == 0 && m < nm, ring);
+    } else if ((lane % SP) == 0 && m < nm) {
       const MzCellLds L = mz_lite_lds(lds + m * stride, P, dim, algo);
       const int W = L.W;
       MzRng rng{mz_cand_seed(seed, id, C, c, epoch, dbg), 0ull, {0u, 0u, 0u, 0u}};
@@ -1330,6 +1338,7 @@ hipError_t mz_lds_attr(const void* fn, size_t bytes) {
 #ifndef MZ_LITE_DFS  // dfs candidates too
 #define MZ_LITE_DFS 1
 #endif
+
 #ifndef MZ_PACK_DFS  // dfs candidate lists packed too (A/B builds: 0)
 #define MZ_PACK_DFS 1
 #endif
@@ -1499,7 +1508,7 @@ hipError_t mz_launch_cand_compact(const MzCompact& cc, int P, const int32_t* ids
   if (MZ_LITE && !algo_list &&
       (algo_all == MZ_ALGO_RPRIM_DEV || (MZ_LITE_DFS && algo_all == MZ_ALGO_DFS_DEV))) {
     // r-prim / dfs: the lite regions
-    const size_t stride = mz_align16(mz_lite_lds_bytes(P, algo_all));
+    const size_t stride = mz_align16(mz_lite_lds_bytes(P, algo_all) + (MZ_RING ? 4 * 4 * (WAVE / MZ_LPACK) : 0));
     const size_t lds = MZ_LPACK * stride + mz_lite_scratch_bytes(P);
     hipError_t ae = mz_lds_attr(reinterpret_cast<const void*>(k_cand_compact_lite), lds);
     if (ae != hipSuccess) return ae;

@@ -372,6 +372,9 @@ class VectorDQNLearner:
                  act_bf16=True, t_max=150, updates_per_epoch=100, allreduce=None, seed=0,
                  use_graph=True, bit_stem=True, overlap=False, greedy_rows=True, acting="x3"):
         self.device = torch.device(device)
+        if self.device.type == "cuda":  # the tuned f32 GEMM choices (gemm_tuning.py)
+            from ..gemm_tuning import enable as _tuned_gemms
+            _tuned_gemms(self.device)
         torch.manual_seed(seed)
         self.variant = variant
         self.source = QNet(3, 6, 4, h_channels, hidden_dim, variant).to(self.device)

@@ -86,6 +86,8 @@ class VectorPPOTrainer:
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise RuntimeError("VectorPPOTrainer runs on the GPU (libmazerl HIP kernels)")
+        from ..gemm_tuning import enable as _tuned_gemms
+        _tuned_gemms(self.device)  # the tuned f32 GEMM choices (gemm_tuning.py)
         if env.window_bits is None or env.reward64 is None:
             raise ValueError("VectorPPOTrainer needs an env with window_bits=True, reward64=True")
         rule = curriculum_rule(curriculum)
