@@ -128,6 +128,12 @@ def parse(argv=None):
     ap.add_argument("--graph", type=int, default=1,
                     help="1: the timed env steps replay captured HIP graphs of k_step launches "
                          "(the Python launch loop is timed beside them); 0: eager launches")
+    # N > 1: the DQN / DDQN learners' reduce-scatter / all-gather captured inside the update graph
+    # (one replay per update; one RCCL rank: 357 vs 382 us per update, no collective 357,
+    # profiles/r06k/) instead of issued between two replays. Off by default: RCCL refuses two
+    # ranks on one GPU, so the captured path is verified at one rank only (tests/
+    # test_gpu_distributed.py) and the driver's multi-GPU runs keep the two-graph path
+    ap.add_argument("--graph-collectives", type=int, default=0)
     ap.add_argument("--graph-chunk", type=int, default=100, help="k_step launches per graph")
     ap.add_argument("--cfg1-episodes", type=int, default=350,
                     help="config 1: tabular Q-learning episodes (training_examples/.../test_q.py)")
@@ -184,7 +190,8 @@ def win_rate(a, dev, rank=0, world=1):
     L = VectorDQNLearner(a.envs, dev, variant="ddqn", lr=1e-3, eps_start=0.95, eps_final=0.1,
                          eps_decay=decay, gamma=0.7, batch_size=a.batch, capacity=2_000_000,
                          updates_per_step=a.updates_per_step, target_every=a.target_every,
-                         allreduce=GradAllReduce() if world > 1 else None, overlap=bool(a.overlap),
+                         allreduce=GradAllReduce() if world > 1 else None,
+                         graph_collectives=bool(a.graph_collectives), overlap=bool(a.overlap),
                          greedy_rows=bool(a.greedy_rows), acting=a.acting)
     if world > 1:
         broadcast_params(L.source)
@@ -251,7 +258,9 @@ def win_rate(a, dev, rank=0, world=1):
                            if L.greedy_rows else "every instance",
             "acting_head": a.acting,
             "grad_allreduce": (f"{dist.get_backend()} ({'RCCL' if dist.get_backend() == 'nccl' else 'rehearsal'}), "
-                               "one 8.56 MB fp32 bucket per update between two graph replays")
+                               "one 8.56 MB fp32 bucket per update, reduce-scatter + all-gather "
+                               + ("captured inside the update graph" if L.graph_collectives
+                                  else "between two graph replays"))
                               if world > 1 else None,
             "acting_argmax_agreement": agree,
             "best_of_6_selection_seconds": round(t6, 3),
@@ -290,7 +299,8 @@ def curriculum_leg(a, dev, rank=0, world=1, rule="global"):
                          eps_decay=decay, gamma=0.7, batch_size=a.curriculum_batch,
                          capacity=2_000_000, updates_per_step=updates,
                          target_every=a.target_every,
-                         allreduce=GradAllReduce() if world > 1 else None, overlap=bool(a.overlap),
+                         allreduce=GradAllReduce() if world > 1 else None,
+                         graph_collectives=bool(a.graph_collectives), overlap=bool(a.overlap),
                          greedy_rows=bool(a.greedy_rows), acting=a.acting, seed=1)
     if world > 1:
         broadcast_params(L.source)
@@ -428,7 +438,8 @@ def config_legs(a, dev, rank=0, world=1):
         L = VectorDQNLearner(B, dev, variant="dqn", lr=1e-3, eps_start=0.95, eps_final=0.1,
                              eps_decay=decay, gamma=0.7, batch_size=2048, updates_per_step=1,
                              capacity=2_000_000, target_every=13,
-                             allreduce=GradAllReduce() if world > 1 else None, overlap=True, seed=0)
+                             allreduce=GradAllReduce() if world > 1 else None,
+                         graph_collectives=bool(a.graph_collectives), overlap=True, seed=0)
         if world > 1:
             broadcast_params(L.source)
             L.target.load_state_dict(L.source.state_dict())
@@ -469,7 +480,8 @@ def config_legs(a, dev, rank=0, world=1):
         L = VectorDQNLearner(B, dev, variant="ddqn", lr=1e-3, eps_start=0.95, eps_final=0.1,
                              eps_decay=decay, gamma=0.7, batch_size=512, updates_per_step=4,
                              capacity=2_000_000, target_every=13,
-                             allreduce=GradAllReduce() if world > 1 else None, overlap=True, seed=0)
+                             allreduce=GradAllReduce() if world > 1 else None,
+                         graph_collectives=bool(a.graph_collectives), overlap=True, seed=0)
         if world > 1:
             broadcast_params(L.source)
             L.target.load_state_dict(L.source.state_dict())

@@ -36,6 +36,10 @@ STACK_ROWS = True  # DDQN on packed windows (GPU): source(s) and source(s') as o
 # the overlapped learner's K updates of a vector step as one graph replay (MZ_K_BLOCK=0: K replays;
 # bit-identical results either way, tests/test_determinism_gpu.py)
 K_BLOCK = os.environ.get("MZ_K_BLOCK", "1") != "0"
+# data-parallel learner: the gradient collectives captured inside the update graph (one replay:
+# backward, reduce-scatter, shard AdamW, all-gather; thread-local capture mode) instead of issued
+# from the host between two replays. MZ_GRAPH_COLLECTIVES=1 (or graph_collectives=True) turns it on.
+GRAPH_COLLECTIVES = os.environ.get("MZ_GRAPH_COLLECTIVES", "0") == "1"
 # GPU: the loss and its gradient w.r.t. the Q rows as two HIP launches (MZ_FUSED_LOSS=0: torch ops)
 FUSED_LOSS = os.environ.get("MZ_FUSED_LOSS", "1") != "0"
 # GPU: both nets' second activation + fc3 + the loss as one launch, its backward through fc3 and
@@ -370,7 +374,8 @@ class VectorDQNLearner:
                  eps_decay=8000.0, gamma=0.7, batch_size=128, capacity=1_000_000,
                  updates_per_step=1, target_every=100, hidden_dim=1024, h_channels=32,
                  act_bf16=True, t_max=150, updates_per_epoch=100, allreduce=None, seed=0,
-                 use_graph=True, bit_stem=True, overlap=False, greedy_rows=True, acting="x3"):
+                 use_graph=True, bit_stem=True, overlap=False, greedy_rows=True, acting="x3",
+                 graph_collectives=None):
         self.device = torch.device(device)
         if self.device.type == "cuda":  # the tuned f32 GEMM choices (gemm_tuning.py)
             from ..gemm_tuning import enable as _tuned_gemms
@@ -386,6 +391,9 @@ class VectorDQNLearner:
         # (N ranks) it is two graphs, backward + pack and unpack + clamp + AdamW, with the one
         # RCCL all-reduce of the flat bucket launched between the replays.
         self.use_graph = bool(use_graph) and self.device.type == "cuda"
+        # with an all-reduce: the collectives inside the one update graph (GRAPH_COLLECTIVES)
+        gc = GRAPH_COLLECTIVES if graph_collectives is None else bool(graph_collectives)
+        self.graph_collectives = gc and self.use_graph and allreduce is not None
         # the update's nets read the replay's packed windows through the HIP f32 stem
         # (agents/stem.py) instead of expanding them to f32 for MIOpen
         self.bit_stem = bool(bit_stem) and self.device.type == "cuda"
@@ -624,7 +632,7 @@ class VectorDQNLearner:
             for k in range(0 if block else K):
                 rp.idx_static.copy_(idx[k])
                 self._graph[0].replay()
-                if self.allreduce is not None:
+                if len(self._graph) == 2:
                     self.allreduce.reduce()
                     self._graph[1].replay()
                     self.allreduce.gather(self.source)
@@ -648,10 +656,11 @@ class VectorDQNLearner:
     # copies included), when neither the target sync nor the cosine schedule's step falls strictly
     # between two of them (those run on the host between replays); else the per-update replays.
     # The same kernels in the same order as K single-update replays: the same results bit for bit.
-    # Not with a gradient all-reduce (the collective runs between graph replays).
+    # Not with a gradient all-reduce issued between graph replays (graph_collectives: inside them).
     def _k_block_ok(self):
         K = self.updates_per_step
-        if K < 2 or self.allreduce is not None or not K_BLOCK or not self.bit_stem:
+        if K < 2 or (self.allreduce is not None and not self.graph_collectives) or not K_BLOCK \
+                or not self.bit_stem:
             return False
         n0 = self.n_updates
         return all((n0 + j) % self.target_every and (n0 + j) % self.updates_per_epoch
@@ -666,7 +675,7 @@ class VectorDQNLearner:
         g = torch.cuda.CUDAGraph()
         keep = rp.idx_static
         try:
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode=self._capture_mode()):
                 for k in range(K):
                     rp.idx_static = self._idx[slot][k]
                     loss = self._one_update(None, static=True)
@@ -811,6 +820,11 @@ class VectorDQNLearner:
     def _loss(self, state, a, r, nxt):
         return q_loss(self.source, self.target, state, a, r, nxt, self.gamma, self.variant == "ddqn")
 
+    def _capture_mode(self):
+        # thread-local: the process group's watchdog thread polls its collectives' events, which
+        # a global-mode capture forbids ("operation not permitted when stream is capturing")
+        return "thread_local" if self.allreduce is not None else "global"
+
     def _graph_update(self, expand, warmup=3):
         ar = self.allreduce
         if self._graph is None:
@@ -823,9 +837,11 @@ class VectorDQNLearner:
                 self._eager_updates += 1
                 return
             self.opt.zero_grad(set_to_none=True)
-            if ar is None:
+            if ar is None or self.graph_collectives:
+                # (with the collectives: the reduce-scatter / all-gather of learner_update are
+                # captured as graph nodes on RCCL's stream, forked from and joined back to this one)
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                with torch.cuda.graph(g, capture_error_mode=self._capture_mode()):
                     self._graph_loss = self._one_update(expand, static=True)
                 self._graph = (g,)
             else:
@@ -850,7 +866,7 @@ class VectorDQNLearner:
                 # the last eager warm-up's rows, which that update already applied
                 self.replay.idx_static.copy_(self.replay.sample_indices(self.batch_size))
         self._graph[0].replay()
-        if ar is not None:
+        if len(self._graph) == 2:
             ar.reduce()
             self._graph[1].replay()
             ar.gather(self.source)

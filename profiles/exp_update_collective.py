@@ -5,6 +5,8 @@ graphs, sequential schedule), timed with HIP events over 200 updates after 20 wa
   none       no process group collective (one graph: backward + clamp + AdamW)
   allreduce  graph A (backward), the 8.56 MB all-reduce, graph B (clamp + AdamW)
   sharded    graph A, reduce-scatter, graph B over the rank's shard, all-gather
+  sharded_ingraph / allreduce_ingraph  the same collectives captured inside ONE update graph
+             (graph_collectives=True, round 6)
 With one rank the collectives are local copies: the numbers bound the cost of the split graphs
 and the collective launches, not the xGMI transfer (the driver's 8-GPU runs). One JSON line."""
 import json
@@ -30,11 +32,12 @@ def main():
     dist.init_process_group("nccl", init_method="env://", device_id=torch.device("cuda", 0))
     env = VectorMazeEnv(4, 21, enrich=True, device="cuda", seed=1)
     rec = {}
-    for mode in ("none", "allreduce", "sharded", "none", "allreduce", "sharded"):
-        ar = None if mode == "none" else GradAllReduce(shard=(mode == "sharded"))
+    modes = ("none", "allreduce", "sharded", "allreduce_ingraph", "sharded_ingraph")
+    for mode in modes + modes:
+        ar = None if mode == "none" else GradAllReduce(shard=mode.startswith("sharded"))
         L = VectorDQNLearner(4, "cuda", variant="ddqn", batch_size=1024, capacity=8192,
                              updates_per_step=1, target_every=13, seed=5, use_graph=True,
-                             overlap=False, allreduce=ar)
+                             overlap=False, allreduce=ar, graph_collectives=mode.endswith("ingraph"))
         for k in range(8):
             _fill(L, n=1024, seed=k)
         for _ in range(20):
