@@ -94,13 +94,20 @@ def parse(argv=None):
     ap.add_argument("--curriculum-steps", type=int, default=2400,
                     help="DDQN vector steps of the curriculum leg (the reference's change_algorithm "
                          "training, evaluated under its test(new=True) protocol; 0 = skip)")
+    # the curriculum legs' exploration: epsilon_decay = the reference's ((N-1)^2 // 2) * 5 / 40, the
+    # reading the win-rate and config legs use (B instances feed one learner: at the reference's
+    # decay, 4,000 at 41 x 41, x12 after the global rule's first vector steps, epsilon stays near
+    # 0.9 for the whole leg — 18 wins in 2,420 vector steps, profiles/r06l; / 40: 4,104 wins,
+    # profiles/r06m). --curriculum-decay-div 1 = the reference's decay.
+    ap.add_argument("--curriculum-decay-div", type=float, default=40.0,
+                    help="the curriculum legs' epsilon_decay = the reference's ((N-1)^2 // 2) * 5 / this")
     # the per-instance rule's leg: each instance is a trainer of its own (its own wins,
-    # epsilon_decay and steps_done), so it needs the reference's per-agent cadence — an instance
-    # reaches its 10th win (dfs) only once its own epsilon has decayed: fewer instances, more
-    # vector steps (41 x 41: epsilon(16,000 steps) = 0.12 before the x3 / x4; at 16,000 steps every
-    # instance had passed its 5th win and none its 10th, profiles/r06/bench_full_r06e.json)
-    ap.add_argument("--curriculum-pi-envs", type=int, default=512)
-    ap.add_argument("--curriculum-pi-steps", type=int, default=32000)
+    # epsilon_decay and steps_done), so it needs the reference's per-agent cadence: an instance
+    # reaches dfs only after 5 prim&kill wins of its own. 1,024 instances x 60,000 vector steps:
+    # median 15 wins, 982 of 1,024 instances at dfs at the end (2,048 x 40,000: median 9, 705 at
+    # dfs; 512 x 16,000: median 7, none past prim&kill — profiles/r06m/)
+    ap.add_argument("--curriculum-pi-envs", type=int, default=1024)
+    ap.add_argument("--curriculum-pi-steps", type=int, default=60000)
     ap.add_argument("--curriculum-pi-updates", type=int, default=2)
     ap.add_argument("--curriculum-rules", default="global,per-instance",
                     help="change_algorithm over the learner's wins (global: the reference's one "
@@ -294,7 +301,7 @@ def curriculum_leg(a, dev, rank=0, world=1, rule="global"):
     env = VectorMazeEnv(B, dim, enrich=True, device=dev, algorithm="r-prim",
                         seed=0xC0CC0000 + rank * B, done_list=False, window=False,
                         window_bits=True, candidates=a.candidates)
-    decay = ((dim - 1) * (dim - 1) // 2) * 5
+    decay = ((dim - 1) * (dim - 1) // 2) * 5 / a.curriculum_decay_div
     L = VectorDQNLearner(B, dev, variant="ddqn", lr=1e-3, eps_start=0.95, eps_final=0.1,
                          eps_decay=decay, gamma=0.7, batch_size=a.curriculum_batch,
                          capacity=2_000_000, updates_per_step=updates,
@@ -334,6 +341,7 @@ def curriculum_leg(a, dev, rank=0, world=1, rule="global"):
                                  if rule == "global" else "each instance's own wins and "
                                  "epsilon_decay"))),
                 "grid": dim, "envs_per_gpu": B, "epsilon_decay": decay,
+                "epsilon_decay_reference": ((dim - 1) * (dim - 1) // 2) * 5,
                 "epsilon_decay_at_end": float(L.eps_decay) if not torch.is_tensor(L.eps_decay)
                 or L.eps_decay.dim() == 0 else float(L.eps_decay.float().mean()),
                 "updates_per_vector_step": updates, "batch": a.curriculum_batch,
