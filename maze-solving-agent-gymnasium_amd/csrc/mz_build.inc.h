@@ -1307,6 +1307,128 @@ __device__ void mz_lite_carve_ring(const MzCellLds& L, int algo, uint64_t key, b
   }
 }
 
+// The lite carves lane-parallel (MZ_LANES): every lane of a maze's SP-lane group runs the carve
+// loop, and lane k < 4 of the group takes neighbour k of an iteration — the four neighbour scans
+// that one lane ran back to back (cs_nb, the two set-bit reads, the candidate list as a packed
+// u64) become one pass over four lanes, the choices wave ballots (the group's 4-bit masks), and
+// the frontier pushes one store per pushing lane at its rank among them. The group's lanes keep
+// the same n / nf / top; the same draws in the same order, the same cells pushed in the same
+// order: the same mazes as mz_lite_carve_ring. An overflowing frontier is flagged as there
+// (the sequential loop's break at nf == cap before a push <=> nf + pushes > cap).
+template <int SP>
+__device__ void mz_lite_carve_lanes(const MzCellLds& L, int algo, uint64_t key, bool live,
+                                    uint32_t* ring) {
+  static_assert(SP >= 4 && SP <= 16 && 64 % SP == 0, "group of 4..16 lanes");
+  constexpr int RW = 4 * SP;
+  const int lane = threadIdx.x, gl = lane % SP, g0 = lane - gl, W = L.W;
+  const bool dfs = algo == MZ_ALGO_DFS_DEV;
+  uint32_t* pw = reinterpret_cast<uint32_t*>(L.pas);
+  int n = 0, rb = 0;  // the group's next draw and the ring's first word
+  mz_ring_fill<SP>(ring, key, 0, lane);
+  __syncthreads();
+  auto mulhi = [](uint32_t u, uint32_t mm) { return (int)(((uint64_t)u * mm) >> 32); };
+  // the group's 4-bit mask of a per-neighbour predicate (lanes g0 .. g0 + 3)
+  auto mask4 = [&](bool p) { return (uint32_t)(__ballot(p) >> g0) & 0xFu; };
+  auto nth = [](uint32_t m, int v) {  // position of the v-th (0-based) set bit of m
+    const uint32_t m1 = m & (m - 1u), m2 = m1 & (m1 - 1u), m3 = m2 & (m2 - 1u);
+    const uint32_t sel = v == 0 ? m : (v == 1 ? m1 : (v == 2 ? m2 : m3));
+    return __ffs(sel) - 1;
+  };
+  const bool nbl = gl < 4;  // a neighbour lane
+  // deept_first_visit's direction order (left, right, up, down) in cs_nb's numbering
+  const int ddir = gl == 0 ? 2 : (gl == 1 ? 3 : gl - 2);
+  int nf = 0, top = 0;  // r-prim: frontier size; dfs: stack size and top
+  bool active = live;
+  if (live) {
+    // start = (randrange(1, G-1, 2), randrange(1, G-1, 2)) (maze_generation.py:21)
+    const int a = mulhi(ring[0], (uint32_t)W), b = mulhi(ring[1], (uint32_t)W);
+    n = 2;
+    const int s0 = a * W + b;
+    if (gl == 0) { L.sh[2] = s0; cs_set(L.b0, s0); }
+    if (dfs) {
+      if (gl == 0) L.list[0] = (uint16_t)s0;
+      nf = 1;
+      top = s0;
+    } else {
+      const int j = nbl ? cs_nb(s0, gl, W, L.mW) : -1;
+      const uint32_t vm = mask4(j >= 0);
+      if (j >= 0) {
+        L.list[__popc(vm & ((1u << gl) - 1u))] = (uint16_t)j;
+        cs_set(L.b1, j);
+      }
+      nf = __popc(vm);
+    }
+  }
+  for (;;) {
+    const bool need = active && n + 2 > rb + RW;
+    if (__any(need)) {  // the groups that need it refill, all their lanes at once
+      if (need) {
+        mz_ring_fill<SP>(ring, key, n & ~3, lane);
+        rb = n & ~3;
+      }
+      __syncthreads();
+    }
+    if (!__any(active)) break;
+    if (!active) continue;
+    if (dfs) {  // one step of deept_first_visit (maze_generation.py:101-128)
+      const int j = nbl ? cs_nb(top, ddir, W, L.mW) : -1;
+      const bool unv = j >= 0 && !((L.b0[j >> 5] >> (j & 31)) & 1u);
+      const uint32_t cm = mask4(unv);
+      if (!cm) {
+        if (--nf > 0) top = L.list[nf - 1];
+        else active = false;
+        continue;
+      }
+      const int k = nth(cm, mulhi(ring[n - rb], (uint32_t)__popc(cm)));
+      ++n;
+      const int dir = k == 0 ? 2 : (k == 1 ? 3 : k - 2);
+      const int jn = cs_nb(top, dir, W, L.mW);
+      if (gl == 0) {
+        cs_link(L, top, dir);
+        cs_set(L.b0, jn);
+        atomicOr(pw + (jn >> 2), (uint32_t)((dir ^ 1) << 2) << (8 * (jn & 3)));
+        L.list[nf] = (uint16_t)jn;
+      }
+      ++nf;
+      top = jn;
+    } else {  // one step of random_prim_visit (maze_generation.py:59-99)
+      const uint32_t u0 = ring[n - rb], u1 = ring[n + 1 - rb];
+      const int i = mulhi(u0, (uint32_t)nf);
+      const int f = L.list[i];
+      const int last = L.list[nf - 1];
+      const int j = nbl ? cs_nb(f, gl, W, L.mW) : -1;
+      const int jj = j >= 0 ? j : f;
+      const bool in0 = j >= 0 && ((L.b0[jj >> 5] >> (jj & 31)) & 1u);
+      const bool in1 = (L.b1[jj >> 5] >> (jj & 31)) & 1u;
+      const uint32_t im = mask4(in0), fm = mask4(j >= 0 && !in0 && !in1);
+      if (gl == 0) L.list[i] = (uint16_t)last;  // list[i] = list[--nf]
+      --nf;
+      ++n;
+      if (im) {
+        const int kk = nth(im, mulhi(u1, (uint32_t)__popc(im)));
+        ++n;
+        if (gl == 0) {
+          cs_set(L.b0, f);
+          cs_link(L, f, kk);
+          atomicOr(pw + (f >> 2), (uint32_t)(kk << 2) << (8 * (f & 3)));
+        }
+        const int np = __popc(fm);
+        if (nf + np > L.cap) {  // past the cap: flagged, abandoned
+          if (gl == 0) L.sh[4] = 1;
+          nf = 0;
+        } else {
+          if ((fm >> gl) & 1u && nbl) {
+            L.list[nf + __popc(fm & ((1u << gl) - 1u))] = (uint16_t)j;
+            cs_set(L.b1, j);
+          }
+          nf += np;
+        }
+      }
+      if (nf == 0) active = false;
+    }
+  }
+}
+
 // The finish of a lite candidate (wave-wide; J / A: the per-wave scratch): carve depths by pointer
 // jumping over the parent directions (J = ancestor | distance << 16), the goal as mz_cs_goal, the
 // distance field as mz_cs_dist's tree path (the goal's root path marked in b1: the solution's

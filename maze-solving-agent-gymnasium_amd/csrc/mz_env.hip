@@ -776,6 +776,9 @@ __global__ __launch_bounds__(WAVE) void k_cand_compact_packed(MzCompact cc, int 
 #ifndef MZ_RING  // the lite carves' Philox words prefetched into an LDS ring (A/B builds: 0)
 #define MZ_RING 1
 #endif
+#ifndef MZ_LANES  // the lite carves lane-parallel (mz_lite_carve_lanes; A/B builds: 0)
+#define MZ_LANES 1
+#endif
 __global__ __launch_bounds__(WAVE) void k_cand_compact_lite(MzCompact cc, int P, const int32_t* ids,
                                                             int base, const int* count, int n, int C,
                                                             int algo, int dim, uint64_t seed,
@@ -801,8 +804,14 @@ __global__ __launch_bounds__(WAVE) void k_cand_compact_lite(MzCompact cc, int P,
     if (MZ_RING) {  // every lane: the carve loop with the Philox ring (mz_lite_carve_ring)
       const MzCellLds L = mz_lite_lds(lds + m * stride, P, dim, algo);
       uint32_t* ring = reinterpret_cast<uint32_t*>(lds + m * stride + mz_lite_lds_bytes(P, algo));
-      mz_lite_carve_ring<SP>(L, algo, mz_cand_seed(seed, id, C, c, epoch, dbg),
-                             (lane % SP) == 0 && m < nm, ring);
+      // r-prim: the group's lanes share each iteration (mz_lite_carve_lanes; 2,048 best-of-6
+      // selections 14.7 -> 11.6 ms, the same mazes); dfs keeps one lane per carve (its lane
+      // version measured slower, 18.8 -> 22.1 ms: profiles/r06o/)
+      if (MZ_LANES && algo != MZ_ALGO_DFS_DEV)
+        mz_lite_carve_lanes<SP>(L, algo, mz_cand_seed(seed, id, C, c, epoch, dbg), m < nm, ring);
+      else
+        mz_lite_carve_ring<SP>(L, algo, mz_cand_seed(seed, id, C, c, epoch, dbg),
+                               (lane % SP) == 0 && m < nm, ring);
     } else if ((lane % SP) == 0 && m < nm) {
       const MzCellLds L = mz_lite_lds(lds + m * stride, P, dim, algo);
       const int W = L.W;
