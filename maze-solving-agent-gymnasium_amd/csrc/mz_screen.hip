@@ -114,9 +114,18 @@ __device__ inline int wsum_i(int x) {
   return x;
 }
 
+// MZ_SCREEN_PROF (profiling builds only): block 0 prints the clock at each step boundary
+#ifndef MZ_SCREEN_PROF
+#define MZ_SCREEN_PROF 0
+#endif
+#define SCR_T(k)                                                       \
+  do {                                                                 \
+    if (MZ_SCREEN_PROF) scr_ts[(k) + 1] = __builtin_readcyclecounter(); \
+  } while (0)
 __device__ void screen_one(const MzCompact& cc, int t, uint8_t* lds, double* out,
                            int32_t* status) {
   const int lane = threadIdx.x;
+  unsigned long long scr_ts[11] = {};
   ScrL L;
   scr_layout(cc.Qp, &L, lds);
   const uint32_t meta = cc.meta[t];
@@ -129,6 +138,7 @@ __device__ void screen_one(const MzCompact& cc, int t, uint8_t* lds, double* out
       status[t] = 2;
     }
   };
+  SCR_T(-1);
   if ((meta & MZ_CMETA_NOSOL) || W < 2 || Q > cc.Qp || s >= Q || g >= Q || s == g) { fail(); return; }
   // exact division by W for q < 4096 (W <= 63): q * ceil(2^18 / W) >> 18
   const uint32_t mW = ((1u << 18) + (uint32_t)W - 1u) / (uint32_t)W;
@@ -144,34 +154,62 @@ __device__ void screen_one(const MzCompact& cc, int t, uint8_t* lds, double* out
     for (int i = lane; i < (Q + 1) / 2; i += WV) la[i] = ga[i];
     for (int i = lane; i < QW; i += WV) L.sol[i] = gs[i];
   }
+  SCR_T(0);
   __syncthreads();
   auto solbit = [&](int q) { return ((L.sol[q >> 5] >> (q & 31)) & 1u) != 0; };
   // ---- 1. per cell: degree, parent direction, point / solution flags; the maze must be a
   // spanning tree whose distances fall by 2 squares per step toward the goal
   int bad = 0, nedge = 0;
-  for (int q = lane; q < Q; q += WV) {
-    const int r = rowof(q), c = q - r * W;
-    const uint8_t pq = L.pas[q];
-    const bool up = r > 0 && (L.pas[q - W] & 2), dn = (pq & 2) != 0;
-    const bool lf = c > 0 && (L.pas[q - 1] & 1), rt = (pq & 1) != 0;
-    if ((dn && r == W - 1) || (rt && c == W - 1)) bad = 1;
-    nedge += (dn ? 1 : 0) + (rt ? 1 : 0);
-    const int deg = (int)up + (int)dn + (int)lf + (int)rt;
-    const int Aq = L.A[q];
-    int pd = -1;
-    if (q != g) {
-      if (up && L.A[q - W] + 2 == Aq) pd = 0;
-      if (dn && L.A[q + W] + 2 == Aq) pd = 1;
-      if (lf && L.A[q - 1] + 2 == Aq) pd = 2;
-      if (rt && L.A[q + 1] + 2 == Aq) pd = 3;
-      if (pd < 0) bad = 1;
-    } else if (Aq != 0 || deg != 1) {
-      bad = 1;  // the goal is a dead end (find_random_position keeps one-neighbour squares)
+  // (2 cells per lane and pass, every load of both issued before any of their flag stores: the
+  // byte stores may alias any LDS read, so a cell-at-a-time loop waited out each cell's reads)
+  for (int q0 = lane; q0 < Q; q0 += 2 * WV) {
+    uint8_t pq[2], pu[2], pl[2];
+    uint16_t aq[2], au[2], ad[2], al[2], ar[2];
+    uint32_t sw[2];
+    int rr[2], cc_[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = min(q0 + u * WV, Q - 1);
+      rr[u] = rowof(q);
+      cc_[u] = q - rr[u] * W;
+      pq[u] = L.pas[q];
+      pu[u] = L.pas[max(q - W, 0)];
+      pl[u] = L.pas[max(q - 1, 0)];
+      aq[u] = L.A[q];
+      au[u] = L.A[max(q - W, 0)];
+      ad[u] = L.A[min(q + W, Q - 1)];
+      al[u] = L.A[max(q - 1, 0)];
+      ar[u] = L.A[min(q + 1, Q - 1)];
+      sw[u] = L.sol[q >> 5];
     }
-    const bool corner = deg == 2 && !(up && dn) && !(lf && rt);
-    const bool pt = deg != 2 || corner || q == s || q == g;
-    L.fl[q] = (uint8_t)(deg | (pt ? F_PT : 0) | (solbit(q) ? F_SOL : 0) | ((pd < 0 ? 0 : pd) << F_PD));
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = q0 + u * WV;
+      if (q >= Q) continue;
+      const int r = rr[u], c = cc_[u];
+      const bool up = r > 0 && (pu[u] & 2), dn = (pq[u] & 2) != 0;
+      const bool lf = c > 0 && (pl[u] & 1), rt = (pq[u] & 1) != 0;
+      if ((dn && r == W - 1) || (rt && c == W - 1)) bad = 1;
+      nedge += (dn ? 1 : 0) + (rt ? 1 : 0);
+      const int deg = (int)up + (int)dn + (int)lf + (int)rt;
+      const int Aq = aq[u];
+      int pd = -1;
+      if (q != g) {
+        if (up && au[u] + 2 == Aq) pd = 0;
+        if (dn && ad[u] + 2 == Aq) pd = 1;
+        if (lf && al[u] + 2 == Aq) pd = 2;
+        if (rt && ar[u] + 2 == Aq) pd = 3;
+        if (pd < 0) bad = 1;
+      } else if (Aq != 0 || deg != 1) {
+        bad = 1;  // the goal is a dead end (find_random_position keeps one-neighbour squares)
+      }
+      const bool corner = deg == 2 && !(up && dn) && !(lf && rt);
+      const bool pt = deg != 2 || corner || q == s || q == g;
+      const bool sb = ((sw[u] >> (q & 31)) & 1u) != 0;
+      L.fl[q] = (uint8_t)(deg | (pt ? F_PT : 0) | (sb ? F_SOL : 0) | ((pd < 0 ? 0 : pd) << F_PD));
+    }
   }
+  SCR_T(1);
   nedge = wsum_i(nedge);
   if (__any(bad) || nedge != Q - 1 || !solbit(s) || !solbit(g)) { fail(); return; }
   __syncthreads();
@@ -187,6 +225,7 @@ __device__ void screen_one(const MzCompact& cc, int t, uint8_t* lds, double* out
     L.pp[q] = p;
   }
   __syncthreads();
+  SCR_T(2);
   // ---- 3. hallway 0, the solution branch (:65-71): its edges, in any order
   double s0 = 0.0;
   long d0 = 0;
@@ -208,6 +247,7 @@ __device__ void screen_one(const MzCompact& cc, int t, uint8_t* lds, double* out
     d0 += (long)__shfl_xor((int)d0, o);  // d0 < 2^31 (at most the maze's squares)
     n0 += ny;
   }
+  SCR_T(3);
   // ---- 4. the break's excluded junctions: a degree-4 hallway node p whose parent is a solution
   // junction adds only its first child's junction before the break; its first child is the one
   // whose subtree holds the smallest dead end (row-major) below p. Every off-solution point x gets
@@ -288,27 +328,43 @@ __device__ void screen_one(const MzCompact& cc, int t, uint8_t* lds, double* out
     }
     __syncthreads();
   }
-  // ---- 5. hallway roots (X) and branch roots (Y): pointer jumping up the pp links
-  for (int q = lane; q < Q; q += WV) {
-    const uint8_t f = L.fl[q];
-    uint16_t x = NONE, y = NONE;
-    const int p = L.pp[q];
-    if (fh(f)) x = fh(L.fl[p]) ? (uint16_t)p : (uint16_t)q;
-    if (fb(f)) y = (p != NONE && fb(L.fl[p])) ? (uint16_t)p : (uint16_t)q;
-    L.X[q] = x;
-    L.Y[q] = y;
+  SCR_T(4);
+  // ---- 5. hallway roots (X) and branch roots (Y): pointer jumping up the pp links, each round
+  // over a worklist of the entries that moved in the previous one (an entry whose target is
+  // already a root never moves again), compacted by wave ballots into the Z / S regions (free
+  // until steps 6 / 7)
+  uint16_t* WLs[2] = {L.Z, reinterpret_cast<uint16_t*>(L.S)};
+  int nw = 0;
+  for (int b0 = 0; b0 < Q; b0 += WV) {
+    const int q = b0 + lane;
+    bool live = false;
+    if (q < Q) {
+      const uint8_t f = L.fl[q];
+      uint16_t x = NONE, y = NONE;
+      const int p = L.pp[q];
+      if (fh(f)) x = fh(L.fl[p]) ? (uint16_t)p : (uint16_t)q;
+      if (fb(f)) y = (p != NONE && fb(L.fl[p])) ? (uint16_t)p : (uint16_t)q;
+      L.X[q] = x;
+      L.Y[q] = y;
+      live = (x != NONE && x != q) || (y != NONE && y != q);
+    }
+    const unsigned long long m = __ballot(live);
+    if (live) WLs[0][nw + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)q;
+    nw += __popcll(m);
   }
   __syncthreads();
-  bool conv = false;
-  for (int it = 0; it < 20 && !conv; ++it) {
-    bool ch = false;
-    for (int q0 = lane; q0 < Q; q0 += 4 * WV) {  // 4 cells' loads in flight per lane
-      int a[4], b[4], c[4], d[4];
+  for (int it = 0, cur = 0; it < 20 && nw > 0; ++it, cur ^= 1) {
+    const uint16_t* wl = WLs[cur];
+    uint16_t* wn = WLs[cur ^ 1];
+    int mw = 0;
+    for (int i0 = 0; i0 < nw; i0 += 4 * WV) {  // 4 entries' loads in flight per lane
+      int q[4], a[4], b[4], c[4], d[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) q[u] = i0 + u * WV + lane < nw ? (int)wl[i0 + u * WV + lane] : -1;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int q = q0 + u * WV;
-        a[u] = q < Q ? L.X[q] : NONE;
-        c[u] = q < Q ? L.Y[q] : NONE;
+        a[u] = q[u] >= 0 ? L.X[q[u]] : NONE;
+        c[u] = q[u] >= 0 ? L.Y[q[u]] : NONE;
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -317,15 +373,19 @@ __device__ void screen_one(const MzCompact& cc, int t, uint8_t* lds, double* out
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int q = q0 + u * WV;
-        if (a[u] != NONE && b[u] != a[u]) { L.X[q] = (uint16_t)b[u]; ch = true; }
-        if (c[u] != NONE && d[u] != c[u]) { L.Y[q] = (uint16_t)d[u]; ch = true; }
+        bool moved = false;
+        if (a[u] != NONE && b[u] != a[u]) { L.X[q[u]] = (uint16_t)b[u]; moved = true; }
+        if (c[u] != NONE && d[u] != c[u]) { L.Y[q[u]] = (uint16_t)d[u]; moved = true; }
+        const unsigned long long m = __ballot(moved);
+        if (moved) wn[mw + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)q[u];
+        mw += __popcll(m);
       }
     }
-    conv = !__any(ch);
+    nw = mw;
     __syncthreads();
   }
-  if (!conv) { fail(); return; }
+  if (nw > 0) { fail(); return; }
+  SCR_T(5);
   // ---- 6. branch ranks (Z at the branch roots), then each hallway root's branch rank (Y)
   int Bn = 0;
   for (int b0 = 0; b0 < Q; b0 += WV) {
@@ -340,6 +400,7 @@ __device__ void screen_one(const MzCompact& cc, int t, uint8_t* lds, double* out
   for (int q = lane; q < Q; q += WV)
     if (fh(L.fl[q]) && L.X[q] == q) L.Y[q] = L.Z[L.Y[q]];
   __syncthreads();
+  SCR_T(6);
   // ---- 7. hallway ranks (Z at the hallway roots), accumulators
   int Hn = 0;
   for (int b0 = 0; b0 < Q; b0 += WV) {
@@ -360,6 +421,7 @@ __device__ void screen_one(const MzCompact& cc, int t, uint8_t* lds, double* out
   if (Hn > L.Hmax) { fail(); return; }
   for (int b = lane; b < Bn; b += WV) L.Cb[b] = 0.0;
   __syncthreads();
+  SCR_T(7);
   // ---- 8. every off-solution edge (x, pp(x)) into the hallway that holds it
   int nt = 0;
   for (int q = lane; q < Q; q += WV) {
@@ -382,6 +444,7 @@ __device__ void screen_one(const MzCompact& cc, int t, uint8_t* lds, double* out
   }
   if (__any(bad)) { fail(); return; }
   __syncthreads();
+  SCR_T(8);
   // ---- 9. C_h = D_h * S_h into its branch; the product over branches, then C_0
   for (int h = lane; h < Hn; h += WV)
     atomicAdd(&L.Cb[L.hb[h]], __dmul_rn((double)L.D[h], L.S[h]));
@@ -401,6 +464,12 @@ __device__ void screen_one(const MzCompact& cc, int t, uint8_t* lds, double* out
     out[2 * t + 1] = 2.5 * K * 0x1p-53;
     status[t] = (prod > 0.0 && prod < __longlong_as_double(0x7FF0000000000000ll)) ? 0 : 2;
   }
+  SCR_T(9);
+  if (MZ_SCREEN_PROF && lane == 0 && blockIdx.x == 0)
+    printf("scr %d %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu\n", t, scr_ts[1] - scr_ts[0],
+           scr_ts[2] - scr_ts[1], scr_ts[3] - scr_ts[2], scr_ts[4] - scr_ts[3], scr_ts[5] - scr_ts[4],
+           scr_ts[6] - scr_ts[5], scr_ts[7] - scr_ts[6], scr_ts[8] - scr_ts[7], scr_ts[9] - scr_ts[8],
+           scr_ts[10] - scr_ts[9]);
 }
 
 __global__ __launch_bounds__(WV) void k_screen(MzCompact cc, int n, double* out, int32_t* status,
