@@ -1354,6 +1354,13 @@ hipError_t mz_lds_attr(const void* fn, size_t bytes) {
 #ifndef MZ_BANK_WGS
 #define MZ_BANK_WGS 0
 #endif
+// resident lite candidate builds (k_cand_compact_lite; 0 = as many as fit, 7 per CU at 81 x 81):
+// the refill shares the chip with the trainer's acting and update streams, and builds past 5 per
+// CU hold LDS their kernels wait for — best-of-6 DDQN training 71.5 -> 75.3 M env steps/s at
+// 1,280 (768 / 1,024 / 1,536 / 1,792 / all: 70.2 / 73.8 / 71.3 / 72.6 / 71.5 M, profiles/r06t/)
+#ifndef MZ_LITE_WGS
+#define MZ_LITE_WGS 1280
+#endif
 // Build launches: the LDS one maze build needs — the cell-space layouts for Philox mazes
 // (mz_build_cells), else the square grid (+ the CPython generator's tables) — and a persistent
 // grid of 4,096 workgroups or, when more fit, as many as can be resident at once (256 CUs x the
@@ -1522,7 +1529,8 @@ hipError_t mz_launch_cand_compact(const MzCompact& cc, int P, const int32_t* ids
     hipError_t ae = mz_lds_attr(reinterpret_cast<const void*>(k_cand_compact_lite), lds);
     if (ae != hipSuccess) return ae;
     const int total = (n * C + MZ_LPACK - 1) / MZ_LPACK;
-    const int grid = std::max(1, MZ_BANK_WGS > 0 ? std::min(total, MZ_BANK_WGS) : mz_build_grid(total, lds));
+    const int cap = MZ_BANK_WGS > 0 ? MZ_BANK_WGS : MZ_LITE_WGS;
+    const int grid = std::max(1, cap > 0 ? std::min(total, cap) : mz_build_grid(total, lds));
     hipLaunchKernelGGL(k_cand_compact_lite, dim3(grid), dim3(WAVE), lds, s, cc, P, ids, base, count,
                        n, C, algo_all, dim, seed, epoch, (int)stride, dbg);
     return hipGetLastError();

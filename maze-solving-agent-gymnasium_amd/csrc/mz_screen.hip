@@ -484,6 +484,13 @@ __global__ __launch_bounds__(WV) void k_screen(MzCompact cc, int n, double* out,
 
 }  // namespace
 
+// resident screens (0 = as many as the LDS holds, 5 per CU at 81 x 81): beside the trainer's
+// other streams 3 per CU leave them LDS — training 75.3 -> 77.6 M env steps/s at 768 (1,024:
+// 75.4 M; profiles/r06t/)
+#ifndef MZ_SCREEN_WGS
+#define MZ_SCREEN_WGS 768
+#endif
+
 size_t mz_screen_lds(int P) { return scr_layout((mz_compact_qp(P) + 15) & ~15, nullptr, nullptr); }
 
 hipError_t mz_launch_screen(const MzCompact& cc, int P, int n, double* out, int32_t* status,
@@ -497,7 +504,8 @@ hipError_t mz_launch_screen(const MzCompact& cc, int P, int n, double* out, int3
     if (e != hipSuccess) return e;
   }
   const int per_cu = (int)(160 * 1024 / bytes) > 0 ? (int)(160 * 1024 / bytes) : 1;
-  const int grid = n < 256 * per_cu ? n : 256 * per_cu;
+  int grid = n < 256 * per_cu ? n : 256 * per_cu;
+  if (MZ_SCREEN_WGS > 0 && grid > MZ_SCREEN_WGS) grid = MZ_SCREEN_WGS;
   hipLaunchKernelGGL(k_screen, dim3(grid), dim3(WV), bytes, s, cc, n, out, status, limit,
                      mult < 1 ? 1 : mult);
   return hipGetLastError();
