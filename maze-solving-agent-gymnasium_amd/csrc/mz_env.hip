@@ -1361,6 +1361,9 @@ hipError_t mz_lds_attr(const void* fn, size_t bytes) {
 #ifndef MZ_LITE_WGS
 #define MZ_LITE_WGS 1280
 #endif
+#ifndef MZ_EXPAND_WGS  // resident k_cand_expand workgroups (0 = the build grid)
+#define MZ_EXPAND_WGS 0
+#endif
 // Build launches: the LDS one maze build needs — the cell-space layouts for Philox mazes
 // (mz_build_cells), else the square grid (+ the CPython generator's tables) — and a persistent
 // grid of 4,096 workgroups or, when more fit, as many as can be resident at once (256 CUs x the
@@ -1571,7 +1574,9 @@ hipError_t mz_launch_cand_expand(const MzCompact& cc, const MzDev& dst, const in
   const size_t lds = mz_align16(mz_cell_lds_bytes(dst.P));
   hipError_t ae = mz_lds_attr(reinterpret_cast<const void*>(k_cand_expand), lds);
   if (ae != hipSuccess) return ae;
-  hipLaunchKernelGGL(k_cand_expand, dim3(std::max(1, mz_build_grid(n, lds))), dim3(WAVE), lds, s, cc,
+  const int eg = mz_build_grid(n, lds);
+  hipLaunchKernelGGL(k_cand_expand, dim3(std::max(1, MZ_EXPAND_WGS > 0 ? std::min(eg, MZ_EXPAND_WGS) : eg)),
+                     dim3(WAVE), lds, s, cc,
                      dst, dst_ids, base, count, n, C, pick, algo_list, algo_all);
   return hipGetLastError();
 }
