@@ -6,7 +6,7 @@
 # leg's MIN all-reduce of the retired flags)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
-O=gpurun_out/r06i
+O=gpurun_out/r06i2
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 MZ_DIST_BACKEND=gloo timeout -k 10 900 python -u bench.py --gpus 4 --envs 16384 --steps 100 --warmup 10 --train-steps 100 --curriculum-steps 100 \
