@@ -8,8 +8,10 @@ Writes profiles/<tag>_kernel_stats.csv (copy of rocprofv3 --stats) and the <mode
 profiles/pmc_k_step.json (stamped with the hash of k_step's sources: bench.py uses a record only
 while the sources are unchanged):
 per-launch HBM bytes of k_step = (2 x FETCH_SIZE + WRITE_SIZE) x 1024, the gfx950 correction of
-MI355X_MICROARCH.md §HBM (FETCH_SIZE reads half of the bytes of wide streaming reads; the
-gathers of k_step are uncalibrated, so the doubled figure is an upper bound on its read side).
+MI355X_MICROARCH.md §HBM (FETCH_SIZE tallies 64 B per L2-miss request, and every request is a
+128-B line: calibrated for k_step's own read shapes — u32 gathers, 64-B coalesced state loads,
+15-row window gathers — in profiles/r06x/fetch_calibration.json, so the doubled figure is the
+line traffic of k_step's reads).
 """
 import argparse
 import csv
