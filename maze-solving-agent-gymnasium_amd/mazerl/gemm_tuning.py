@@ -32,11 +32,14 @@ def enable(device=None):
     if "gfx950" not in torch.cuda.get_device_properties(device).gcnArchName:
         return False
     import torch.cuda.tunable as T
-    T.enable(True)
-    T.tuning_enable(False)
-    # (torch writes its in-memory results at exit: to a scratch file, never into the package)
-    T.set_filename(os.path.join(tempfile.gettempdir(), f"mazerl_tunableop_{os.getpid()}.csv"))
-    ok = bool(T.read_file(_FILE))
+    try:
+        T.enable(True)
+        T.tuning_enable(False)
+        # (torch writes its in-memory results at exit: to a scratch file, never into the package)
+        T.set_filename(os.path.join(tempfile.gettempdir(), f"mazerl_tunableop_{os.getpid()}.csv"))
+        ok = bool(T.read_file(_FILE))
+    except RuntimeError:  # an unreadable file or a torch without TunableOp: torch's defaults
+        ok = False
     if not ok:
         T.enable(False)
     _state["active"] = ok
