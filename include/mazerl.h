@@ -336,6 +336,12 @@ int mz_stem_forward(const uint32_t* bits_dev, const float* obs6_dev, int32_t n,
 int mz_stem_backward(const uint32_t* bits_dev, const uint8_t* code_dev, const float* gfeat_dev,
                      int32_t ld, int32_t n, float drop_p, float* partial_dev, float* dw_dev,
                      float* db_dev, void* stream);
+/* mz_stem_backward that also advances the device u64 rng_advance_dev by one after the gradient
+ * launches (NULL: nothing advanced): a learner whose nets read one dropout counter in every
+ * forward of an update moves it on from the backward, with no launch of its own per forward. */
+int mz_stem_backward_ex(const uint32_t* bits_dev, const uint8_t* code_dev, const float* gfeat_dev,
+                        int32_t ld, int32_t n, float drop_p, float* partial_dev, float* dw_dev,
+                        float* db_dev, uint64_t* rng_advance_dev, void* stream);
 int mz_stem_workspace_floats(int32_t n);
 
 /* The learner's parameter update: grad.clamp_(-clamp, clamp) on every parameter, then one

@@ -607,16 +607,23 @@ int mz_stem_forward(const uint32_t* bits_dev, const float* obs6_dev, int32_t n,
   return MZ_OK;
 }
 
-int mz_stem_backward(const uint32_t* bits_dev, const uint8_t* code_dev, const float* gfeat_dev,
-                     int32_t ld, int32_t n, float drop_p, float* partial_dev, float* dw_dev,
-                     float* db_dev, void* stream) {
+int mz_stem_backward_ex(const uint32_t* bits_dev, const uint8_t* code_dev, const float* gfeat_dev,
+                        int32_t ld, int32_t n, float drop_p, float* partial_dev, float* dw_dev,
+                        float* db_dev, uint64_t* rng_advance_dev, void* stream) {
   if (!bits_dev || !code_dev || !gfeat_dev || !partial_dev || !dw_dev || !db_dev || n < 0)
     return fail(MZ_EINVAL, "bad arguments");
   if (ld < 1568) return fail(MZ_EINVAL, "gradient stride %d", ld);
   if (!(drop_p >= 0.0f && drop_p < 1.0f)) return fail(MZ_EINVAL, "dropout p %g", (double)drop_p);
   MZ_HIP(mz_launch_stem_bwd(bits_dev, code_dev, gfeat_dev, ld, n, drop_p, partial_dev, dw_dev,
-                            db_dev, static_cast<hipStream_t>(stream)));
+                            db_dev, static_cast<hipStream_t>(stream), rng_advance_dev));
   return MZ_OK;
+}
+
+int mz_stem_backward(const uint32_t* bits_dev, const uint8_t* code_dev, const float* gfeat_dev,
+                     int32_t ld, int32_t n, float drop_p, float* partial_dev, float* dw_dev,
+                     float* db_dev, void* stream) {
+  return mz_stem_backward_ex(bits_dev, code_dev, gfeat_dev, ld, n, drop_p, partial_dev, dw_dev,
+                             db_dev, nullptr, stream);
 }
 
 int mz_adamw_flat(float* param_dev, float* exp_avg_dev, float* exp_avg_sq_dev,

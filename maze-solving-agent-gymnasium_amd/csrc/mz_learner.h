@@ -9,7 +9,7 @@ hipError_t mz_launch_stem_fwd(const uint32_t* bits, const float* obs6, int n, co
                               float* feat, int ld, uint8_t* code, hipStream_t s);
 hipError_t mz_launch_stem_bwd(const uint32_t* bits, const uint8_t* code, const float* g, int ld,
                               int n, float drop_p, float* partial, float* dw, float* db,
-                              hipStream_t s);
+                              hipStream_t s, uint64_t* advance = nullptr);
 #define MZ_OPT_MAX_SEGS 16
 
 hipError_t mz_launch_adamw(float* p, float* m, float* v, const float* const* grads,

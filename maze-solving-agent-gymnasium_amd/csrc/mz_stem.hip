@@ -269,9 +269,13 @@ __global__ __launch_bounds__(256) void k_stem_bwd(const uint32_t* __restrict__ b
         ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
 }
 
+// advance (nullable): the dropout counter the forward read, advanced here for the next forward —
+// the learner's nets read it in both forwards of an update and the source's backward moves it on,
+// so no separate add launch per forward (agents/stem.py stem_features(advance="backward"))
 __global__ void k_stem_reduce(const float* __restrict__ partial, int chunks, float* __restrict__ dw,
-                              float* __restrict__ db) {
+                              float* __restrict__ db, unsigned long long* advance) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (advance && t == 0) *advance = *advance + 1ull;
   if (t >= 32 * NACC) return;
   const int c = t / NACC, k = t - c * NACC;
   // 8 chunks' loads in flight before their adds (same order, so the same sums): the serial
@@ -317,16 +321,20 @@ hipError_t mz_launch_stem_fwd(const uint32_t* bits, const float* obs6, int n, co
 
 hipError_t mz_launch_stem_bwd(const uint32_t* bits, const uint8_t* code, const float* g, int ld,
                               int n, float drop_p, float* partial, float* dw, float* db,
-                              hipStream_t s) {
+                              hipStream_t s, uint64_t* advance) {
   const int chunks = mz_stem_chunks(n);
   if (chunks == 0) {
-    const hipError_t e = hipMemsetAsync(dw, 0, 32 * 27 * sizeof(float), s);
-    return e != hipSuccess ? e : hipMemsetAsync(db, 0, 32 * sizeof(float), s);
+    hipError_t e = hipMemsetAsync(dw, 0, 32 * 27 * sizeof(float), s);
+    if (e == hipSuccess) e = hipMemsetAsync(db, 0, 32 * sizeof(float), s);
+    if (e != hipSuccess || !advance) return e;
+    hipLaunchKernelGGL(k_stem_reduce, dim3(1), dim3(64), 0, s, partial, 0, dw, db,
+                       reinterpret_cast<unsigned long long*>(advance));
+    return hipGetLastError();
   }
   const float scale = drop_p > 0.0f ? (float)(1.0 / (1.0 - (double)drop_p)) : 1.0f;
   hipLaunchKernelGGL(k_stem_bwd, dim3(chunks, 32), dim3(256), 0, s, bits, code, g, ld, n, scale,
                      partial);
   hipLaunchKernelGGL(k_stem_reduce, dim3((32 * NACC + 255) / 256), dim3(256), 0, s, partial,
-                     chunks, dw, db);
+                     chunks, dw, db, reinterpret_cast<unsigned long long*>(advance));
   return hipGetLastError();
 }

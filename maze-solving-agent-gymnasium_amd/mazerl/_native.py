@@ -42,7 +42,7 @@ EXPORTS = ["mz_last_error", "mz_device_count", "mz_create", "mz_destroy", "mz_lo
            "mz_bank_slot_grid", "mz_generate_best", "mz_select_stats", "mz_select_stats_ex",
            "mz_set_debug", "mz_screen_batch", "mz_set_regen_dims",
            "mz_bank_consumed", "mz_state_bytes", "mz_state_save", "mz_state_load",
-           "mz_stem_forward", "mz_stem_backward", "mz_stem_workspace_floats", "mz_adamw_flat",
+           "mz_stem_forward", "mz_stem_backward", "mz_stem_backward_ex", "mz_stem_workspace_floats", "mz_adamw_flat",
            "mz_pair_surrogate", "mz_leaky_relu_bf16", "mz_colsum_f32",
            "mz_replay_gather", "mz_host_alloc", "mz_host_free", "mz_q_front_rows", "mz_greedy_rows",
            "mz_trainer_tick", "mz_greedy_scatter", "mz_head_bf16", "mz_replay_push",
@@ -146,6 +146,9 @@ def load(build_if_missing=True):
     L.mz_stem_forward.argtypes = [vp, vp, C.c_int32, vp, vp, C.c_float, vp, C.c_uint32, vp,
                                   C.c_int32, vp, vp]
     L.mz_stem_backward.argtypes = [vp, vp, vp, C.c_int32, C.c_int32, C.c_float, vp, vp, vp, vp]
+    if hasattr(L, "mz_stem_backward_ex"):
+        L.mz_stem_backward_ex.argtypes = [vp, vp, vp, C.c_int32, C.c_int32, C.c_float, vp, vp, vp,
+                                          vp, vp]
     L.mz_stem_workspace_floats.argtypes = [C.c_int32]
     L.mz_qact_workspace_floats.argtypes = [C.c_int32]
     L.mz_leaky_relu_bf16.argtypes = [vp, C.c_int64, C.c_float, vp]

@@ -385,6 +385,15 @@ class VectorDQNLearner:
         self.source = QNet(3, 6, 4, h_channels, hidden_dim, variant).to(self.device)
         self.target = QNet(3, 6, 4, h_channels, hidden_dim, variant).to(self.device)
         self.target.load_state_dict(self.source.state_dict())
+        if variant == "ddqn" and self.device.type == "cuda" and bit_stem and \
+                os.environ.get("MZ_STEM_COUNTER_FOLD", "1") != "0":
+            # one dropout counter for both nets' HIP stems: read by source(s, s') and target(s')
+            # in an update, moved on by the source stem's backward (agents/stem.py) — the keys
+            # each net draws are the 0, 1, 2, ... per update they were with an add per forward,
+            # without the two add launches
+            ctr = torch.zeros(1, dtype=torch.int64, device=self.device)
+            self.source._stem_rng, self.target._stem_rng = ctr, ctr
+            self.source._stem_advance, self.target._stem_advance = "backward", "none"
         # One update (sample -> expand -> loss -> backward -> clamp -> AdamW) is ~150 small
         # kernels: it is captured once into a HIP graph and replayed (capturable AdamW with a
         # device-side lr, so the cosine schedule still applies). With a gradient all-reduce

@@ -32,6 +32,7 @@ class QNet(nn.Module):
         QNet._count += 1
         self._salt = QNet._count
         self._stem_rng = None
+        self._stem_advance = "add"  # how the stem's dropout counter moves on (agents/stem.py)
         self.in_channels = in_channels
         self.variant = variant
         conv = [nn.Conv2d(in_channels, h_channels, kernel_size=3, stride=1, padding=1), nn.LeakyReLU()]
@@ -109,7 +110,8 @@ class QNet(nn.Module):
                     p = float(m.p)
         if p > 0 and (self._stem_rng is None or self._stem_rng.device != bits.device):
             self._stem_rng = torch.zeros(1, dtype=torch.int64, device=bits.device)
-        return stem_features(bits, s, self.conv[0], p, self._stem_rng, self._salt, n_grad)
+        return stem_features(bits, s, self.conv[0], p, self._stem_rng, self._salt, n_grad,
+                             self._stem_advance)
 
 
 def count_params(net):

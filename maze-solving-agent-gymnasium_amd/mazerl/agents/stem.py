@@ -13,7 +13,10 @@ replay's storage, DeviceReplay.sw) on the GPU runs this instead of Conv2d -> Lea
 
 Dropout (DDQN, train mode: SURVEY Q13) draws its masks from a counter hash keyed by a device-side
 u64 that is advanced after every call (an in-graph add), so a captured HIP graph replays fresh
-masks; P(drop) = round(p * 65536) / 65536. Same f32 arithmetic as the torch stem element by
+masks; P(drop) = round(p * 65536) / 65536. `advance`: "add" (that add), "backward" (the stem's
+backward advances the counter instead — one launch fewer per forward; the learner shares one
+counter between its source and target nets and moves it on from the source's backward, so each
+net's key sequence is the same 0, 1, 2, ... per update as with an add per forward) or "none". Same f32 arithmetic as the torch stem element by
 element; the conv and weight-gradient sums associate differently (f32 tolerance).
 """
 import torch
@@ -26,7 +29,7 @@ IN_DIM = FEAT + 6
 
 class _StemFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, bits, obs6, weight, bias, p, rng, salt, n_grad=None):
+    def forward(ctx, bits, obs6, weight, bias, p, rng, salt, n_grad=None, advance=None):
         n = bits.shape[0]
         L = N.load()
         feat = torch.empty(n, IN_DIM, dtype=torch.float32, device=bits.device)
@@ -42,6 +45,7 @@ class _StemFn(torch.autograd.Function):
         ctx.p = float(p)
         ctx.n_grad = n if n_grad is None else max(0, min(int(n_grad), n))
         ctx.wp, ctx.bp = weight, bias  # flat gradient segments (agents/flat.py), if any
+        ctx.advance = advance  # the dropout counter the backward advances (None: none)
         return feat
 
     @staticmethod
@@ -61,13 +65,21 @@ class _StemFn(torch.autograd.Function):
             dw = torch.empty(32, 3, 3, 3, dtype=torch.float32, device=dev)
             db = torch.empty(32, dtype=torch.float32, device=dev)
         st = torch.cuda.current_stream(dev).cuda_stream
-        N.check(L.mz_stem_backward(bits.data_ptr(), code.data_ptr(), gfeat.data_ptr(), IN_DIM, n,
-                                   ctx.p, ws.data_ptr(), dw.data_ptr(), db.data_ptr(), st))
-        return None, None, dw, db, None, None, None, None
+        adv = ctx.advance
+        ctx.advance = None
+        if adv is not None:
+            N.check(L.mz_stem_backward_ex(bits.data_ptr(), code.data_ptr(), gfeat.data_ptr(), IN_DIM,
+                                          n, ctx.p, ws.data_ptr(), dw.data_ptr(), db.data_ptr(),
+                                          adv.data_ptr(), st))
+        else:
+            N.check(L.mz_stem_backward(bits.data_ptr(), code.data_ptr(), gfeat.data_ptr(), IN_DIM,
+                                       n, ctx.p, ws.data_ptr(), dw.data_ptr(), db.data_ptr(), st))
+        return None, None, dw, db, None, None, None, None, None
 
 
-def stem_features(bits, obs6, conv, p, rng, salt, n_grad=None):
-    """fc.0 input [n, 1574] f32 from packed windows; `conv` is the stem's nn.Conv2d(3, 32, 3)."""
+def stem_features(bits, obs6, conv, p, rng, salt, n_grad=None, advance="add"):
+    """fc.0 input [n, 1574] f32 from packed windows; `conv` is the stem's nn.Conv2d(3, 32, 3).
+    advance: how the dropout counter `rng` moves on (module docstring)."""
     if conv.weight.shape != (32, 3, 3, 3) or conv.bias is None:
         raise ValueError("the bit stem implements Conv2d(3, 32, 3, padding=1) with bias")
     if not bits.is_cuda:
@@ -75,7 +87,10 @@ def stem_features(bits, obs6, conv, p, rng, salt, n_grad=None):
     bits = bits.contiguous()
     obs6 = obs6.contiguous().float()
     w = conv.weight.contiguous()
-    feat = _StemFn.apply(bits, obs6, w, conv.bias, p, rng, salt, n_grad)
-    if p > 0:
+    by_backward = (advance == "backward" and p > 0 and torch.is_grad_enabled()
+                   and (w.requires_grad or conv.bias.requires_grad))
+    feat = _StemFn.apply(bits, obs6, w, conv.bias, p, rng, salt, n_grad,
+                         rng if by_backward else None)
+    if p > 0 and (advance == "add" or (advance == "backward" and not by_backward)):
         rng.add_(1)  # next call (or graph replay) draws new masks
     return feat

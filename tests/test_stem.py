@@ -182,3 +182,48 @@ def test_learner_bit_stem_tracks_f32_stem():
     for (name, pa), pb in zip(A.source.named_parameters(), B.source.parameters()):
         assert float((pa - pb).abs().max()) <= 8 * 1e-3 + 1e-6, name
     env.close()
+
+
+@pytest.mark.parametrize("overlap", [False, True], ids=["sequential", "overlapped"])
+def test_learner_counter_advanced_by_backward_draws_the_same_masks(overlap):
+    """VectorDQNLearner (DDQN, packed windows) gives its two nets ONE dropout counter and moves it
+    on from the source stem's backward (mz_stem_backward_ex; no add launch per forward). Each net
+    still draws keys 0, 1, 2, ... per update, as with its own counter advanced after every
+    forward — so, dropout active, the same weights bit for bit over eager and graph-captured
+    updates."""
+    from mazerl import VectorMazeEnv
+    from mazerl.agents.dqn import VectorDQNLearner
+    from test_learner_graph import _fill
+    env = VectorMazeEnv(4, 21, enrich=True, device="cuda", seed=1)
+    mk = lambda: VectorDQNLearner(4, "cuda", variant="ddqn", batch_size=64, capacity=256,  # noqa: E731
+                                  updates_per_step=1, target_every=4, updates_per_epoch=2, seed=5,
+                                  use_graph=True, overlap=overlap)
+    A, B = mk(), mk()
+    assert A.source._stem_rng is A.target._stem_rng
+    assert (A.source._stem_advance, A.target._stem_advance) == ("backward", "none")
+    # B: the per-forward scheme — a counter per net, an add after every forward
+    for ma, mb in ((A.source, B.source), (A.target, B.target)):
+        mb._stem_rng = torch.zeros(1, dtype=torch.int64, device="cuda")
+        mb._stem_advance = "add"
+        mb._salt = ma._salt  # the construction-order salts (before any capture bakes them in)
+        mb.load_state_dict(ma.state_dict())
+    assert A.source.training and A.target.training  # Dropout(0.2) active (SURVEY Q13)
+    for L in (A, B):
+        for k in range(4):
+            _fill(L, n=64, seed=k)
+    n = 10
+    # one learner after the other, each from the same CUDA generator state: the sequential graph
+    # learner samples its rows from the default generator, so interleaved updates would draw
+    # different rows
+    for L in (A, B):
+        torch.cuda.manual_seed(123)
+        for _ in range(n):
+            L.update(env.expand_window, reserve=0)
+        if overlap:
+            L.finish()
+        torch.cuda.synchronize()
+    assert int(A.source._stem_rng.item()) == n
+    assert int(B.source._stem_rng.item()) == n and int(B.target._stem_rng.item()) == n
+    for pa, pb in zip(A.source.parameters(), B.source.parameters()):
+        assert torch.equal(pa, pb)
+    env.close()
